@@ -1,0 +1,196 @@
+/*
+ * super_rag_mi355x.h — C-ABI of the MI355X (gfx950) embed -> retrieve -> rerank hot path.
+ *
+ * This library replaces the arithmetic that promoteAI/super-rag sends out of process:
+ *   - the SeekDB HNSW cosine search behind
+ *       super_rag/vectorstore/seekdb_connector.py:98-115  (SeekDBVectorStoreConnector.search)
+ *       super_rag/vectorstore/seekdb_connector.py:56-96   (create_collection / add / delete)
+ *     -> sr_store_*  (in-HBM exact cosine top-k, fp16 rows, MFMA scan + fused threshold filter)
+ *   - the remote embedding server reached by litellm.embedding() at
+ *       super_rag/llm/embed/embedding_service.py:153-194  (EmbeddingService._embed_batch)
+ *     -> sr_encoder_forward*  (BERT / XLM-R encoder, CLS or masked-mean pool, L2 normalise)
+ *   - the remote cross-encoder reached by litellm.arerank() at
+ *       super_rag/llm/rerank/rerank_service.py:87-153    (RerankService._rank_texts)
+ *     -> sr_cross_score*  (XLM-R encoder + RoBERTa classification head -> one logit per pair)
+ *
+ * Conventions
+ *   - Every int-returning entry point returns SR_OK (0) on success and a negative SR_ERR_* code on
+ *     failure; the message is available from sr_last_error() (thread-local, valid until the next
+ *     call on the same thread).
+ *   - Host pointers are caller-owned and only read/written during the call.  Device pointers
+ *     (the *_dev entry points) must live on the object's device; `stream` is a hipStream_t
+ *     (NULL = the object's own stream) and the call is asynchronous on it unless stated.
+ *   - Objects are internally locked: every entry point is safe to call from several host threads.
+ *     The Python binding calls through ctypes.CDLL, which releases the GIL for the duration.
+ *   - Scores follow SeekDB's cosine semantics: dist = 1 - cos(q, x)  (lower is better,
+ *     seekdb_connector.py:143 passes the distance through as DocumentWithScore.score).
+ *     Ties are broken by ascending row id.  Missing results (k > live rows) are reported as
+ *     row = -1, dist = +inf.
+ */
+#ifndef SUPER_RAG_MI355X_H
+#define SUPER_RAG_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#pragma GCC visibility push(default)
+#endif
+
+#define SR_OK 0
+#define SR_ERR_INVALID (-1)   /* bad argument / shape                                   */
+#define SR_ERR_HIP (-2)       /* HIP runtime or kernel launch failure                    */
+#define SR_ERR_OOM (-3)       /* device allocation failed                                */
+#define SR_ERR_IO (-4)        /* snapshot read/write failure                             */
+#define SR_ERR_STATE (-5)     /* object not ready (e.g. encoder weights missing)         */
+
+#define SR_DTYPE_F32 0
+#define SR_DTYPE_F16 1
+
+#define SR_POOL_CLS 0         /* BGE models: hidden state of the first token             */
+#define SR_POOL_MEAN 1        /* attention-mask weighted mean over tokens                */
+
+#define SR_MAX_TOPK 1024
+
+typedef struct sr_store sr_store;
+typedef struct sr_encoder sr_encoder;
+
+const char* sr_last_error(void);
+int sr_version(void);
+/* Number of visible HIP devices (0 on a host without a GPU; never fails on such a host). */
+int sr_device_count(int* out);
+/* Copy `bytes` between host and device memory of `device` (kind: 0 = H2D, 1 = D2H, 2 = D2D). */
+int sr_memcpy(void* dst, const void* src, int64_t bytes, int kind, int device);
+
+/* ------------------------------------------------------------------------------------------------
+ * Vector store  (replaces SeekDBVectorStoreConnector, seekdb_connector.py:31-155)
+ * Rows are L2-normalised on insertion and kept as fp16 in HBM, row-major, dim padded to 64.
+ * ---------------------------------------------------------------------------------------------- */
+
+/* create_collection(vector_size=dim) — seekdb_connector.py:56-66 (HNSW, distance="cosine"). */
+int sr_store_create(int dim, int device, int64_t initial_capacity, sr_store** out);
+/* add(nodes) — seekdb_connector.py:68-85: n host fp32 rows (n x dim); out_rows[i] = row id. */
+int sr_store_add(sr_store* s, const float* vecs, int64_t n, int64_t* out_rows);
+/* Same, rows already on the device (dtype SR_DTYPE_F32 or SR_DTYPE_F16, n x dim, row-major).
+ * Row ids are first_row .. first_row + n - 1. */
+int sr_store_add_dev(sr_store* s, const void* vecs, int dtype, int64_t n, int64_t* first_row,
+                     void* stream);
+/* delete(ids=...) — seekdb_connector.py:90-96: tombstones rows (ignored ids are an error). */
+int sr_store_remove(sr_store* s, const int64_t* rows, int64_t n);
+int sr_store_count(sr_store* s, int64_t* n_rows, int64_t* n_live);
+int sr_store_dim(sr_store* s, int* dim);
+/* Read back stored (normalised, fp16-rounded) rows as fp32, for with_vectors / parity checks. */
+int sr_store_get(sr_store* s, const int64_t* rows, int64_t n, float* out);
+/* search(QueryWithEmbedding) — seekdb_connector.py:98-115 (collection.query n_results=top_k).
+ * q: B x dim host fp32 (normalised internally).  out_dist / out_rows: B x k host buffers, each
+ * query's results sorted by (dist asc, row asc).  Blocking. */
+int sr_store_search(sr_store* s, const float* q, int B, int k, float* out_dist, int64_t* out_rows);
+/* Device variant: q is B x dim on the device (SR_DTYPE_F32 or SR_DTYPE_F16), out_sim/out_rows
+ * device buffers of B x k (similarity = 1 - dist, rows int64; -1 / -inf when missing).
+ * row_offset is added to every returned row (global row id of a shard).  Synchronises `stream`
+ * once at the end to check the candidate-overflow flag (and reruns the exact slow path if set). */
+int sr_store_search_dev(sr_store* s, const void* q, int q_dtype, int B, int k, float* out_sim,
+                        int64_t* out_rows, int64_t row_offset, void* stream);
+/* Snapshot (checkpoint/resume of the corpus; SeekDB persisted rows server-side). */
+int sr_store_save(sr_store* s, const char* path);
+int sr_store_load(const char* path, int device, sr_store** out);
+/* Drop tombstoned rows; old_to_new (host, n_rows entries, may be NULL) receives the new row id
+ * of every old row (-1 for removed rows). */
+int sr_store_compact(sr_store* s, int64_t* old_to_new);
+void sr_store_destroy(sr_store* s);
+
+/* Merge P per-shard top-k lists (device buffers P x B x k of similarity and global row, as written
+ * by sr_store_search_dev) into one B x k_out list per query, on `device`. */
+int sr_topk_merge_dev(const float* sims, const int64_t* rows, int P, int B, int k, int k_out,
+                      float* out_sim, int64_t* out_rows, int device, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Transformer encoder (BERT / XLM-R family: bge-small/base-en, bge-m3, bge-reranker-*)
+ * Weights are set by Hugging Face tensor name without the model prefix, e.g.
+ * "embeddings.word_embeddings.weight", "encoder.layer.3.attention.self.query.weight",
+ * "classifier.dense.weight", "classifier.out_proj.bias".  Matrices are stored fp16 in HBM,
+ * biases / LayerNorm parameters fp32.  Activations are fp16 GEMM operands with an fp32
+ * residual stream; accumulation is fp32 everywhere.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct sr_encoder_config {
+  int vocab_size;
+  int hidden;           /* d                                         */
+  int layers;           /* L                                         */
+  int heads;            /* d / heads must be 32 or 64               */
+  int intermediate;     /* FFN width                                 */
+  int max_position;
+  int type_vocab;       /* token-type rows (1 for XLM-R, 2 for BERT) */
+  float ln_eps;         /* 1e-12 BERT, 1e-5 XLM-R                    */
+  int position_offset;  /* 0: BERT (pos = index); >0: XLM-R padding_idx (pos = cumsum(mask)+pad) */
+  int classifier;       /* 0: none; 1: RoBERTa classification head (dense+tanh+out_proj)       */
+  int num_labels;       /* classifier outputs (1 for bge-reranker)                             */
+  int max_tokens;       /* workspace size in tokens per launch chunk (0 = default 262144)      */
+} sr_encoder_config;
+
+int sr_encoder_create(const sr_encoder_config* cfg, int device, sr_encoder** out);
+int sr_encoder_set_weight(sr_encoder* e, const char* name, const float* data, int64_t numel);
+/* Returns SR_OK when every weight has been set, SR_ERR_STATE (message lists a missing one) else. */
+int sr_encoder_ready(sr_encoder* e);
+/* Sentence embeddings: ids/mask/type_ids are B x S int32 host arrays (type_ids may be NULL);
+ * out: B x hidden fp32, L2-normalised (EmbeddingService.embed_documents result rows). Blocking. */
+int sr_encoder_forward(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                       const int32_t* type_ids, int B, int S, int pool, float* out);
+/* Device variant; out dtype SR_DTYPE_F32 (B x hidden) or SR_DTYPE_F16 (B x ld_out, row-major,
+ * ld_out >= hidden, zero-padded to ld_out so it can be fed to sr_store_search_dev). */
+int sr_encoder_forward_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                           const int32_t* type_ids, int B, int S, int pool, void* out,
+                           int out_dtype, int ld_out, void* stream);
+/* Cross-encoder relevance: P (query, passage) pairs already packed as token ids (P x S);
+ * out_logits: P x num_labels fp32 raw logits (bge-reranker scores = logits, sigmoid optional). */
+int sr_cross_score(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                   const int32_t* type_ids, int P, int S, float* out_logits);
+int sr_cross_score_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                       const int32_t* type_ids, int P, int S, float* out_logits, void* stream);
+void sr_encoder_destroy(sr_encoder* e);
+
+/* ------------------------------------------------------------------------------------------------
+ * Device pipeline helpers for the batched search path (embed -> top-K -> pairs -> rerank)
+ * ---------------------------------------------------------------------------------------------- */
+/* Pack cross-encoder inputs for every (query b, candidate j):
+ *   style 0 (RoBERTa/XLM-R):  <s> q </s> </s> p </s>      style 1 (BERT): [CLS] q [SEP] p [SEP]
+ * q_tok: B x lq_max content tokens (no specials), q_len: B;  p_tok: N x lp_max, p_len: N;
+ * cand_rows: B x K (int64; rows < 0 give an all-padding pair).  The passage is truncated first,
+ * then the query.  out_ids / out_mask / out_type: (B*K) x S int32 (out_type may be NULL). */
+int sr_build_pairs_dev(const int32_t* q_tok, const int32_t* q_len, int lq_max,
+                       const int32_t* p_tok, const int32_t* p_len, int lp_max,
+                       const int64_t* cand_rows, int B, int K, int S, int style,
+                       int bos_id, int eos_id, int pad_id,
+                       int32_t* out_ids, int32_t* out_mask, int32_t* out_type,
+                       int device, void* stream);
+/* Per query: order the K candidates by (logit desc, candidate index asc) and keep k_out.
+ * logits: B x K fp32; out_index: B x k_out int32 positions into the candidate list. */
+int sr_rerank_select_dev(const float* logits, int B, int K, int k_out, int32_t* out_index,
+                         int device, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Profiling: per-kernel HIP-event timing of every launch on the library's streams.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct sr_kernel_stat {
+  char name[64];        /* kernel family, e.g. "gemm_f16_gelu", "cosine_scan"              */
+  int64_t launches;
+  double total_ms;      /* sum of HIP-event durations                                        */
+  double flops;         /* algorithmic FLOPs over all launches                               */
+  double bytes;         /* algorithmic HBM bytes over all launches                           */
+} sr_kernel_stat;
+
+int sr_profile_enable(int on);              /* clears the table when turned on                  */
+/* Fills up to max entries (synchronises the recorded events); *n receives the number written. */
+int sr_profile_read(sr_kernel_stat* out, int max, int* n);
+
+#if defined(__GNUC__) || defined(__clang__)
+#pragma GCC visibility pop
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SUPER_RAG_MI355X_H */

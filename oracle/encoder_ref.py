@@ -1,0 +1,137 @@
+"""fp32 CPU restatement of the BERT / XLM-R encoders (TEST INFRASTRUCTURE ONLY — see oracle/__init__.py).
+
+The reference sends text to remote servers running BAAI/bge-* (embedding, litellm.embedding at
+super_rag/llm/embed/embedding_service.py:168-175) and BAAI/bge-reranker-* (cross-encoder,
+litellm.arerank at super_rag/llm/rerank/rerank_service.py:95-104).  Those models are public
+architectures outside the reference:
+  * BERT (bge-small/base/large-en): post-LN encoder, absolute positions 0..S-1, token types.
+  * XLM-R (bge-m3, bge-reranker-*): same block, positions padding_idx + cumsum(ids != pad),
+    classification head dense -> tanh -> out_proj on the first token.
+  * Sentence embedding = CLS pooling (BGE model cards) or masked mean, then L2 normalisation.
+This module is pinned to ``transformers`` on identical weights in tests/test_oracle.py.
+Weights use Hugging Face names without the model prefix ("embeddings.word_embeddings.weight", ...).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+
+@dataclass
+class RefConfig:
+    vocab_size: int
+    hidden: int
+    layers: int
+    heads: int
+    intermediate: int
+    max_position: int
+    type_vocab: int
+    ln_eps: float
+    position_offset: int = 0      # XLM-R: padding_idx (1); BERT: 0
+    classifier: int = 0
+    num_labels: int = 1
+
+
+def position_ids(ids: torch.Tensor, offset: int) -> torch.Tensor:
+    if offset == 0:
+        return torch.arange(ids.shape[1]).unsqueeze(0).expand_as(ids)
+    m = (ids != offset).long()
+    return torch.cumsum(m, dim=1) * m + offset
+
+
+def _ln(x, w, b, eps):
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+def _t(w, name):
+    v = w[name]
+    return v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v), dtype=torch.float32)
+
+
+@torch.no_grad()
+def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None) -> torch.Tensor:
+    """Final hidden states [B, S, d] in fp32."""
+    ids = torch.as_tensor(np.asarray(ids), dtype=torch.long)
+    mask = torch.as_tensor(np.asarray(mask), dtype=torch.float32)
+    B, S = ids.shape
+    tt = torch.zeros_like(ids) if type_ids is None else torch.as_tensor(np.asarray(type_ids), dtype=torch.long)
+    pos = position_ids(ids, cfg.position_offset)
+    x = (_t(w, "embeddings.word_embeddings.weight")[ids]
+         + _t(w, "embeddings.position_embeddings.weight")[pos]
+         + _t(w, "embeddings.token_type_embeddings.weight")[tt])
+    h = _ln(x, _t(w, "embeddings.LayerNorm.weight"), _t(w, "embeddings.LayerNorm.bias"), cfg.ln_eps)
+    d, H = cfg.hidden, cfg.heads
+    dh = d // H
+    bias = (1.0 - mask)[:, None, None, :] * torch.finfo(torch.float32).min
+    for l in range(cfg.layers):
+        p = f"encoder.layer.{l}."
+        def lin(x, n):
+            return x @ _t(w, p + n + ".weight").T + _t(w, p + n + ".bias")
+        q = lin(h, "attention.self.query").view(B, S, H, dh).transpose(1, 2)
+        k = lin(h, "attention.self.key").view(B, S, H, dh).transpose(1, 2)
+        v = lin(h, "attention.self.value").view(B, S, H, dh).transpose(1, 2)
+        s = q @ k.transpose(-1, -2) / math.sqrt(dh) + bias
+        ctx = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, S, d)
+        h = _ln(lin(ctx, "attention.output.dense") + h, _t(w, p + "attention.output.LayerNorm.weight"),
+                _t(w, p + "attention.output.LayerNorm.bias"), cfg.ln_eps)
+        f = torch.nn.functional.gelu(lin(h, "intermediate.dense"))
+        h = _ln(lin(f, "output.dense") + h, _t(w, p + "output.LayerNorm.weight"),
+                _t(w, p + "output.LayerNorm.bias"), cfg.ln_eps)
+    return h
+
+
+@torch.no_grad()
+def embed(cfg: RefConfig, w: dict, ids, mask, type_ids=None, pool: str = "cls") -> np.ndarray:
+    """Sentence embeddings [B, d], pooled then L2-normalised (fp32)."""
+    h = encode_hidden(cfg, w, ids, mask, type_ids)
+    m = torch.as_tensor(np.asarray(mask), dtype=torch.float32)
+    if pool == "cls":
+        e = h[:, 0]
+    else:
+        e = (h * m[..., None]).sum(1) / m.sum(1, keepdim=True).clamp_min(1e-30)
+    n = e.norm(dim=-1, keepdim=True)
+    e = torch.where(n > 0, e / n, torch.zeros_like(e))
+    return e.numpy()
+
+
+@torch.no_grad()
+def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None) -> np.ndarray:
+    """RoBERTa classification head on the first token: [P, num_labels] raw logits."""
+    h = encode_hidden(cfg, w, ids, mask, type_ids)[:, 0]
+    t = torch.tanh(h @ _t(w, "classifier.dense.weight").T + _t(w, "classifier.dense.bias"))
+    return (t @ _t(w, "classifier.out_proj.weight").T + _t(w, "classifier.out_proj.bias")).numpy()
+
+
+def pack_pairs(q_tok, q_len, p_tok, p_len, rows, S, style, bos, eos, pad):
+    """Reference packing of (query, passage) pairs — HF tokenizer pair layout with 'longest_first'
+    truncation (FlagEmbedding's reranker calls tokenizer(pairs, truncation=True)).
+    style 0: <s> q </s></s> p </s>;  style 1: [CLS] q [SEP] p [SEP] (token type 1 on the passage)."""
+    B, K = rows.shape
+    ids = np.full((B * K, S), pad, dtype=np.int32)
+    msk = np.zeros((B * K, S), dtype=np.int32)
+    typ = np.zeros((B * K, S), dtype=np.int32)
+    nspec = 4 if style == 0 else 3
+    for b in range(B):
+        for j in range(K):
+            r = int(rows[b, j])
+            q = list(q_tok[b][: q_len[b]])
+            p = list(p_tok[r][: p_len[r]]) if r >= 0 else []
+            while len(q) + len(p) > S - nspec:
+                if len(q) > len(p):
+                    q.pop()
+                else:
+                    p.pop()
+            if style == 0:
+                seq = [bos] + q + [eos, eos] + p + [eos]
+                tps = [0] * len(seq)
+            else:
+                seq = [bos] + q + [eos] + p + [eos]
+                tps = [0] * (len(q) + 2) + [1] * (len(p) + 1)
+            i = b * K + j
+            ids[i, : len(seq)] = seq
+            msk[i, : len(seq)] = 1
+            typ[i, : len(seq)] = tps
+    return ids, msk, typ

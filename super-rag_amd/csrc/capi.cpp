@@ -1,0 +1,434 @@
+// C-ABI entry points (include/super_rag_mi355x.h): argument checks, exception -> error-code
+// mapping, per-object locking, and the HIP-event profiler.
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "sr_kernels.h"
+#include "sr_runtime.h"
+
+struct sr_store {
+  sr::Store* impl;
+};
+struct sr_encoder {
+  sr::Encoder* impl;
+};
+
+namespace sr {
+
+static thread_local std::string t_last_error;
+void set_last_error(const std::string& msg) { t_last_error = msg; }
+
+// ---- profiler --------------------------------------------------------------------------------
+namespace {
+struct ProfRecord {
+  std::string name;
+  hipEvent_t ev0, ev1;
+  double flops, bytes;
+};
+struct ProfAgg {
+  int64_t launches = 0;
+  double ms = 0, flops = 0, bytes = 0;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRecord> g_prof_pending;
+std::vector<hipEvent_t> g_event_pool;
+std::map<std::string, ProfAgg> g_prof_agg;
+
+hipEvent_t take_event() {
+  if (!g_event_pool.empty()) {
+    hipEvent_t e = g_event_pool.back();
+    g_event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  SR_HIP(hipEventCreate(&e));
+  return e;
+}
+
+void drain_pending_locked() {
+  for (auto& r : g_prof_pending) {
+    (void)hipEventSynchronize(r.ev1);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.ev0, r.ev1) == hipSuccess) {
+      ProfAgg& a = g_prof_agg[r.name];
+      a.launches += 1;
+      a.ms += ms;
+      a.flops += r.flops;
+      a.bytes += r.bytes;
+    }
+    g_event_pool.push_back(r.ev0);
+    g_event_pool.push_back(r.ev1);
+  }
+  g_prof_pending.clear();
+}
+}  // namespace
+
+ProfScope::ProfScope(const char* n, hipStream_t s, double f, double b)
+    : name(n), flops(f), bytes(b), stream(s) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (!g_prof_on) return;
+  ev0 = take_event();
+  ev1 = take_event();
+  if (hipEventRecord(ev0, stream) != hipSuccess) {
+    g_event_pool.push_back(ev0);
+    g_event_pool.push_back(ev1);
+    ev0 = ev1 = nullptr;
+  }
+}
+
+ProfScope::~ProfScope() {
+  if (!ev0) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (hipEventRecord(ev1, stream) == hipSuccess) {
+    g_prof_pending.push_back(ProfRecord{name, ev0, ev1, flops, bytes});
+    if (g_prof_pending.size() > 65536) drain_pending_locked();
+  } else {
+    g_event_pool.push_back(ev0);
+    g_event_pool.push_back(ev1);
+  }
+}
+
+}  // namespace sr
+
+#define SR_API_BEGIN try {
+#define SR_API_END                           \
+  return SR_OK;                              \
+  }                                          \
+  catch (const sr::Error& e) {               \
+    sr::set_last_error(e.what());            \
+    return e.code;                           \
+  }                                          \
+  catch (const std::bad_alloc&) {            \
+    sr::set_last_error("host out of memory"); \
+    return SR_ERR_OOM;                       \
+  }                                          \
+  catch (const std::exception& e) {          \
+    sr::set_last_error(e.what());            \
+    return SR_ERR_INVALID;                   \
+  }
+
+#define SR_NONNULL(p)                                                   \
+  do {                                                                  \
+    if (!(p)) throw sr::Error(SR_ERR_INVALID, "null argument: " #p);    \
+  } while (0)
+
+extern "C" {
+
+const char* sr_last_error(void) { return sr::t_last_error.c_str(); }
+int sr_version(void) { return 100; }
+
+int sr_device_count(int* out) {
+  SR_API_BEGIN
+  SR_NONNULL(out);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *out = n;
+  SR_API_END
+}
+
+int sr_memcpy(void* dst, const void* src, int64_t bytes, int kind, int device) {
+  SR_API_BEGIN
+  SR_NONNULL(dst);
+  SR_NONNULL(src);
+  sr::DeviceGuard g(device);
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                          : kind == 1 ? hipMemcpyDeviceToHost
+                                      : hipMemcpyDeviceToDevice;
+  SR_HIP(hipMemcpy(dst, src, (size_t)bytes, k));
+  SR_API_END
+}
+
+// ---- store -----------------------------------------------------------------------------------
+int sr_store_create(int dim, int device, int64_t initial_capacity, sr_store** out) {
+  SR_API_BEGIN
+  SR_NONNULL(out);
+  *out = nullptr;
+  auto* s = new sr_store{new sr::Store(dim, device, initial_capacity)};
+  *out = s;
+  SR_API_END
+}
+
+int sr_store_add(sr_store* s, const float* vecs, int64_t n, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->add_host(vecs, n, out_rows);
+  SR_API_END
+}
+
+int sr_store_add_dev(sr_store* s, const void* vecs, int dtype, int64_t n, int64_t* first_row,
+                     void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  SR_NONNULL(vecs);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  const int64_t first = s->impl->add_dev(vecs, dtype, n, reinterpret_cast<hipStream_t>(stream));
+  if (first_row) *first_row = first;
+  SR_API_END
+}
+
+int sr_store_remove(sr_store* s, const int64_t* rows, int64_t n) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->remove(rows, n);
+  SR_API_END
+}
+
+int sr_store_count(sr_store* s, int64_t* n_rows, int64_t* n_live) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  if (n_rows) *n_rows = s->impl->rows();
+  if (n_live) *n_live = s->impl->live();
+  SR_API_END
+}
+
+int sr_store_dim(sr_store* s, int* dim) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  SR_NONNULL(dim);
+  *dim = s->impl->dim();
+  SR_API_END
+}
+
+int sr_store_get(sr_store* s, const int64_t* rows, int64_t n, float* out) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  if (n > 0) {
+    SR_NONNULL(rows);
+    SR_NONNULL(out);
+  }
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->get(rows, n, out);
+  SR_API_END
+}
+
+int sr_store_search(sr_store* s, const float* q, int B, int k, float* out_dist, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->search_host(q, B, k, out_dist, out_rows);
+  SR_API_END
+}
+
+int sr_store_search_dev(sr_store* s, const void* q, int q_dtype, int B, int k, float* out_sim,
+                        int64_t* out_rows, int64_t row_offset, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  if (B > 0) {
+    SR_NONNULL(q);
+    SR_NONNULL(out_sim);
+    SR_NONNULL(out_rows);
+  }
+  SR_CHECK(q_dtype == SR_DTYPE_F32 || q_dtype == SR_DTYPE_F16, "search: q dtype must be f32/f16");
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->search_dev(q, q_dtype, B, k, out_sim, out_rows, row_offset,
+                      reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+int sr_store_save(sr_store* s, const char* path) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  SR_NONNULL(path);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->save(path);
+  SR_API_END
+}
+
+int sr_store_load(const char* path, int device, sr_store** out) {
+  SR_API_BEGIN
+  SR_NONNULL(path);
+  SR_NONNULL(out);
+  *out = nullptr;
+  sr::Store* st = sr::Store::load(path, device);
+  *out = new sr_store{st};
+  SR_API_END
+}
+
+int sr_store_compact(sr_store* s, int64_t* old_to_new) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->compact(old_to_new);
+  SR_API_END
+}
+
+void sr_store_destroy(sr_store* s) {
+  if (!s) return;
+  delete s->impl;
+  delete s;
+}
+
+int sr_topk_merge_dev(const float* sims, const int64_t* rows, int P, int B, int k, int k_out,
+                      float* out_sim, int64_t* out_rows, int device, void* stream) {
+  SR_API_BEGIN
+  SR_CHECK(P >= 1 && B >= 0 && k >= 1, "merge: bad shape");
+  if (B > 0) {
+    SR_NONNULL(sims);
+    SR_NONNULL(rows);
+    SR_NONNULL(out_sim);
+    SR_NONNULL(out_rows);
+  }
+  sr::DeviceGuard g(device);
+  sr::launch_topk_merge(sims, rows, P, B, k, k_out, out_sim, out_rows,
+                        reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+// ---- encoder ---------------------------------------------------------------------------------
+int sr_encoder_create(const sr_encoder_config* cfg, int device, sr_encoder** out) {
+  SR_API_BEGIN
+  SR_NONNULL(cfg);
+  SR_NONNULL(out);
+  *out = nullptr;
+  auto* e = new sr_encoder{new sr::Encoder(*cfg, device)};
+  *out = e;
+  SR_API_END
+}
+
+int sr_encoder_set_weight(sr_encoder* e, const char* name, const float* data, int64_t numel) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  SR_NONNULL(name);
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  e->impl->set_weight(name, data, numel);
+  SR_API_END
+}
+
+int sr_encoder_ready(sr_encoder* e) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  const std::string m = e->impl->missing();
+  if (!m.empty()) throw sr::Error(SR_ERR_STATE, "encoder: weight not set: " + m);
+  SR_API_END
+}
+
+int sr_encoder_forward(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                       const int32_t* type_ids, int B, int S, int pool, float* out) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  e->impl->forward_host(ids, mask, type_ids, B, S, 0, pool, out);
+  SR_API_END
+}
+
+int sr_encoder_forward_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                           const int32_t* type_ids, int B, int S, int pool, void* out,
+                           int out_dtype, int ld_out, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  if (B > 0) {
+    SR_NONNULL(ids);
+    SR_NONNULL(mask);
+    SR_NONNULL(out);
+  }
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  e->impl->forward_dev(ids, mask, type_ids, B, S, 0, pool, out, out_dtype, ld_out,
+                       reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+int sr_cross_score(sr_encoder* e, const int32_t* ids, const int32_t* mask, const int32_t* type_ids,
+                   int P, int S, float* out_logits) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  e->impl->forward_host(ids, mask, type_ids, P, S, 1, SR_POOL_CLS, out_logits);
+  SR_API_END
+}
+
+int sr_cross_score_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
+                       const int32_t* type_ids, int P, int S, float* out_logits, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  if (P > 0) {
+    SR_NONNULL(ids);
+    SR_NONNULL(mask);
+    SR_NONNULL(out_logits);
+  }
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  e->impl->forward_dev(ids, mask, type_ids, P, S, 1, SR_POOL_CLS, out_logits, SR_DTYPE_F32,
+                       e->impl->config().hidden, reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+void sr_encoder_destroy(sr_encoder* e) {
+  if (!e) return;
+  delete e->impl;
+  delete e;
+}
+
+// ---- pipeline helpers ------------------------------------------------------------------------
+int sr_build_pairs_dev(const int32_t* q_tok, const int32_t* q_len, int lq_max, const int32_t* p_tok,
+                       const int32_t* p_len, int lp_max, const int64_t* cand_rows, int B, int K,
+                       int S, int style, int bos_id, int eos_id, int pad_id, int32_t* out_ids,
+                       int32_t* out_mask, int32_t* out_type, int device, void* stream) {
+  SR_API_BEGIN
+  SR_CHECK(B >= 0 && K >= 1 && lq_max >= 1 && lp_max >= 1, "build_pairs: bad shape");
+  if (B > 0) {
+    SR_NONNULL(q_tok);
+    SR_NONNULL(q_len);
+    SR_NONNULL(p_tok);
+    SR_NONNULL(p_len);
+    SR_NONNULL(cand_rows);
+    SR_NONNULL(out_ids);
+    SR_NONNULL(out_mask);
+  }
+  sr::DeviceGuard g(device);
+  sr::launch_build_pairs(q_tok, q_len, lq_max, p_tok, p_len, lp_max, cand_rows, B, K, S, style,
+                         bos_id, eos_id, pad_id, out_ids, out_mask, out_type,
+                         reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+int sr_rerank_select_dev(const float* logits, int B, int K, int k_out, int32_t* out_index,
+                         int device, void* stream) {
+  SR_API_BEGIN
+  if (B > 0) {
+    SR_NONNULL(logits);
+    SR_NONNULL(out_index);
+  }
+  sr::DeviceGuard g(device);
+  sr::launch_rerank_select(logits, B, K, k_out, out_index, reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+// ---- profiling -------------------------------------------------------------------------------
+int sr_profile_enable(int on) {
+  SR_API_BEGIN
+  std::lock_guard<std::mutex> lk(sr::g_prof_mu);
+  if (on) {
+    sr::drain_pending_locked();
+    sr::g_prof_agg.clear();
+  }
+  sr::g_prof_on = on != 0;
+  SR_API_END
+}
+
+int sr_profile_read(sr_kernel_stat* out, int max, int* n) {
+  SR_API_BEGIN
+  SR_NONNULL(n);
+  std::lock_guard<std::mutex> lk(sr::g_prof_mu);
+  sr::drain_pending_locked();
+  int i = 0;
+  for (const auto& kv : sr::g_prof_agg) {
+    if (i >= max || !out) break;
+    sr_kernel_stat& st = out[i++];
+    std::memset(&st, 0, sizeof(st));
+    std::strncpy(st.name, kv.first.c_str(), sizeof(st.name) - 1);
+    st.launches = kv.second.launches;
+    st.total_ms = kv.second.ms;
+    st.flops = kv.second.flops;
+    st.bytes = kv.second.bytes;
+  }
+  *n = i;
+  SR_API_END
+}
+
+}  // extern "C"

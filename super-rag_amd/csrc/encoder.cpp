@@ -1,0 +1,223 @@
+// Transformer encoder runtime (BERT / XLM-R): replaces the remote embedding server reached through
+// litellm.embedding() (super_rag/llm/embed/embedding_service.py:168-175) and the remote
+// cross-encoder reached through litellm.arerank() (super_rag/llm/rerank/rerank_service.py:95-104).
+//
+// Per layer (post-LN BERT block), all on one HIP stream:
+//   qkv  = GEMM(h16, Wqkv) + bqkv                 fp16  [M, 3d]     (K4, bias epilogue)
+//   ctx  = MHA(qkv, mask)                         fp16  [M, d]      (K5)
+//   y32  = GEMM(ctx, Wo) + bo + h32               fp32  [M, d]      (K4, residual epilogue)
+//   h    = LayerNorm(y32)                         fp16 + fp32       (K6)
+//   f    = GELU(GEMM(h16, W1) + b1)               fp16  [M, F]      (K4, GELU epilogue)
+//   y32  = GEMM(f, W2) + b2 + h32                 fp32              (K4, residual epilogue)
+//   h    = LayerNorm(y32)                         fp16 + fp32       (K6)
+// The residual stream stays fp32 (fp16 residuals cost ~2x the embedding error).
+// Embedding mode pools (CLS / masked mean) and L2-normalises (K7); cross-encoder mode applies the
+// RoBERTa classification head: tanh(GEMM(h16[CLS rows], Wc) + bc) (fp32) . Wout + bout (K4 + K8).
+#include <algorithm>
+#include <vector>
+
+#include "sr_kernels.h"
+#include "sr_runtime.h"
+
+namespace sr {
+
+Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(device) {
+  const int d = cfg.hidden;
+  SR_CHECK(cfg.vocab_size > 0 && d > 0 && cfg.layers > 0 && cfg.heads > 0 &&
+               cfg.intermediate > 0 && cfg.max_position > 0 && cfg.type_vocab > 0,
+           "encoder: config fields must be positive");
+  SR_CHECK(d % cfg.heads == 0 && (d / cfg.heads == 64 || d / cfg.heads == 32),
+           "encoder: head dim must be 32 or 64");
+  SR_CHECK(d % 128 == 0 && cfg.intermediate % 128 == 0,
+           "encoder: hidden and intermediate must be multiples of 128");
+  SR_CHECK(d <= 2048, "encoder: hidden must be <= 2048");
+  SR_CHECK(cfg.classifier == 0 || (cfg.classifier == 1 && cfg.num_labels >= 1),
+           "encoder: classifier must be 0 or 1 (with num_labels >= 1)");
+  max_tokens_ = cfg.max_tokens > 0 ? cfg.max_tokens : 262144;
+  DeviceGuard g(device_);
+  SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+
+  const int64_t D = d, F = cfg.intermediate;
+  register_target("embeddings.word_embeddings.weight", wemb_, (int64_t)cfg.vocab_size * D, true);
+  register_target("embeddings.position_embeddings.weight", pemb_, (int64_t)cfg.max_position * D, true);
+  register_target("embeddings.token_type_embeddings.weight", temb_, (int64_t)cfg.type_vocab * D, true);
+  register_target("embeddings.LayerNorm.weight", embg_, D, false);
+  register_target("embeddings.LayerNorm.bias", embb_, D, false);
+  layers_.resize(cfg.layers);
+  for (int l = 0; l < cfg.layers; ++l) {
+    Layer& L = layers_[l];
+    const std::string p = "encoder.layer." + std::to_string(l) + ".";
+    register_target(p + "attention.self.query.weight", L.wqkv, D * D, true, 0, 3 * D * D);
+    register_target(p + "attention.self.key.weight", L.wqkv, D * D, true, D * D, 3 * D * D);
+    register_target(p + "attention.self.value.weight", L.wqkv, D * D, true, 2 * D * D, 3 * D * D);
+    register_target(p + "attention.self.query.bias", L.bqkv, D, false, 0, 3 * D);
+    register_target(p + "attention.self.key.bias", L.bqkv, D, false, D, 3 * D);
+    register_target(p + "attention.self.value.bias", L.bqkv, D, false, 2 * D, 3 * D);
+    register_target(p + "attention.output.dense.weight", L.wo, D * D, true);
+    register_target(p + "attention.output.dense.bias", L.bo, D, false);
+    register_target(p + "attention.output.LayerNorm.weight", L.ln1g, D, false);
+    register_target(p + "attention.output.LayerNorm.bias", L.ln1b, D, false);
+    register_target(p + "intermediate.dense.weight", L.w1, F * D, true);
+    register_target(p + "intermediate.dense.bias", L.b1, F, false);
+    register_target(p + "output.dense.weight", L.w2, D * F, true);
+    register_target(p + "output.dense.bias", L.b2, D, false);
+    register_target(p + "output.LayerNorm.weight", L.ln2g, D, false);
+    register_target(p + "output.LayerNorm.bias", L.ln2b, D, false);
+  }
+  if (cfg.classifier == 1) {
+    register_target("classifier.dense.weight", wc_, D * D, true);
+    register_target("classifier.dense.bias", bc_, D, false);
+    register_target("classifier.out_proj.weight", wout_, (int64_t)cfg.num_labels * D, false);
+    register_target("classifier.out_proj.bias", bout_, cfg.num_labels, false);
+  }
+}
+
+Encoder::~Encoder() {
+  if (stream_) {
+    (void)hipSetDevice(device_);
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
+}
+
+void Encoder::register_target(const std::string& name, DevBuf& buf, int64_t numel, bool f16,
+                              int64_t offset_elems, int64_t total_elems) {
+  const int64_t total = total_elems < 0 ? numel : total_elems;
+  const size_t esz = f16 ? sizeof(half_t) : sizeof(float);
+  if (buf.p == nullptr) {
+    buf.reserve((size_t)total * esz);
+    SR_HIP(hipMemset(buf.p, 0, (size_t)total * esz));
+  }
+  targets_[name] = Target{reinterpret_cast<char*>(buf.p) + offset_elems * esz, numel, f16};
+  is_set_[name] = false;
+}
+
+void Encoder::set_weight(const std::string& name, const float* data, int64_t numel) {
+  auto it = targets_.find(name);
+  SR_CHECK(it != targets_.end(), "encoder: unknown weight '" + name + "'");
+  const Target& t = it->second;
+  SR_CHECK(numel == t.numel, "encoder: weight '" + name + "' has " + std::to_string(numel) +
+                                 " elements, expected " + std::to_string(t.numel));
+  SR_CHECK(data != nullptr, "encoder: null weight data");
+  DeviceGuard g(device_);
+  if (t.f16) {
+    std::vector<half_t> h((size_t)numel);
+    for (int64_t i = 0; i < numel; ++i) h[i] = (half_t)data[i];
+    SR_HIP(hipMemcpy(t.ptr, h.data(), (size_t)numel * sizeof(half_t), hipMemcpyHostToDevice));
+  } else {
+    SR_HIP(hipMemcpy(t.ptr, data, (size_t)numel * sizeof(float), hipMemcpyHostToDevice));
+  }
+  is_set_[name] = true;
+}
+
+std::string Encoder::missing() const {
+  for (const auto& kv : is_set_)
+    if (!kv.second) return kv.first;
+  return std::string();
+}
+
+void Encoder::ensure_ws(int64_t tokens, int B) {
+  if (tokens <= ws_tokens_) return;
+  const int64_t d = cfg_.hidden, F = cfg_.intermediate;
+  ids_.reserve((size_t)tokens * sizeof(int32_t));
+  mask_.reserve((size_t)tokens * sizeof(int32_t));
+  types_.reserve((size_t)tokens * sizeof(int32_t));
+  pos_.reserve((size_t)tokens * sizeof(int32_t));
+  h16_.reserve((size_t)tokens * d * sizeof(half_t));
+  h32_.reserve((size_t)tokens * d * sizeof(float));
+  qkv_.reserve((size_t)tokens * 3 * d * sizeof(half_t));
+  ctx_.reserve((size_t)tokens * d * sizeof(half_t));
+  y32_.reserve((size_t)tokens * d * sizeof(float));
+  ffn_.reserve((size_t)tokens * F * sizeof(half_t));
+  (void)B;
+  ws_tokens_ = tokens;
+}
+
+void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t* types, int B,
+                          int S, int mode, int pool, void* out, int out_dtype, int ld_out,
+                          hipStream_t s) {
+  SR_CHECK(B >= 0 && S >= 1, "encoder: bad batch shape");
+  SR_CHECK(S <= cfg_.max_position - std::max(cfg_.position_offset, 0) - (cfg_.position_offset > 0 ? 1 : 0),
+           "encoder: sequence longer than the position table");
+  SR_CHECK(mode == 0 || cfg_.classifier == 1, "encoder: model has no classification head");
+  SR_CHECK(pool == SR_POOL_CLS || pool == SR_POOL_MEAN, "encoder: pool must be CLS or MEAN");
+  SR_CHECK(out_dtype == SR_DTYPE_F32 || out_dtype == SR_DTYPE_F16, "encoder: bad output dtype");
+  SR_CHECK(mode == 1 || ld_out >= cfg_.hidden, "encoder: ld_out must be >= hidden");
+  const std::string miss = missing();
+  if (!miss.empty()) throw Error(SR_ERR_STATE, "encoder: weight not set: " + miss);
+  if (B == 0) return;
+  DeviceGuard g(device_);
+  if (!s) s = stream_;
+  const int d = cfg_.hidden, F = cfg_.intermediate, H = cfg_.heads;
+  const int64_t seqs_per_chunk = std::max<int64_t>(1, max_tokens_ / S);
+  const int64_t chunk_tokens = std::min<int64_t>((int64_t)B, seqs_per_chunk) * S;
+  ensure_ws(chunk_tokens, B);
+  if (mode == 1) clst_.reserve((size_t)std::min<int64_t>(B, seqs_per_chunk) * d * sizeof(float));
+  half_t* h16 = h16_.as<half_t>();
+  float* h32 = h32_.as<float>();
+  half_t* qkv = qkv_.as<half_t>();
+  half_t* ctx = ctx_.as<half_t>();
+  float* y32 = y32_.as<float>();
+  half_t* ffn = ffn_.as<half_t>();
+  int32_t* pos = pos_.as<int32_t>();
+
+  for (int64_t b0 = 0; b0 < B; b0 += seqs_per_chunk) {
+    const int nb = (int)std::min<int64_t>(seqs_per_chunk, B - b0);
+    const int M = nb * S;
+    const int32_t* cids = ids + b0 * S;
+    const int32_t* cmask = mask + b0 * S;
+    const int32_t* ctypes = types ? types + b0 * S : nullptr;
+    launch_positions(cids, pos, nb, S, cfg_.position_offset, s);
+    launch_embed_ln(cids, pos, ctypes, wemb_.as<half_t>(), pemb_.as<half_t>(), temb_.as<half_t>(),
+                    embg_.as<float>(), embb_.as<float>(), cfg_.ln_eps, M, d, cfg_.vocab_size,
+                    cfg_.max_position, cfg_.type_vocab, h16, h32, s);
+    for (const Layer& L : layers_) {
+      launch_gemm(EPI_BIAS_F16, h16, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
+                  3 * d, M, 3 * d, d, s);
+      launch_attention(qkv, cmask, ctx, nb, S, d, H, s);
+      launch_gemm(EPI_BIAS_RES_F32, ctx, d, L.wo.as<half_t>(), L.bo.as<float>(), h32, d, y32, d,
+                  M, d, d, s);
+      launch_layernorm(y32, L.ln1g.as<float>(), L.ln1b.as<float>(), cfg_.ln_eps, M, d, h16, h32, s);
+      launch_gemm(EPI_BIAS_GELU_F16, h16, d, L.w1.as<half_t>(), L.b1.as<float>(), nullptr, 0, ffn,
+                  F, M, F, d, s);
+      launch_gemm(EPI_BIAS_RES_F32, ffn, F, L.w2.as<half_t>(), L.b2.as<float>(), h32, d, y32, d, M,
+                  d, F, s);
+      launch_layernorm(y32, L.ln2g.as<float>(), L.ln2b.as<float>(), cfg_.ln_eps, M, d, h16, h32, s);
+    }
+    if (mode == 0) {
+      const size_t esz = out_dtype == SR_DTYPE_F32 ? sizeof(float) : sizeof(half_t);
+      launch_pool_l2(h32, cmask, nb, S, d, pool,
+                     reinterpret_cast<char*>(out) + (size_t)b0 * ld_out * esz, out_dtype, ld_out, s);
+    } else {
+      float* t = clst_.as<float>();
+      // CLS rows of h16 are rows b*S: a strided GEMM operand (lda = S*d).
+      launch_gemm(EPI_BIAS_TANH_F32, h16, (int64_t)S * d, wc_.as<half_t>(), bc_.as<float>(),
+                  nullptr, 0, t, d, nb, d, d, s);
+      launch_cls_logits(t, wout_.as<float>(), bout_.as<float>(), nb, d, cfg_.num_labels,
+                        reinterpret_cast<float*>(out) + b0 * cfg_.num_labels, s);
+    }
+  }
+}
+
+void Encoder::forward_host(const int32_t* ids, const int32_t* mask, const int32_t* types, int B,
+                           int S, int mode, int pool, float* out) {
+  SR_CHECK(B >= 0 && S >= 1 && (B == 0 || (ids && mask && out)), "encoder: null buffer");
+  if (B == 0) return;
+  DeviceGuard g(device_);
+  const int64_t n = (int64_t)B * S;
+  const int64_t out_elems = (int64_t)B * (mode == 0 ? cfg_.hidden : cfg_.num_labels);
+  const size_t in_bytes = (size_t)n * sizeof(int32_t) * (types ? 3 : 2);
+  hostio_.reserve(in_bytes + (size_t)out_elems * sizeof(float));
+  int32_t* dids = hostio_.as<int32_t>();
+  int32_t* dmask = dids + n;
+  int32_t* dtypes = types ? dmask + n : nullptr;
+  float* dout = reinterpret_cast<float*>(hostio_.as<char>() + in_bytes);
+  SR_HIP(hipMemcpyAsync(dids, ids, n * sizeof(int32_t), hipMemcpyHostToDevice, stream_));
+  SR_HIP(hipMemcpyAsync(dmask, mask, n * sizeof(int32_t), hipMemcpyHostToDevice, stream_));
+  if (types) SR_HIP(hipMemcpyAsync(dtypes, types, n * sizeof(int32_t), hipMemcpyHostToDevice, stream_));
+  forward_dev(dids, dmask, dtypes, B, S, mode, pool, dout, SR_DTYPE_F32, cfg_.hidden, stream_);
+  SR_HIP(hipMemcpyAsync(out, dout, (size_t)out_elems * sizeof(float), hipMemcpyDeviceToHost, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+}
+
+}  // namespace sr

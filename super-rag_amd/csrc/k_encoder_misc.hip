@@ -1,0 +1,285 @@
+// K3 / K6 / K7 / K8 and small helpers of the encoder: position ids, embedding gather + LayerNorm,
+// LayerNorm, pooling + L2 normalisation, classification logits, row normalisation.
+// All are HBM-bound row kernels: one wave per row, 16-byte vector accesses, fp32 statistics with
+// wave shuffles (two-pass mean / variance held in registers).
+#include "sr_common.h"
+#include "sr_kernels.h"
+
+namespace sr {
+
+namespace {
+
+constexpr int MAXV = 8;  // float4 per lane per row: d <= 2048
+
+// Position ids.  BERT (offset 0): pos = s.  XLM-R (offset = padding_idx): HF
+// create_position_ids_from_input_ids: pos = (ids != pad) ? padding_idx + cumsum(ids != pad) : pad.
+__global__ void positions_kernel(const int32_t* __restrict__ ids, int32_t* __restrict__ pos, int S,
+                                 int offset) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int32_t* row = ids + (int64_t)b * S;
+  int32_t* out = pos + (int64_t)b * S;
+  if (offset == 0) {
+    for (int s = lane; s < S; s += 64) out[s] = s;
+    return;
+  }
+  int running = 0;
+  for (int s0 = 0; s0 < S; s0 += 64) {
+    const int s = s0 + lane;
+    const bool keep = s < S && row[s] != offset;
+    const uint64_t bal = __ballot(keep);
+    const int before = __popcll(bal & ((1ull << lane) - 1));
+    if (s < S) out[s] = keep ? offset + running + before + 1 : offset;
+    running += __popcll(bal);
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void ln_store(float4v (&x)[NV], int n4, const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, float eps, int d,
+                                         half_t* __restrict__ h16, float* __restrict__ h32,
+                                         int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (lane + 64 * i < n4) s += x[i][0] + x[i][1] + x[i][2] + x[i][3];
+  const float mean = wave_sum(s) / d;
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (lane + 64 * i < n4) {
+      const float4v t = x[i] - mean;
+      v += t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
+    }
+  const float rstd = rsqrtf(wave_sum(v) / d + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n4) {
+      const float4v g = reinterpret_cast<const float4v*>(gamma)[c];
+      const float4v bb = reinterpret_cast<const float4v*>(beta)[c];
+      const float4v y = (x[i] - mean) * rstd * g + bb;
+      reinterpret_cast<float4v*>(h32)[c] = y;
+      half4 hy = {(half_t)y[0], (half_t)y[1], (half_t)y[2], (half_t)y[3]};
+      reinterpret_cast<half4*>(h16)[c] = hy;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_ln_kernel(
+    const int32_t* __restrict__ ids, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ types, const half_t* __restrict__ wemb,
+    const half_t* __restrict__ pemb, const half_t* __restrict__ temb,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int M, int d,
+    int vocab, int max_pos, int type_vocab, half_t* __restrict__ h16, float* __restrict__ h32) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  int id = ids[m];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  int p = pos[m];
+  p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
+  int t = types ? types[m] : 0;
+  t = t < 0 ? 0 : (t >= type_vocab ? type_vocab - 1 : t);
+  const int n4 = d >> 2;
+  float4v x[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n4) {
+      const half4 a = reinterpret_cast<const half4*>(wemb + (int64_t)id * d)[c];
+      const half4 bp = reinterpret_cast<const half4*>(pemb + (int64_t)p * d)[c];
+      const half4 ct = reinterpret_cast<const half4*>(temb + (int64_t)t * d)[c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[i][j] = (float)a[j] + (float)bp[j] + (float)ct[j];
+    }
+  }
+  ln_store<MAXV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 + m * d, lane);
+}
+
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ y,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps,
+                                                        int M, int d, half_t* __restrict__ h16,
+                                                        float* __restrict__ h32) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int n4 = d >> 2;
+  float4v x[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n4) x[i] = reinterpret_cast<const float4v*>(y + m * d)[c];
+  }
+  ln_store<MAXV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 + m * d, lane);
+}
+
+// Pool (CLS row or attention-mask mean) of the fp32 hidden states, then L2-normalise.
+__global__ __launch_bounds__(64) void pool_l2_kernel(const float* __restrict__ h32,
+                                                     const int32_t* __restrict__ mask, int S,
+                                                     int d, int pool, void* __restrict__ out,
+                                                     int out_dtype, int ld_out) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int n4 = d >> 2;
+  float4v x[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) x[i] = float4v{0.f, 0.f, 0.f, 0.f};
+  const float* seq = h32 + (int64_t)b * S * d;
+  if (pool == SR_POOL_CLS) {
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+      if (lane + 64 * i < n4) x[i] = reinterpret_cast<const float4v*>(seq)[lane + 64 * i];
+  } else {
+    float cnt = 0.f;
+    for (int s = 0; s < S; ++s) {
+      if (mask[(int64_t)b * S + s] == 0) continue;
+      cnt += 1.f;
+#pragma unroll
+      for (int i = 0; i < MAXV; ++i)
+        if (lane + 64 * i < n4) x[i] += reinterpret_cast<const float4v*>(seq + (int64_t)s * d)[lane + 64 * i];
+    }
+    const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) x[i] *= inv;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (lane + 64 * i < n4) ss += x[i][0] * x[i][0] + x[i][1] * x[i][1] + x[i][2] * x[i][2] + x[i][3] * x[i][3];
+  const float nrm = sqrtf(wave_sum(ss));
+  const float inv = nrm > 0.f ? 1.f / nrm : 0.f;  // zero-norm guard (graphiti helpers.py:100-103)
+  if (out_dtype == SR_DTYPE_F32) {
+    float* o = reinterpret_cast<float*>(out) + (int64_t)b * ld_out;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+      if (lane + 64 * i < n4) reinterpret_cast<float4v*>(o)[lane + 64 * i] = x[i] * inv;
+  } else {
+    half_t* o = reinterpret_cast<half_t*>(out) + (int64_t)b * ld_out;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+      if (lane + 64 * i < n4) {
+        const float4v v = x[i] * inv;
+        half4 hv = {(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+        reinterpret_cast<half4*>(o)[lane + 64 * i] = hv;
+      }
+    for (int c = d + lane; c < ld_out; c += 64) o[c] = (half_t)0.f;
+  }
+}
+
+// logits[p][j] = dot(t[p], w[j]) + bias[j]   (RoBERTa classification head out_proj).
+__global__ __launch_bounds__(256) void cls_logits_kernel(const float* __restrict__ t,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int P,
+                                                         int d, int labels,
+                                                         float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const int n4 = d >> 2;
+  for (int j = 0; j < labels; ++j) {
+    float s = 0.f;
+    for (int c = lane; c < n4; c += 64) {
+      const float4v a = reinterpret_cast<const float4v*>(t + p * d)[c];
+      const float4v bw = reinterpret_cast<const float4v*>(w + (int64_t)j * d)[c];
+      s += a[0] * bw[0] + a[1] * bw[1] + a[2] * bw[2] + a[3] * bw[3];
+    }
+    s = wave_sum(s);
+    if (lane == 0) out[p * labels + j] = s + bias[j];
+  }
+}
+
+// out[r][:dim] = fp16(x[r] / ||x[r]||), out[r][dim:ld] = 0.  Zero rows stay zero.
+__global__ __launch_bounds__(256) void normalize_rows_kernel(const void* __restrict__ x, int dtype,
+                                                             int64_t n, int dim,
+                                                             half_t* __restrict__ out, int ld) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  float ss = 0.f;
+  if (dtype == SR_DTYPE_F32) {
+    const float* row = reinterpret_cast<const float*>(x) + r * dim;
+    for (int c = lane; c < dim; c += 64) ss += row[c] * row[c];
+    const float nrm = sqrtf(wave_sum(ss));
+    const float inv = nrm > 0.f ? 1.f / nrm : 0.f;
+    for (int c = lane; c < ld; c += 64) out[r * ld + c] = (half_t)(c < dim ? row[c] * inv : 0.f);
+  } else {
+    const half_t* row = reinterpret_cast<const half_t*>(x) + r * dim;
+    for (int c = lane; c < dim; c += 64) ss += (float)row[c] * (float)row[c];
+    const float nrm = sqrtf(wave_sum(ss));
+    const float inv = nrm > 0.f ? 1.f / nrm : 0.f;
+    for (int c = lane; c < ld; c += 64) out[r * ld + c] = (half_t)(c < dim ? (float)row[c] * inv : 0.f);
+  }
+}
+
+__global__ void convert_f32_f16_kernel(const float* __restrict__ in, half_t* __restrict__ out,
+                                       int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (half_t)in[i];
+}
+
+}  // namespace
+
+void launch_positions(const int32_t* ids, int32_t* pos, int B, int S, int offset, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(positions_kernel, dim3(B), dim3(64), 0, s, ids, pos, S, offset);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* types,
+                     const half_t* wemb, const half_t* pemb, const half_t* temb,
+                     const float* gamma, const float* beta, float eps, int M, int d, int vocab,
+                     int max_pos, int type_vocab, half_t* h16, float* h32, hipStream_t s) {
+  SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "embed_ln: hidden must be a multiple of 4, <= 2048");
+  if (M <= 0) return;
+  ProfScope prof("embed_ln", s, 0.0, (double)M * d * (3 * 2 + 2 + 4));
+  hipLaunchKernelGGL(embed_ln_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, ids, pos,
+                     types, wemb, pemb, temb, gamma, beta, eps, M, d, vocab, max_pos, type_vocab,
+                     h16, h32);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_layernorm(const float* y, const float* gamma, const float* beta, float eps, int M,
+                      int d, half_t* h16, float* h32, hipStream_t s) {
+  SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "layernorm: hidden must be a multiple of 4, <= 2048");
+  if (M <= 0) return;
+  ProfScope prof("layernorm", s, 0.0, (double)M * d * (4 + 4 + 2));
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, y, gamma,
+                     beta, eps, M, d, h16, h32);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_pool_l2(const float* h32, const int32_t* mask, int B, int S, int d, int pool,
+                    void* out, int out_dtype, int ld_out, hipStream_t s) {
+  SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "pool: hidden must be a multiple of 4, <= 2048");
+  if (B <= 0) return;
+  ProfScope prof("pool_l2", s, 0.0, (double)B * d * 4.0 * (pool == SR_POOL_CLS ? 1 : S));
+  hipLaunchKernelGGL(pool_l2_kernel, dim3(B), dim3(64), 0, s, h32, mask, S, d, pool, out,
+                     out_dtype, ld_out);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_cls_logits(const float* t, const float* w, const float* bias, int P, int d,
+                       int labels, float* out, hipStream_t s) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(cls_logits_kernel, dim3((unsigned)ceil_div(P, 4)), dim3(256), 0, s, t, w,
+                     bias, P, d, labels, out);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_normalize_rows(const void* x, int dtype, int64_t n, int dim, half_t* out, int ld,
+                           hipStream_t s) {
+  if (n <= 0) return;
+  ProfScope prof("normalize_rows", s, 0.0, (double)n * (dim * (dtype == SR_DTYPE_F32 ? 4 : 2) + ld * 2));
+  hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, x,
+                     dtype, n, dim, out, ld);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_convert_f32_f16(const float* in, half_t* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(convert_f32_f16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                     in, out, n);
+  SR_LAUNCH_CHECK();
+}
+
+}  // namespace sr

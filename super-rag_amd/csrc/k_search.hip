@@ -1,0 +1,518 @@
+// K1 / K2: exact cosine top-k over the in-HBM corpus (replaces SeekDB HNSW cosine search,
+// super_rag/vectorstore/seekdb_connector.py:98-115), plus the multi-shard merge, the cross-encoder
+// pair packer and the rerank ordering.
+//
+// K1 cosine_scan: sims = C_tile . Q^T on MFMA (v_mfma_f32_16x16x32_f16, fp32 accumulate) for a
+// 256-row corpus tile against up to 256 queries per workgroup (8 waves, 32 rows each).  The
+// corpus streams once from HBM through a double-buffered LDS-DMA (global_load_lds_dwordx4) ring;
+// the query block is L2-resident and restaged per k-step.  The score matrix is never written:
+// the epilogue keeps only (query, row) pairs whose similarity is >= the query's running k-th
+// best (tau), appending 64-bit keys (ordered(sim) << 32 | ~row) to a per-query candidate list.
+// The very first chunk of rows runs in DENSE mode (every key written, no atomics) to seed tau.
+//
+// K2 select: one workgroup per query loads its candidate keys into LDS, finds the k-th largest
+// key by an MSB radix select (8-bit digits, per-wave LDS histograms, wave-parallel suffix scan)
+// and bitonic-sorts the k winners.  Keys are unique (row in the low word), so the k-th key is
+// exact and ties in similarity resolve by ascending row id, as the oracle does.
+#include "sr_common.h"
+#include "sr_kernels.h"
+
+namespace sr {
+
+namespace {
+
+constexpr int SROWS = 256;    // corpus rows per scan workgroup
+constexpr int SBK = 64;       // k per stage (fp16 elements)
+constexpr int STHREADS = 512; // 8 waves
+
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void glds_rows(const half_t* __restrict__ g, int64_t ld, int64_t row0,
+                                          int64_t row_last, int k0, half_t* lds_piece, int prow0,
+                                          int lane) {
+  // One 1 KiB wave-instruction: 8 rows (prow0 .. prow0+7 of the LDS image) x 64 fp16.
+  const int r = prow0 + (lane >> 3);
+  const int c = swz_chunk(r, lane & 7);
+  int64_t gr = row0 + r;
+  gr = gr < row_last ? gr : row_last;
+  __builtin_amdgcn_global_load_lds((const void*)(g + gr * ld + k0 + c * 8), SR_LDS(lds_piece), 16,
+                                   0, 0);
+}
+
+__device__ __forceinline__ half8 lds_frag(const half_t* tile, int row, int chunk) {
+  return *reinterpret_cast<const half8*>(tile + row * SBK + swz_chunk(row, chunk) * 8);
+}
+
+template <int QT, bool DENSE>
+__global__ __launch_bounds__(STHREADS, 1) void cosine_scan_kernel(
+    const half_t* __restrict__ corpus, int64_t ldc, const uint8_t* __restrict__ live, int64_t r0,
+    int64_t r1, const half_t* __restrict__ Q, int B, const float* __restrict__ tau,
+    uint64_t* __restrict__ cand, int* __restrict__ cnt, int cap) {
+  constexpr int QROWS = 16 * QT;
+  constexpr int STAGE = (SROWS + QROWS) * SBK;  // halfs per stage
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t row0 = r0 + (int64_t)blockIdx.x * SROWS;
+  const int64_t row_last = r1 - 1;
+  const int nk = (int)(ldc / SBK);
+
+  float4v acc[2][QT];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int q = 0; q < QT; ++q) acc[a][q] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int kt, int buf) {
+    half_t* C = lds + buf * STAGE;
+    half_t* Qs = C + SROWS * SBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int prow = wave * 32 + i * 8;
+      glds_rows(corpus, ldc, row0, row_last, kt * SBK, C + prow * SBK, prow, lane);
+    }
+    for (int i = wave; i < 2 * QT; i += 8)
+      glds_rows(Q, ldc, 0, QROWS - 1, kt * SBK, Qs + i * 8 * SBK, i * 8, lane);
+  };
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const half_t* C = lds + cur * STAGE;
+    const half_t* Qs = C + SROWS * SBK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int chunk = (lane >> 4) + 4 * s;
+      half8 a[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) a[rt] = lds_frag(C, wave * 32 + rt * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const half8 b = lds_frag(Qs, qt * 16 + (lane & 15), chunk);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], b, acc[rt][qt], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // Epilogue: lane owns sim(row = row0 + 32w + 16rt + 4(lane>>4) + r, query = 16qt + (lane&15)).
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int q = qt * 16 + (lane & 15);
+    if (q >= B) continue;
+    const float t = DENSE ? -INFINITY : tau[q];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + wave * 32 + rt * 16 + 4 * (lane >> 4) + r;
+        if (row > row_last) continue;
+        const bool alive = live == nullptr || live[row] != 0;
+        const float sim = acc[rt][qt][r];
+        if constexpr (DENSE) {
+          cand[(int64_t)q * cap + (row - r0)] = alive ? make_key(sim, (uint32_t)row) : 0ull;
+        } else {
+          if (alive && sim >= t) {
+            const int pos = atomicAdd(&cnt[q], 1);
+            if (pos < cap) cand[(int64_t)q * cap + pos] = make_key(sim, (uint32_t)row);
+          }
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Block-wide top-k over keys in LDS.
+constexpr int SEL_THREADS = 512;
+constexpr int SEL_CAP = 16384;  // keys per query held in LDS (128 KiB)
+
+__device__ __forceinline__ void bitonic_sort_desc(uint64_t* v, int n /*pow2*/) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < (n >> 1); i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const uint64_t a = v[lo], b = v[hi];
+        if ((a < b) == desc) {
+          v[lo] = b;
+          v[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+struct SelShared {
+  int hist[SEL_THREADS / 64][256];
+  int tot[256];
+  uint64_t sel[SR_MAX_TOPK];
+  int nsel;
+  int digit;
+  int above;
+};
+
+// keys[0..n) in LDS (all non-zero, unique).  On return sh.sel[0..m) holds the m = min(n, k)
+// largest keys sorted descending; returns m.
+__device__ int block_topk(const uint64_t* keys, int n, int k, SelShared& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int shift_final = 0;
+  uint64_t prefix = 0;
+  if (n > k) {
+    int kk = k;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      const uint64_t mask_hi = shift == 56 ? 0ull : (~0ull << (shift + 8));
+      for (int i = tid; i < (SEL_THREADS / 64) * 256; i += blockDim.x) (&sh.hist[0][0])[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < n; i += blockDim.x) {
+        const uint64_t key = keys[i];
+        if ((key & mask_hi) == prefix) atomicAdd(&sh.hist[wave][(key >> shift) & 255], 1);
+      }
+      __syncthreads();
+      if (tid < 256) {
+        int t = 0;
+#pragma unroll
+        for (int w = 0; w < SEL_THREADS / 64; ++w) t += sh.hist[w][tid];
+        sh.tot[tid] = t;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        // lane l owns digits 4l .. 4l+3; suffix sums from the top digit down.
+        int c[4], t = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c[j] = sh.tot[4 * lane + j];
+          t += c[j];
+        }
+        int suf = t;  // inclusive suffix sum over lanes >= lane
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_down(suf, o, 64);
+          if (lane + o < 64) suf += v;
+        }
+        const uint64_t bal = __ballot(suf >= kk);
+        const int L = 63 - __clzll(bal);
+        if (lane == L) {
+          int above = suf - t;  // keys in lanes > L
+          int dsel = 4 * lane;
+          for (int j = 3; j >= 0; --j) {
+            if (above + c[j] >= kk) {
+              dsel = 4 * lane + j;
+              break;
+            }
+            above += c[j];
+          }
+          sh.digit = dsel;
+          sh.above = above;
+        }
+      }
+      __syncthreads();
+      const int d = sh.digit;
+      kk -= sh.above;
+      prefix |= (uint64_t)d << shift;
+      shift_final = shift;
+      const int td = sh.tot[d];
+      __syncthreads();
+      if (td == kk) break;  // every key with this prefix is in the top-k
+    }
+  }
+  if (tid == 0) sh.nsel = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += blockDim.x) {
+    const uint64_t key = keys[i];
+    if (n <= k || (key >> shift_final) >= (prefix >> shift_final)) {
+      const int p = atomicAdd(&sh.nsel, 1);
+      if (p < SR_MAX_TOPK) sh.sel[p] = key;
+    }
+  }
+  __syncthreads();
+  const int m = min(sh.nsel, k);
+  int np2 = 1;
+  while (np2 < sh.nsel) np2 <<= 1;
+  np2 = min(np2, SR_MAX_TOPK);
+  for (int i = sh.nsel + tid; i < np2; i += blockDim.x) sh.sel[i] = 0ull;
+  __syncthreads();
+  bitonic_sort_desc(sh.sel, np2);
+  return m;
+}
+
+struct SelectSmem {
+  uint64_t keys[SEL_CAP];
+  SelShared sh;
+};
+
+__global__ __launch_bounds__(SEL_THREADS, 1) void topk_select_kernel(
+    uint64_t* __restrict__ cand, int* __restrict__ cnt, int cap, float* __restrict__ tau, int k,
+    int* __restrict__ overflow, int final_pass, float* __restrict__ out_sim,
+    int64_t* __restrict__ out_rows, int64_t row_offset) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SelectSmem& S = *reinterpret_cast<SelectSmem*>(smem_raw);
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int n_raw = cnt[q];
+  if (n_raw > cap && tid == 0) atomicOr(overflow, 1);
+  const int n_in = min(n_raw, cap);
+  uint64_t* list = cand + (int64_t)q * cap;
+  // Load non-zero keys (zero = dead row in a dense chunk) into LDS.
+  if (tid == 0) S.sh.nsel = 0;
+  __syncthreads();
+  for (int i = tid; i < n_in; i += blockDim.x) {
+    const uint64_t key = list[i];
+    if (key != 0ull) {
+      const int p = atomicAdd(&S.sh.nsel, 1);
+      S.keys[p] = key;
+    }
+  }
+  __syncthreads();
+  const int n = S.sh.nsel;
+  __syncthreads();
+  const int m = block_topk(S.keys, n, k, S.sh);
+  for (int i = tid; i < m; i += blockDim.x) list[i] = S.sh.sel[i];
+  if (tid == 0) {
+    cnt[q] = m;
+    tau[q] = (m == k) ? key_sim(S.sh.sel[k - 1]) : -INFINITY;
+  }
+  if (final_pass) {
+    for (int i = tid; i < k; i += blockDim.x) {
+      const bool ok = i < m;
+      out_sim[(int64_t)q * k + i] = ok ? key_sim(S.sh.sel[i]) : -INFINITY;
+      out_rows[(int64_t)q * k + i] = ok ? (int64_t)key_row(S.sh.sel[i]) + row_offset : -1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(SEL_THREADS, 1) void topk_merge_kernel(
+    const float* __restrict__ sims, const int64_t* __restrict__ rows, int P, int B, int k,
+    int k_out, float* __restrict__ out_sim, int64_t* __restrict__ out_rows) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SelectSmem& S = *reinterpret_cast<SelectSmem*>(smem_raw);
+  const int q = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) S.sh.nsel = 0;
+  __syncthreads();
+  for (int i = tid; i < P * k; i += blockDim.x) {
+    const int p = i / k, j = i - p * k;
+    const int64_t off = ((int64_t)p * B + q) * k + j;
+    const int64_t r = rows[off];
+    if (r >= 0) {
+      const int pos = atomicAdd(&S.sh.nsel, 1);
+      S.keys[pos] = make_key(sims[off], (uint32_t)r);
+    }
+  }
+  __syncthreads();
+  const int n = S.sh.nsel;
+  __syncthreads();
+  const int m = block_topk(S.keys, n, k_out, S.sh);
+  for (int i = tid; i < k_out; i += blockDim.x) {
+    const bool ok = i < m;
+    out_sim[(int64_t)q * k_out + i] = ok ? key_sim(S.sh.sel[i]) : -INFINITY;
+    out_rows[(int64_t)q * k_out + i] = ok ? (int64_t)key_row(S.sh.sel[i]) : -1;
+  }
+}
+
+__global__ void fill_int_kernel(int* __restrict__ p, int n, int v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+__global__ void fill_float_kernel(float* __restrict__ p, int n, float v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Cross-encoder pair packing (HF tokenizer pair layout, 'longest_first' truncation).
+__global__ __launch_bounds__(256) void build_pairs_kernel(
+    const int32_t* __restrict__ q_tok, const int32_t* __restrict__ q_len, int lq_max,
+    const int32_t* __restrict__ p_tok, const int32_t* __restrict__ p_len, int lp_max,
+    const int64_t* __restrict__ cand_rows, int B, int K, int S, int style, int bos, int eos,
+    int pad, int32_t* __restrict__ out_ids, int32_t* __restrict__ out_mask,
+    int32_t* __restrict__ out_type) {
+  const int lane = threadIdx.x & 63;
+  const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= (int64_t)B * K) return;
+  const int b = (int)(pair / K);
+  const int64_t row = cand_rows[pair];
+  int lq = min(max(q_len[b], 0), lq_max);
+  int lp = row >= 0 ? min(max(p_len[row], 0), lp_max) : 0;
+  const int nspec = style == 0 ? 4 : 3;
+  const int budget = max(S - nspec, 0);
+  // longest_first: drop from the longer side, from the passage on ties (HF truncate_sequences).
+  int excess = lq + lp - budget;
+  if (excess > 0) {
+    const int diff = lp - lq;
+    if (diff >= 0) {
+      const int cut = min(diff, excess);
+      lp -= cut;
+      excess -= cut;
+    } else {
+      const int cut = min(-diff, excess);
+      lq -= cut;
+      excess -= cut;
+    }
+    lp -= (excess + 1) / 2;
+    lq -= excess / 2;
+  }
+  const int32_t* qt = q_tok + (int64_t)b * lq_max;
+  const int32_t* pt = row >= 0 ? p_tok + row * lp_max : nullptr;
+  // Segment boundaries.
+  const int q_start = 1;
+  const int q_end = q_start + lq;                 // first separator
+  const int p_start = q_end + (style == 0 ? 2 : 1);
+  const int p_end = p_start + lp;                 // final separator
+  const int total = p_end + 1;
+  int32_t* oi = out_ids + pair * S;
+  int32_t* om = out_mask + pair * S;
+  int32_t* ot = out_type ? out_type + pair * S : nullptr;
+  for (int s = lane; s < S; s += 64) {
+    int id;
+    if (s == 0) id = bos;
+    else if (s < q_end) id = qt[s - q_start];
+    else if (s < p_start) id = eos;
+    else if (s < p_end) id = pt[s - p_start];
+    else if (s == p_end) id = eos;
+    else id = pad;
+    oi[s] = id;
+    om[s] = s < total ? 1 : 0;
+    if (ot) ot[s] = (style == 1 && s >= p_start && s < total) ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void rerank_select_kernel(const float* __restrict__ logits,
+                                                            int K, int k_out,
+                                                            int32_t* __restrict__ out_index) {
+  __shared__ uint64_t v[SR_MAX_TOPK];
+  const int b = blockIdx.x;
+  int np2 = 1;
+  while (np2 < K) np2 <<= 1;
+  for (int i = threadIdx.x; i < np2; i += blockDim.x)
+    v[i] = i < K ? make_key(logits[(int64_t)b * K + i], (uint32_t)i) : 0ull;
+  __syncthreads();
+  bitonic_sort_desc(v, np2);
+  for (int i = threadIdx.x; i < k_out; i += blockDim.x)
+    out_index[(int64_t)b * k_out + i] = i < K ? (int32_t)key_row(v[i]) : -1;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Host launchers
+
+template <int QT>
+static void scan_qt(bool dense, dim3 grid, hipStream_t s, const half_t* corpus, int64_t ldc,
+                    const uint8_t* live, int64_t r0, int64_t r1, const half_t* Q, int B,
+                    const float* tau, uint64_t* cand, int* cnt, int cap) {
+  if (dense)
+    hipLaunchKernelGGL((cosine_scan_kernel<QT, true>), grid, dim3(STHREADS), 0, s, corpus, ldc,
+                       live, r0, r1, Q, B, tau, cand, cnt, cap);
+  else
+    hipLaunchKernelGGL((cosine_scan_kernel<QT, false>), grid, dim3(STHREADS), 0, s, corpus, ldc,
+                       live, r0, r1, Q, B, tau, cand, cnt, cap);
+}
+
+int scan_query_tiles(int B) {
+  if (B <= 16) return 1;
+  if (B <= 32) return 2;
+  if (B <= 64) return 4;
+  if (B <= 128) return 8;
+  return 16;
+}
+
+void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uint8_t* live,
+                        int64_t r0, int64_t r1, const half_t* Q, int B, const float* tau,
+                        uint64_t* cand, int* cnt, int cap, hipStream_t s) {
+  SR_CHECK(B > 0 && B <= 256, "cosine_scan: 1..256 queries per launch");
+  SR_CHECK(ldc % SBK == 0, "cosine_scan: padded dim must be a multiple of 64");
+  if (r1 <= r0) return;
+  SR_CHECK(!dense || r1 - r0 <= cap, "cosine_scan: dense chunk larger than the candidate list");
+  const int qt = scan_query_tiles(B);
+  const dim3 grid((unsigned)ceil_div(r1 - r0, SROWS));
+  const double rows = (double)(r1 - r0);
+  ProfScope prof(dense ? "cosine_scan_dense" : "cosine_scan", s, 2.0 * rows * ldc * B,
+                 rows * ldc * 2.0 + (double)B * ldc * 2.0 + (dense ? rows * B * 8.0 : 0.0));
+  switch (qt) {
+    case 1: scan_qt<1>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+    case 2: scan_qt<2>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+    case 4: scan_qt<4>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+    case 8: scan_qt<8>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+    default: scan_qt<16>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+  }
+  SR_LAUNCH_CHECK();
+}
+
+static bool g_select_attr_set = false;
+
+static void ensure_select_attrs() {
+  if (g_select_attr_set) return;
+  SR_HIP(hipFuncSetAttribute((const void*)topk_select_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(SelectSmem)));
+  SR_HIP(hipFuncSetAttribute((const void*)topk_merge_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(SelectSmem)));
+  g_select_attr_set = true;
+}
+
+int select_capacity() { return SEL_CAP; }
+
+void launch_topk_select(uint64_t* cand, int* cnt, int cap, float* tau, int B, int k,
+                        int* overflow, bool final_pass, float* out_sim, int64_t* out_rows,
+                        int64_t row_offset, hipStream_t s) {
+  SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "topk: k must be in [1, 1024]");
+  SR_CHECK(cap <= SEL_CAP, "topk: candidate capacity too large");
+  ensure_select_attrs();
+  ProfScope prof("topk_select", s, 0.0, (double)B * cap * 8.0);
+  hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(SEL_THREADS), sizeof(SelectSmem), s, cand,
+                     cnt, cap, tau, k, overflow, final_pass ? 1 : 0, out_sim, out_rows, row_offset);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_topk_merge(const float* sims, const int64_t* rows, int P, int B, int k, int k_out,
+                       float* out_sim, int64_t* out_rows, hipStream_t s) {
+  SR_CHECK(k_out >= 1 && k_out <= SR_MAX_TOPK, "merge: k_out must be in [1, 1024]");
+  SR_CHECK((int64_t)P * k <= SEL_CAP, "merge: P * k must be <= 16384");
+  if (B <= 0) return;
+  ensure_select_attrs();
+  ProfScope prof("topk_merge", s, 0.0, (double)P * B * k * 12.0);
+  hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(SEL_THREADS), sizeof(SelectSmem), s, sims,
+                     rows, P, B, k, k_out, out_sim, out_rows);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_fill_int(int* p, int n, int v, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fill_int_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, p, n, v);
+  SR_LAUNCH_CHECK();
+}
+void launch_fill_float(float* p, int n, float v, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fill_float_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, p, n, v);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_build_pairs(const int32_t* q_tok, const int32_t* q_len, int lq_max,
+                        const int32_t* p_tok, const int32_t* p_len, int lp_max,
+                        const int64_t* cand_rows, int B, int K, int S, int style, int bos, int eos,
+                        int pad, int32_t* out_ids, int32_t* out_mask, int32_t* out_type,
+                        hipStream_t s) {
+  SR_CHECK(style == 0 || style == 1, "build_pairs: style must be 0 (RoBERTa) or 1 (BERT)");
+  SR_CHECK(S >= 4, "build_pairs: sequence too short");
+  const int64_t pairs = (int64_t)B * K;
+  if (pairs <= 0) return;
+  hipLaunchKernelGGL(build_pairs_kernel, dim3((unsigned)ceil_div(pairs, 4)), dim3(256), 0, s,
+                     q_tok, q_len, lq_max, p_tok, p_len, lp_max, cand_rows, B, K, S, style, bos,
+                     eos, pad, out_ids, out_mask, out_type);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_rerank_select(const float* logits, int B, int K, int k_out, int32_t* out_index,
+                          hipStream_t s) {
+  SR_CHECK(K >= 1 && K <= SR_MAX_TOPK && k_out >= 1 && k_out <= K,
+           "rerank_select: need 1 <= k_out <= K <= 1024");
+  if (B <= 0) return;
+  hipLaunchKernelGGL(rerank_select_kernel, dim3(B), dim3(256), 0, s, logits, K, k_out, out_index);
+  SR_LAUNCH_CHECK();
+}
+
+}  // namespace sr

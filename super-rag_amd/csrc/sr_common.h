@@ -1,0 +1,91 @@
+// Shared host/device definitions for the MI355X (gfx950) hot path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/super_rag_mi355x.h"
+
+namespace sr {
+
+typedef _Float16 half_t;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float float4v __attribute__((ext_vector_type(4)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+// ---- error plumbing (host) -------------------------------------------------------------------
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define SR_HIP(call)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (call);                                                                  \
+    if (_e != hipSuccess) {                                                                  \
+      throw ::sr::Error(_e == hipErrorOutOfMemory ? SR_ERR_OOM : SR_ERR_HIP,                 \
+                        std::string(#call) + ": " + hipGetErrorString(_e) + " at " +         \
+                            __FILE__ + ":" + std::to_string(__LINE__));                      \
+    }                                                                                        \
+  } while (0)
+
+#define SR_CHECK(cond, msg)                                                                   \
+  do {                                                                                        \
+    if (!(cond)) throw ::sr::Error(SR_ERR_INVALID, std::string(msg));                         \
+  } while (0)
+
+#define SR_LAUNCH_CHECK() SR_HIP(hipGetLastError())
+
+// ---- profiling (host) ------------------------------------------------------------------------
+// Records a begin/end HIP event pair around a launch when profiling is on.
+struct ProfScope {
+  const char* name;
+  double flops, bytes;
+  hipStream_t stream;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  ProfScope(const char* n, hipStream_t s, double f, double b);
+  ~ProfScope();
+};
+
+// ---- small helpers ---------------------------------------------------------------------------
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+// Device pointer helpers for LDS address space.
+#define SR_LDS(p) ((__attribute__((address_space(3))) void*)(p))
+
+// Order-preserving float -> uint32 (larger float -> larger uint).
+__device__ __forceinline__ uint32_t ordered_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unordered_bits(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+// Top-k key: (similarity desc, row asc) <=> key desc.  key == 0 marks "no entry".
+__device__ __forceinline__ uint64_t make_key(float sim, uint32_t row) {
+  return ((uint64_t)ordered_bits(sim) << 32) | (uint64_t)(0xffffffffu - row);
+}
+__device__ __forceinline__ float key_sim(uint64_t key) { return unordered_bits((uint32_t)(key >> 32)); }
+__device__ __forceinline__ uint32_t key_row(uint64_t key) { return 0xffffffffu - (uint32_t)key; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace sr

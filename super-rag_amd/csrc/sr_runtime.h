@@ -1,0 +1,140 @@
+// Host runtime objects behind the C-ABI: the in-HBM vector store and the transformer encoder.
+#pragma once
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sr_common.h"
+
+namespace sr {
+
+// RAII device allocation.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) {
+    o.p = nullptr;
+    o.bytes = 0;
+  }
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // Grow to at least n bytes (contents are NOT preserved).
+  void reserve(size_t n) {
+    if (n <= bytes) return;
+    release();
+    SR_HIP(hipMalloc(&p, n));
+    bytes = n;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+// Scoped device selection (restores the caller's current device).
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int dev) {
+    SR_HIP(hipGetDevice(&prev));
+    if (prev != dev) SR_HIP(hipSetDevice(dev));
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+// ------------------------------------------------------------------------------------------------
+class Store {
+ public:
+  Store(int dim, int device, int64_t capacity);
+  ~Store();
+
+  int dim() const { return dim_; }
+  int ld() const { return ld_; }
+  int device() const { return device_; }
+  int64_t rows() const { return n_rows_; }
+  int64_t live() const { return n_live_; }
+
+  void add_host(const float* vecs, int64_t n, int64_t* out_rows);
+  int64_t add_dev(const void* vecs, int dtype, int64_t n, hipStream_t s);
+  void remove(const int64_t* rows, int64_t n);
+  void get(const int64_t* rows, int64_t n, float* out);
+  void search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows);
+  void search_dev(const void* q, int q_dtype, int B, int k, float* out_sim, int64_t* out_rows,
+                  int64_t row_offset, hipStream_t s);
+  void save(const char* path);
+  static Store* load(const char* path, int device);
+  void compact(int64_t* old_to_new);
+
+  std::mutex mu;
+
+ private:
+  void ensure_capacity(int64_t rows);
+  void ensure_query_ws(int B);
+  // Runs the chunked scan/select schedule for one block of <= 256 normalised queries.
+  void search_block(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
+                    int64_t row_offset, hipStream_t s, bool safe);
+
+  int dim_, ld_, device_;
+  int64_t n_rows_ = 0, n_live_ = 0, capacity_ = 0;
+  DevBuf corpus_, live_;
+  std::vector<uint8_t> live_host_;
+  hipStream_t stream_ = nullptr;
+  // search workspace
+  DevBuf qbuf_, qstage_, cand_, cnt_, tau_, overflow_, osim_, orows_, scratch_;
+  int ws_queries_ = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
+class Encoder {
+ public:
+  Encoder(const sr_encoder_config& cfg, int device);
+  ~Encoder();
+
+  void set_weight(const std::string& name, const float* data, int64_t numel);
+  std::string missing() const;  // empty when every weight is set
+
+  // mode 0: pooled embeddings to `out` (dtype/ld_out); mode 1: classifier logits (fp32).
+  void forward_dev(const int32_t* ids, const int32_t* mask, const int32_t* types, int B, int S,
+                   int mode, int pool, void* out, int out_dtype, int ld_out, hipStream_t s);
+  void forward_host(const int32_t* ids, const int32_t* mask, const int32_t* types, int B, int S,
+                    int mode, int pool, float* out);
+
+  const sr_encoder_config& config() const { return cfg_; }
+  int device() const { return device_; }
+  std::mutex mu;
+
+ private:
+  struct Target {
+    void* ptr;
+    int64_t numel;
+    bool f16;
+  };
+  struct Layer {
+    DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, w1, b1, w2, b2, ln2g, ln2b;
+  };
+  void register_target(const std::string& name, DevBuf& buf, int64_t numel, bool f16,
+                       int64_t offset_elems = 0, int64_t total_elems = -1);
+  void ensure_ws(int64_t tokens, int B);
+
+  sr_encoder_config cfg_;
+  int device_;
+  hipStream_t stream_ = nullptr;
+  int64_t max_tokens_;
+  DevBuf wemb_, pemb_, temb_, embg_, embb_, wc_, bc_, wout_, bout_;
+  std::vector<Layer> layers_;
+  std::map<std::string, Target> targets_;
+  std::map<std::string, bool> is_set_;
+  // workspace
+  DevBuf ids_, mask_, types_, pos_, h16_, h32_, qkv_, ctx_, y32_, ffn_, clst_, hostio_;
+  int64_t ws_tokens_ = 0;
+};
+
+}  // namespace sr

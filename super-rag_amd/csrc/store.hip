@@ -1,0 +1,344 @@
+// In-HBM exact cosine vector store (replaces SeekDB's HNSW collection,
+// super_rag/vectorstore/seekdb_connector.py:31-155).
+//
+// Layout in HBM: corpus = capacity x ld fp16 rows (ld = dim rounded up to 64, zero padded),
+// every row L2-normalised on insertion; live = capacity bytes (1 = live, 0 = tombstoned).
+// Search runs K1 (cosine_scan) over geometrically growing row chunks, each followed by K2
+// (topk_select) that keeps the exact top-k and raises the per-query threshold tau:
+//   chunk 0: DENSE scan of min(n, 8192) rows (seeds tau), then chunks growing by up to 8x.
+// A per-query candidate list holds at most select_capacity() keys; if any list overflows (an
+// adversarial row order), the whole block is re-run in "safe" mode with chunks of
+// capacity - k rows, which can never overflow.  Results are exact either way.
+#include <fstream>
+
+#include "sr_kernels.h"
+#include "sr_runtime.h"
+
+namespace sr {
+
+namespace {
+constexpr int kDenseRows = 8192;
+constexpr int kQueryBlock = 256;
+constexpr int64_t kAddChunk = 1 << 16;
+
+__global__ void clear_flags_kernel(uint8_t* live, const int64_t* rows, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) live[rows[i]] = 0;
+}
+__global__ void gather_rows_kernel(const half_t* __restrict__ src, int ld,
+                                   const int64_t* __restrict__ rows, int64_t n,
+                                   half_t* __restrict__ dst) {
+  const int64_t r = blockIdx.x;
+  if (r >= n) return;
+  const half8* s = reinterpret_cast<const half8*>(src + rows[r] * ld);
+  half8* d = reinterpret_cast<half8*>(dst + r * ld);
+  for (int c = threadIdx.x; c < ld / 8; c += blockDim.x) d[c] = s[c];
+}
+__global__ void f16_to_f32_rows_kernel(const half_t* __restrict__ src, int ld,
+                                       const int64_t* __restrict__ rows, int64_t n, int dim,
+                                       float* __restrict__ out) {
+  const int64_t r = blockIdx.x;
+  if (r >= n) return;
+  for (int c = threadIdx.x; c < dim; c += blockDim.x) out[r * dim + c] = (float)src[rows[r] * ld + c];
+}
+}  // namespace
+
+Store::Store(int dim, int device, int64_t capacity) : dim_(dim), device_(device) {
+  SR_CHECK(dim > 0 && dim <= 8192, "store: dim must be in [1, 8192]");
+  ld_ = (int)round_up(dim, 64);
+  DeviceGuard g(device_);
+  SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  ensure_capacity(capacity > 0 ? capacity : 1024);
+}
+
+Store::~Store() {
+  if (stream_) {
+    (void)hipSetDevice(device_);
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
+}
+
+void Store::ensure_capacity(int64_t rows) {
+  if (rows <= capacity_) return;
+  int64_t cap = std::max<int64_t>(rows, capacity_ + capacity_ / 2);
+  cap = round_up(cap, 256);
+  DevBuf nc, nl;
+  nc.reserve((size_t)cap * ld_ * sizeof(half_t));
+  nl.reserve((size_t)cap);
+  SR_HIP(hipMemsetAsync(nl.p, 0, (size_t)cap, stream_));
+  if (n_rows_ > 0) {
+    SR_HIP(hipMemcpyAsync(nc.p, corpus_.p, (size_t)n_rows_ * ld_ * sizeof(half_t),
+                          hipMemcpyDeviceToDevice, stream_));
+    SR_HIP(hipMemcpyAsync(nl.p, live_.p, (size_t)n_rows_, hipMemcpyDeviceToDevice, stream_));
+  }
+  SR_HIP(hipStreamSynchronize(stream_));
+  std::swap(corpus_.p, nc.p);
+  std::swap(corpus_.bytes, nc.bytes);
+  std::swap(live_.p, nl.p);
+  std::swap(live_.bytes, nl.bytes);
+  capacity_ = cap;
+  live_host_.resize((size_t)cap, 0);
+}
+
+void Store::add_host(const float* vecs, int64_t n, int64_t* out_rows) {
+  SR_CHECK(n >= 0 && (n == 0 || vecs), "store.add: null vectors");
+  DeviceGuard g(device_);
+  ensure_capacity(n_rows_ + n);
+  for (int64_t off = 0; off < n; off += kAddChunk) {
+    const int64_t m = std::min(kAddChunk, n - off);
+    scratch_.reserve((size_t)m * dim_ * sizeof(float));
+    SR_HIP(hipMemcpyAsync(scratch_.p, vecs + off * dim_, (size_t)m * dim_ * sizeof(float),
+                          hipMemcpyHostToDevice, stream_));
+    const int64_t first = add_dev(scratch_.p, SR_DTYPE_F32, m, stream_);
+    if (out_rows)
+      for (int64_t i = 0; i < m; ++i) out_rows[off + i] = first + i;
+  }
+  SR_HIP(hipStreamSynchronize(stream_));
+}
+
+int64_t Store::add_dev(const void* vecs, int dtype, int64_t n, hipStream_t s) {
+  SR_CHECK(dtype == SR_DTYPE_F32 || dtype == SR_DTYPE_F16, "store.add: dtype must be f32 or f16");
+  DeviceGuard g(device_);
+  const int64_t first = n_rows_;
+  if (n <= 0) return first;
+  if (n_rows_ + n > capacity_) {
+    SR_HIP(hipStreamSynchronize(s));
+    ensure_capacity(n_rows_ + n);
+  }
+  launch_normalize_rows(vecs, dtype, n, dim_, corpus_.as<half_t>() + first * ld_, ld_, s);
+  SR_HIP(hipMemsetAsync(live_.as<uint8_t>() + first, 1, (size_t)n, s));
+  std::fill(live_host_.begin() + first, live_host_.begin() + first + n, 1);
+  n_rows_ += n;
+  n_live_ += n;
+  return first;
+}
+
+void Store::remove(const int64_t* rows, int64_t n) {
+  SR_CHECK(n > 0 && rows, "store.delete: ids is required");
+  for (int64_t i = 0; i < n; ++i)
+    SR_CHECK(rows[i] >= 0 && rows[i] < n_rows_ && live_host_[rows[i]],
+             "store.delete: unknown or already deleted row " + std::to_string(rows[i]));
+  DeviceGuard g(device_);
+  scratch_.reserve((size_t)n * sizeof(int64_t));
+  SR_HIP(hipMemcpyAsync(scratch_.p, rows, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
+  hipLaunchKernelGGL(clear_flags_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream_,
+                     live_.as<uint8_t>(), scratch_.as<int64_t>(), n);
+  SR_LAUNCH_CHECK();
+  SR_HIP(hipStreamSynchronize(stream_));
+  for (int64_t i = 0; i < n; ++i) {
+    if (live_host_[rows[i]]) {
+      live_host_[rows[i]] = 0;
+      --n_live_;
+    }
+  }
+}
+
+void Store::get(const int64_t* rows, int64_t n, float* out) {
+  if (n <= 0) return;
+  for (int64_t i = 0; i < n; ++i)
+    SR_CHECK(rows[i] >= 0 && rows[i] < n_rows_, "store.get: row out of range");
+  DeviceGuard g(device_);
+  scratch_.reserve((size_t)n * (sizeof(int64_t) + dim_ * sizeof(float)));
+  int64_t* drows = scratch_.as<int64_t>();
+  float* dout = reinterpret_cast<float*>(drows + n);
+  SR_HIP(hipMemcpyAsync(drows, rows, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
+  hipLaunchKernelGGL(f16_to_f32_rows_kernel, dim3((unsigned)n), dim3(256), 0, stream_,
+                     corpus_.as<half_t>(), ld_, drows, n, dim_, dout);
+  SR_LAUNCH_CHECK();
+  SR_HIP(hipMemcpyAsync(out, dout, (size_t)n * dim_ * sizeof(float), hipMemcpyDeviceToHost, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+}
+
+void Store::ensure_query_ws(int B) {
+  const int nq = (int)round_up(std::max(B, 1), kQueryBlock);
+  if (nq <= ws_queries_) return;
+  const int cap = select_capacity();
+  qbuf_.reserve((size_t)nq * ld_ * sizeof(half_t));
+  SR_HIP(hipMemsetAsync(qbuf_.p, 0, qbuf_.bytes, stream_));
+  cand_.reserve((size_t)kQueryBlock * cap * sizeof(uint64_t));
+  cnt_.reserve(kQueryBlock * sizeof(int));
+  tau_.reserve(kQueryBlock * sizeof(float));
+  overflow_.reserve(sizeof(int));
+  SR_HIP(hipStreamSynchronize(stream_));
+  ws_queries_ = nq;
+}
+
+void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
+                         int64_t row_offset, hipStream_t s, bool safe) {
+  const int cap = select_capacity();
+  uint64_t* cand = cand_.as<uint64_t>();
+  int* cnt = cnt_.as<int>();
+  float* tau = tau_.as<float>();
+  int* ovf = overflow_.as<int>();
+  const uint8_t* live = live_.as<uint8_t>();
+  const half_t* C = corpus_.as<half_t>();
+  const int64_t n = n_rows_;
+  if (n == 0) {
+    launch_fill_int(cnt, B, 0, s);
+    launch_topk_select(cand, cnt, cap, tau, B, k, ovf, true, out_sim, out_rows, row_offset, s);
+    return;
+  }
+  const int64_t dense = std::min<int64_t>(n, safe ? (int64_t)(cap - k) : kDenseRows);
+  launch_cosine_scan(true, C, ld_, live, 0, dense, qn, B, tau, cand, cnt, cap, s);
+  launch_fill_int(cnt, B, (int)dense, s);
+  launch_topk_select(cand, cnt, cap, tau, B, k, ovf, dense == n, out_sim, out_rows, row_offset, s);
+  const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(8, (cap - k) / (2 * k)));
+  int64_t r = dense;
+  while (r < n) {
+    const int64_t step = safe ? (int64_t)(cap - k) : std::max<int64_t>(r * growth, kDenseRows);
+    const int64_t next = std::min(n, r + step);
+    launch_cosine_scan(false, C, ld_, live, r, next, qn, B, tau, cand, cnt, cap, s);
+    launch_topk_select(cand, cnt, cap, tau, B, k, ovf, next == n, out_sim, out_rows, row_offset, s);
+    r = next;
+  }
+}
+
+void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
+                       int64_t* out_rows, int64_t row_offset, hipStream_t s) {
+  SR_CHECK(B >= 0, "store.search: negative batch");
+  SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "store.search: top_k must be in [1, 1024]");
+  SR_CHECK(k <= select_capacity() / 4, "store.search: top_k too large");
+  if (B == 0) return;
+  DeviceGuard g(device_);
+  if (!s) s = stream_;
+  ensure_query_ws(B);
+  half_t* qn = qbuf_.as<half_t>();
+  launch_normalize_rows(q, q_dtype, B, dim_, qn, ld_, s);
+  SR_HIP(hipMemsetAsync(overflow_.p, 0, sizeof(int), s));
+  for (int b0 = 0; b0 < B; b0 += kQueryBlock) {
+    const int bb = std::min(kQueryBlock, B - b0);
+    search_block(qn + (int64_t)b0 * ld_, bb, k, out_sim + (int64_t)b0 * k,
+                 out_rows + (int64_t)b0 * k, row_offset, s, false);
+  }
+  int ovf = 0;
+  SR_HIP(hipMemcpyAsync(&ovf, overflow_.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  SR_HIP(hipStreamSynchronize(s));
+  if (ovf) {
+    // Rare: a candidate list overflowed (row order adversarial to the threshold).  Redo exactly.
+    for (int b0 = 0; b0 < B; b0 += kQueryBlock) {
+      const int bb = std::min(kQueryBlock, B - b0);
+      search_block(qn + (int64_t)b0 * ld_, bb, k, out_sim + (int64_t)b0 * k,
+                   out_rows + (int64_t)b0 * k, row_offset, s, true);
+    }
+  }
+}
+
+void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows) {
+  SR_CHECK(B >= 0 && (B == 0 || (q && out_dist && out_rows)), "store.search: null buffer");
+  if (B == 0) return;
+  DeviceGuard g(device_);
+  const size_t qb = (size_t)B * dim_ * sizeof(float);
+  const size_t ob = (size_t)B * k * (sizeof(float) + sizeof(int64_t));
+  qstage_.reserve(qb + ob);
+  float* dq = qstage_.as<float>();
+  float* dsim = reinterpret_cast<float*>(qstage_.as<char>() + qb);
+  int64_t* drows = reinterpret_cast<int64_t*>(dsim + (size_t)B * k);
+  SR_HIP(hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, stream_));
+  search_dev(dq, SR_DTYPE_F32, B, k, dsim, drows, 0, stream_);
+  SR_HIP(hipMemcpyAsync(out_dist, dsim, (size_t)B * k * sizeof(float), hipMemcpyDeviceToHost, stream_));
+  SR_HIP(hipMemcpyAsync(out_rows, drows, (size_t)B * k * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+  for (int64_t i = 0; i < (int64_t)B * k; ++i)
+    out_dist[i] = out_rows[i] >= 0 ? 1.0f - out_dist[i] : INFINITY;
+}
+
+// Snapshot format (little endian): "SRMISTO1", int32 dim, int64 n_rows, n_rows x dim fp16
+// (normalised rows, unpadded), n_rows bytes of live flags.
+void Store::save(const char* path) {
+  DeviceGuard g(device_);
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw Error(SR_ERR_IO, std::string("store.save: cannot open ") + path);
+  f.write("SRMISTO1", 8);
+  const int32_t d = dim_;
+  f.write(reinterpret_cast<const char*>(&d), 4);
+  f.write(reinterpret_cast<const char*>(&n_rows_), 8);
+  std::vector<half_t> buf;
+  const int64_t chunk = 1 << 16;
+  for (int64_t r = 0; r < n_rows_; r += chunk) {
+    const int64_t m = std::min(chunk, n_rows_ - r);
+    buf.resize((size_t)m * dim_);
+    SR_HIP(hipMemcpy2D(buf.data(), dim_ * sizeof(half_t), corpus_.as<half_t>() + r * ld_,
+                       ld_ * sizeof(half_t), dim_ * sizeof(half_t), (size_t)m,
+                       hipMemcpyDeviceToHost));
+    f.write(reinterpret_cast<const char*>(buf.data()), (std::streamsize)(buf.size() * sizeof(half_t)));
+  }
+  f.write(reinterpret_cast<const char*>(live_host_.data()), (std::streamsize)n_rows_);
+  if (!f) throw Error(SR_ERR_IO, std::string("store.save: write failed for ") + path);
+}
+
+Store* Store::load(const char* path, int device) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw Error(SR_ERR_IO, std::string("store.load: cannot open ") + path);
+  char magic[8];
+  f.read(magic, 8);
+  if (!f || std::memcmp(magic, "SRMISTO1", 8) != 0)
+    throw Error(SR_ERR_IO, std::string("store.load: not a store snapshot: ") + path);
+  int32_t d = 0;
+  int64_t n = 0;
+  f.read(reinterpret_cast<char*>(&d), 4);
+  f.read(reinterpret_cast<char*>(&n), 8);
+  if (!f || d <= 0 || n < 0) throw Error(SR_ERR_IO, "store.load: corrupt header");
+  Store* s = new Store(d, device, std::max<int64_t>(n, 1024));
+  try {
+    DeviceGuard g(device);
+    std::vector<half_t> buf;
+    const int64_t chunk = 1 << 16;
+    for (int64_t r = 0; r < n; r += chunk) {
+      const int64_t m = std::min(chunk, n - r);
+      buf.resize((size_t)m * d);
+      f.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(buf.size() * sizeof(half_t)));
+      if (!f) throw Error(SR_ERR_IO, "store.load: truncated rows");
+      SR_HIP(hipMemcpy2D(s->corpus_.as<half_t>() + r * s->ld_, s->ld_ * sizeof(half_t), buf.data(),
+                         d * sizeof(half_t), d * sizeof(half_t), (size_t)m, hipMemcpyHostToDevice));
+    }
+    if (s->ld_ > d && n > 0)
+      SR_HIP(hipMemset2D(s->corpus_.as<half_t>() + d, s->ld_ * sizeof(half_t), 0,
+                         (s->ld_ - d) * sizeof(half_t), (size_t)n));
+    f.read(reinterpret_cast<char*>(s->live_host_.data()), (std::streamsize)n);
+    if (!f) throw Error(SR_ERR_IO, "store.load: truncated live flags");
+    SR_HIP(hipMemcpy(s->live_.p, s->live_host_.data(), (size_t)n, hipMemcpyHostToDevice));
+    s->n_rows_ = n;
+    s->n_live_ = 0;
+    for (int64_t i = 0; i < n; ++i) s->n_live_ += s->live_host_[i] ? 1 : 0;
+  } catch (...) {
+    delete s;
+    throw;
+  }
+  return s;
+}
+
+void Store::compact(int64_t* old_to_new) {
+  DeviceGuard g(device_);
+  std::vector<int64_t> keep;
+  keep.reserve((size_t)n_live_);
+  for (int64_t r = 0; r < n_rows_; ++r) {
+    if (live_host_[r]) {
+      if (old_to_new) old_to_new[r] = (int64_t)keep.size();
+      keep.push_back(r);
+    } else if (old_to_new) {
+      old_to_new[r] = -1;
+    }
+  }
+  const int64_t m = (int64_t)keep.size();
+  DevBuf nc, rows;
+  nc.reserve((size_t)std::max<int64_t>(capacity_, 1) * ld_ * sizeof(half_t));
+  if (m > 0) {
+    rows.reserve((size_t)m * sizeof(int64_t));
+    SR_HIP(hipMemcpyAsync(rows.p, keep.data(), (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)m), dim3(64), 0, stream_,
+                       corpus_.as<half_t>(), ld_, rows.as<int64_t>(), m, nc.as<half_t>());
+    SR_LAUNCH_CHECK();
+  }
+  SR_HIP(hipMemsetAsync(live_.p, 0, (size_t)capacity_, stream_));
+  if (m > 0) SR_HIP(hipMemsetAsync(live_.p, 1, (size_t)m, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+  std::swap(corpus_.p, nc.p);
+  std::swap(corpus_.bytes, nc.bytes);
+  std::fill(live_host_.begin(), live_host_.end(), 0);
+  std::fill(live_host_.begin(), live_host_.begin() + m, 1);
+  n_rows_ = m;
+  n_live_ = m;
+}
+
+}  // namespace sr
