@@ -1,0 +1,283 @@
+"""Benchmark of the embed -> exact top-K -> cross-encoder rerank hot path on MI355X.
+
+BASELINE.json metric: "queries/sec (embed+ANN top-10+rerank) over 10M x 768-d @1/2/4/8 GPU;
+recall@10".  One step = one batch of B synthetic queries per rank through the whole path:
+  bge-base-en (768-d, 12L) query embed at S=32  ->  exact cosine top-100 over the 10M x 768 fp16
+  corpus (row-sharded over the ranks)  ->  bge-reranker-base (XLM-R base) cross-encoder on the
+  100 candidates per query at S_pair=128  ->  top-10.
+Weights are seeded random (no checkpoints offline), inputs synthetic.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
+(one rank per GPU, RCCL).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "super-rag_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_F16_TFLOPS = 2500.0    # dense fp16/bf16 MFMA spec (no sparsity)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--corpus-rows", type=int, default=10_000_000)
+    ap.add_argument("--batch", type=int, default=256, help="queries per rank per step")
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--k-cand", type=int, default=100)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--q-len", type=int, default=32)
+    ap.add_argument("--pair-len", type=int, default=128)
+    ap.add_argument("--passage-len", type=int, default=94)
+    ap.add_argument("--embed-model", default="bge-base-en")
+    ap.add_argument("--rerank-model", default="bge-reranker-base")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-queries", type=int, default=2)
+    ap.add_argument("--cpu-rows", type=int, default=200_000)
+    ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
+    return ap.parse_args()
+
+
+def gen_corpus_chunk(r0, r1, dim, centers, dev):
+    """Rows r0..r1 of the clustered synthetic corpus: x_i = c_{i mod 1024} + 0.5 eps_i, with eps
+    drawn per 1M-row block from a generator seeded by the block index (shard-independent)."""
+    out = torch.empty((r1 - r0, dim), dtype=torch.float32, device=dev)
+    blk = 1 << 20
+    r = r0
+    while r < r1:
+        b = r // blk
+        b_end = min(r1, (b + 1) * blk)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1_000_003 + b)
+        eps = torch.randn(((b + 1) * blk - b * blk, dim), generator=g, device=dev)
+        lo, hi = r - b * blk, b_end - b * blk
+        idx = torch.arange(r, b_end, device=dev) % centers.shape[0]
+        out[r - r0:b_end - r0] = centers[idx] + 0.5 * eps[lo:hi]
+        r = b_end
+    return out
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from super_rag_amd import _native as N
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    from super_rag_amd.pipeline import SearchPipeline
+    from super_rag_amd.store import NativeStore
+
+    t_setup = time.time()
+    es, rs = MODELS[a.embed_model], MODELS[a.rerank_model]
+    assert es.hidden == a.dim
+    w_embed = random_weights(es, seed=11, style="hf")
+    w_rerank = random_weights(rs, seed=12, style="hf")
+    embedder = Encoder(es, device=local, weights=w_embed, max_tokens=a.batch * a.q_len)
+    reranker = Encoder(rs, device=local, weights=w_rerank, max_tokens=524288)
+
+    # ---- corpus shard (rows [r0, r1) of the global 10M) -----------------------------------------
+    N_total = a.corpus_rows
+    per = (N_total + world - 1) // world
+    r0, r1 = rank * per, min(N_total, (rank + 1) * per)
+    gc = torch.Generator(device="cpu")
+    gc.manual_seed(0)
+    centers = torch.randn((1024, a.dim), generator=gc).to(dev)
+    store = NativeStore(a.dim, device=local, capacity=r1 - r0)
+    step_rows = 1 << 20
+    for c0 in range(r0, r1, step_rows):
+        chunk = gen_corpus_chunk(c0, min(r1, c0 + step_rows), a.dim, centers, dev)
+        store.add_dev(chunk)
+        del chunk
+    torch.cuda.synchronize()
+    # replicated passage token table for the cross-encoder (content tokens, no specials)
+    gp = torch.Generator(device=dev)
+    gp.manual_seed(5)
+    p_tok = torch.randint(1000, rs.vocab_size, (N_total, a.passage_len), generator=gp, device=dev,
+                          dtype=torch.int32)
+    p_len = torch.full((N_total,), a.passage_len, dtype=torch.int32, device=dev)
+
+    # ---- resident synthetic query batches ------------------------------------------------------
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(2 + rank)
+    batches = []
+    for _ in range(a.batches):
+        ids = torch.randint(1000, es.vocab_size, (a.batch, a.q_len), generator=gq, device=dev,
+                            dtype=torch.int32)
+        ids[:, 0] = es.bos_id
+        ids[:, -1] = es.eos_id
+        mask = torch.ones_like(ids)
+        lq = a.q_len - 2
+        qtok = torch.randint(1000, rs.vocab_size, (a.batch, lq), generator=gq, device=dev,
+                             dtype=torch.int32)
+        qlen = torch.full((a.batch,), lq, dtype=torch.int32, device=dev)
+        batches.append((ids, mask, qtok, qlen))
+    pipe = SearchPipeline(embedder, reranker, store, p_tok, p_len, k_candidates=a.k_cand,
+                          k_final=a.k, pair_len=a.pair_len, shard_offset=r0)
+    setup_s = time.time() - t_setup
+
+    # ---- warmup + timed region -----------------------------------------------------------------
+    for i in range(a.warmup):
+        pipe.run(*batches[i % a.batches])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    N.profile_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        res = pipe.run(*batches[i % a.batches])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    N.profile_enable(False)
+    prof = N.profile_read()
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    queries = world * a.batch * a.steps
+    value = queries / dt
+
+    # ---- recall@10 of the search stage vs exact fp32 (outside the timed region) -----------------
+    recall = None
+    if world == 1:
+        ids, mask, _, _ = batches[0]
+        nq = min(32, a.batch)
+        q16 = embedder.embed_dev(ids[:nq], mask[:nq], fp16=False)
+        _, rows = store.search_dev(q16, a.k)
+        best_s = torch.full((nq, 0), -2.0, device=dev)
+        best_r = torch.zeros((nq, 0), dtype=torch.int64, device=dev)
+        for c0 in range(0, N_total, step_rows):
+            x = gen_corpus_chunk(c0, min(N_total, c0 + step_rows), a.dim, centers, dev)
+            s = q16 @ torch.nn.functional.normalize(x, dim=1).T
+            best_s = torch.cat([best_s, s], 1)
+            best_r = torch.cat([best_r, torch.arange(c0, c0 + x.shape[0], device=dev).expand(nq, -1)], 1)
+            top = best_s.topk(a.k, dim=1)
+            best_s, best_r = top.values, best_r.gather(1, top.indices)
+        hit = sum(len(set(rows[i].tolist()) & set(best_r[i].tolist())) for i in range(nq))
+        recall = hit / (nq * a.k)
+
+    # ---- roofline of the dominant kernel -------------------------------------------------------
+    dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
+    avg_ms = dom["total_ms"] / dom["launches"]
+    if dom["flops"] > 0 and not dom_name.startswith("cosine_scan"):
+        achieved = dom["flops"] / (dom["total_ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_F16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": None}
+    else:
+        achieved = dom["bytes"] / (dom["total_ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None}
+    roof.update({"kernel": dom_name, "launches": dom["launches"], "avg_ms": round(avg_ms, 4),
+                 "per_launch": (f"{dom['flops'] / dom['launches']:.4g} FLOP" if roof["bound"] == "mfma"
+                                else f"{dom['bytes'] / dom['launches']:.4g} B")})
+    step_ms = dt / a.steps * 1e3
+    kern = {k: {"ms_per_step": round(v["total_ms"] / a.steps, 3), "launches": v["launches"],
+                ("tflops" if v["flops"] > 0 else "gbs"):
+                    round((v["flops"] / 1e12 if v["flops"] > 0 else v["bytes"] / 1e9) / (v["total_ms"] * 1e-3), 1)}
+            for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["total_ms"])}
+    scan = {k: v for k, v in prof.items() if k.startswith("cosine_scan")}
+    if scan:
+        sb = sum(v["bytes"] for v in scan.values())
+        sm = sum(v["total_ms"] for v in scan.values())
+        search_roof = {"bound": "hbm", "achieved": round(sb / (sm * 1e-3) / 1e9, 1),
+                       "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                       "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    else:
+        search_roof = None
+
+    # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) ----------------------------
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a, es, rs, w_embed, w_rerank, centers.cpu(), batches[0], p_tok, N_total)
+
+    line = {
+        "metric": "queries/sec (embed+ANN top-10+rerank) over 10M x 768-d; recall@10",
+        "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f16", "data": "synthetic",
+        "config": {"workload": "config4: bge-base-en embed (S=32) + exact cosine top-100 over "
+                               f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
+                               f"rerank of 100 pairs (S={a.pair_len}) -> top-{a.k}",
+                   "queries_per_rank": a.batch, "global_batch": world * a.batch,
+                   "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
+                   "parallelism": f"corpus row-shard x{world}, query DP x{world}"},
+        "recall_at_10": recall,
+        "roofline": roof,
+        "search_roofline": search_roof,
+        "cpu_baseline": cpu,
+        "kernels": kern,
+        "setup_s": round(setup_s, 1),
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total):
+    """Oracle (oracle/*, the CPU restatement) timed on host cores on a bounded sample."""
+    from oracle import encoder_ref as R
+    from oracle.cosine_topk import cosine_topk
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    nq = a.cpu_queries
+    cfg = lambda s: R.RefConfig(s.vocab_size, s.hidden, s.layers, s.heads, s.intermediate,
+                                s.max_position, s.type_vocab, s.ln_eps, s.position_offset,
+                                s.classifier, s.num_labels)
+    ids, mask, qtok, qlen = (t[:nq].cpu().numpy() for t in batch)
+    wt_e = {k: torch.from_numpy(v) for k, v in w_embed.items()}
+    wt_r = {k: torch.from_numpy(v) for k, v in w_rerank.items()}
+    t0 = time.perf_counter()
+    q = R.embed(cfg(es), wt_e, ids, mask)
+    t_embed = time.perf_counter() - t0
+    g = torch.Generator().manual_seed(1)
+    rows = a.cpu_rows
+    x = (centers[torch.arange(rows) % centers.shape[0]]
+         + 0.5 * torch.randn((rows, a.dim), generator=g)).numpy()
+    t0 = time.perf_counter()
+    _, cand = cosine_topk(x, q, a.k_cand)
+    t_search = (time.perf_counter() - t0) * (N_total / rows)
+    pt = p_tok[torch.from_numpy(np.clip(cand, 0, None).reshape(-1)).to(p_tok.device)].view(nq, a.k_cand, -1).cpu().numpy()
+    pids, pmask, _ = R.pack_pairs(qtok, qlen, pt.reshape(nq * a.k_cand, -1),
+                                  np.full(nq * a.k_cand, pt.shape[-1]),
+                                  np.arange(nq * a.k_cand).reshape(nq, a.k_cand), a.pair_len, 0,
+                                  rs.bos_id, rs.eos_id, rs.pad_id)
+    t0 = time.perf_counter()
+    R.cross_logits(cfg(rs), wt_r, pids, pmask)
+    t_rerank = time.perf_counter() - t0
+    per_q = (t_embed + t_search + t_rerank) / nq
+    return {"value": round(1.0 / per_q, 4), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": (f"{nq} queries end-to-end through the oracle (torch-CPU fp32 encoders, "
+                       f"numpy fp64 exact cosine top-{a.k_cand}); search timed over {rows} rows and "
+                       f"scaled x{N_total / rows:.0f} to {N_total} rows"),
+            "stage_s_per_query": {"embed": round(t_embed / nq, 4),
+                                  "search_10M": round(t_search / nq, 3),
+                                  "rerank": round(t_rerank / nq, 3)}}
+
+
+if __name__ == "__main__":
+    main()

@@ -18,8 +18,10 @@
  *     failure; the message is available from sr_last_error() (thread-local, valid until the next
  *     call on the same thread).
  *   - Host pointers are caller-owned and only read/written during the call.  Device pointers
- *     (the *_dev entry points) must live on the object's device; `stream` is a hipStream_t
- *     (NULL = the object's own stream) and the call is asynchronous on it unless stated.
+ *     (the *_dev entry points) must live on the object's device; `stream` is a hipStream_t used
+ *     as given (NULL = the HIP null stream, which is what PyTorch reports for its default
+ *     stream) and the call is asynchronous on it unless stated.  Host-pointer entry points run
+ *     on the object's own stream and are blocking.
  *   - Objects are internally locked: every entry point is safe to call from several host threads.
  *     The Python binding calls through ctypes.CDLL, which releases the GIL for the duration.
  *   - Scores follow SeekDB's cosine semantics: dist = 1 - cos(q, x)  (lower is better,

@@ -36,6 +36,7 @@ Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(
   max_tokens_ = cfg.max_tokens > 0 ? cfg.max_tokens : 262144;
   DeviceGuard g(device_);
   SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  SR_HIP(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
 
   const int64_t D = d, F = cfg.intermediate;
   register_target("embeddings.word_embeddings.weight", wemb_, (int64_t)cfg.vocab_size * D, true);
@@ -73,8 +74,12 @@ Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(
 }
 
 Encoder::~Encoder() {
+  (void)hipSetDevice(device_);
+  if (done_) {
+    (void)hipEventSynchronize(done_);
+    (void)hipEventDestroy(done_);
+  }
   if (stream_) {
-    (void)hipSetDevice(device_);
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
   }
@@ -100,6 +105,8 @@ void Encoder::set_weight(const std::string& name, const float* data, int64_t num
                                  " elements, expected " + std::to_string(t.numel));
   SR_CHECK(data != nullptr, "encoder: null weight data");
   DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
   if (t.f16) {
     std::vector<half_t> h((size_t)numel);
     for (int64_t i = 0; i < numel; ++i) h[i] = (half_t)data[i];
@@ -118,6 +125,7 @@ std::string Encoder::missing() const {
 
 void Encoder::ensure_ws(int64_t tokens, int B) {
   if (tokens <= ws_tokens_) return;
+  SR_HIP(hipEventSynchronize(done_));  // the previous call may still use the old workspace
   const int64_t d = cfg_.hidden, F = cfg_.intermediate;
   ids_.reserve((size_t)tokens * sizeof(int32_t));
   mask_.reserve((size_t)tokens * sizeof(int32_t));
@@ -147,11 +155,14 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
   if (!miss.empty()) throw Error(SR_ERR_STATE, "encoder: weight not set: " + miss);
   if (B == 0) return;
   DeviceGuard g(device_);
-  if (!s) s = stream_;
+  // s == nullptr is the HIP null stream (torch's default stream): use it as-is.
+  begin(s);
   const int d = cfg_.hidden, F = cfg_.intermediate, H = cfg_.heads;
   const int64_t seqs_per_chunk = std::max<int64_t>(1, max_tokens_ / S);
   const int64_t chunk_tokens = std::min<int64_t>((int64_t)B, seqs_per_chunk) * S;
   ensure_ws(chunk_tokens, B);
+  if (mode == 1 && clst_.bytes < (size_t)std::min<int64_t>(B, seqs_per_chunk) * d * sizeof(float))
+    SR_HIP(hipEventSynchronize(done_));
   if (mode == 1) clst_.reserve((size_t)std::min<int64_t>(B, seqs_per_chunk) * d * sizeof(float));
   half_t* h16 = h16_.as<half_t>();
   float* h32 = h32_.as<float>();
@@ -197,6 +208,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
                         reinterpret_cast<float*>(out) + b0 * cfg_.num_labels, s);
     }
   }
+  end(s);
 }
 
 void Encoder::forward_host(const int32_t* ids, const int32_t* mask, const int32_t* types, int B,

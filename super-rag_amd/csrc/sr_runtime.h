@@ -76,6 +76,12 @@ class Store {
   std::mutex mu;
 
  private:
+  // Cross-stream ordering: every operation first makes its stream wait for the previous
+  // operation's completion event, and records the event when it has enqueued its work, so calls
+  // on different streams (the object's own stream, torch's stream, the null stream) never race
+  // on the corpus or the shared workspaces.
+  void begin(hipStream_t s) { SR_HIP(hipStreamWaitEvent(s, done_, 0)); }
+  void end(hipStream_t s) { SR_HIP(hipEventRecord(done_, s)); }
   void ensure_capacity(int64_t rows);
   void ensure_query_ws(int B);
   // Runs the chunked scan/select schedule for one block of <= 256 normalised queries.
@@ -87,6 +93,7 @@ class Store {
   DevBuf corpus_, live_;
   std::vector<uint8_t> live_host_;
   hipStream_t stream_ = nullptr;
+  hipEvent_t done_ = nullptr;
   // search workspace
   DevBuf qbuf_, qstage_, cand_, cnt_, tau_, overflow_, osim_, orows_, scratch_;
   int ws_queries_ = 0;
@@ -120,6 +127,8 @@ class Encoder {
   struct Layer {
     DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, w1, b1, w2, b2, ln2g, ln2b;
   };
+  void begin(hipStream_t s) { SR_HIP(hipStreamWaitEvent(s, done_, 0)); }
+  void end(hipStream_t s) { SR_HIP(hipEventRecord(done_, s)); }
   void register_target(const std::string& name, DevBuf& buf, int64_t numel, bool f16,
                        int64_t offset_elems = 0, int64_t total_elems = -1);
   void ensure_ws(int64_t tokens, int B);
@@ -127,6 +136,7 @@ class Encoder {
   sr_encoder_config cfg_;
   int device_;
   hipStream_t stream_ = nullptr;
+  hipEvent_t done_ = nullptr;
   int64_t max_tokens_;
   DevBuf wemb_, pemb_, temb_, embg_, embb_, wc_, bc_, wout_, bout_;
   std::vector<Layer> layers_;

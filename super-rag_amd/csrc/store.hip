@@ -48,12 +48,17 @@ Store::Store(int dim, int device, int64_t capacity) : dim_(dim), device_(device)
   ld_ = (int)round_up(dim, 64);
   DeviceGuard g(device_);
   SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  SR_HIP(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   ensure_capacity(capacity > 0 ? capacity : 1024);
 }
 
 Store::~Store() {
+  (void)hipSetDevice(device_);
+  if (done_) {
+    (void)hipEventSynchronize(done_);
+    (void)hipEventDestroy(done_);
+  }
   if (stream_) {
-    (void)hipSetDevice(device_);
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
   }
@@ -84,6 +89,7 @@ void Store::ensure_capacity(int64_t rows) {
 void Store::add_host(const float* vecs, int64_t n, int64_t* out_rows) {
   SR_CHECK(n >= 0 && (n == 0 || vecs), "store.add: null vectors");
   DeviceGuard g(device_);
+  begin(stream_);
   ensure_capacity(n_rows_ + n);
   for (int64_t off = 0; off < n; off += kAddChunk) {
     const int64_t m = std::min(kAddChunk, n - off);
@@ -102,12 +108,14 @@ int64_t Store::add_dev(const void* vecs, int dtype, int64_t n, hipStream_t s) {
   DeviceGuard g(device_);
   const int64_t first = n_rows_;
   if (n <= 0) return first;
+  begin(s);
   if (n_rows_ + n > capacity_) {
     SR_HIP(hipStreamSynchronize(s));
     ensure_capacity(n_rows_ + n);
   }
   launch_normalize_rows(vecs, dtype, n, dim_, corpus_.as<half_t>() + first * ld_, ld_, s);
   SR_HIP(hipMemsetAsync(live_.as<uint8_t>() + first, 1, (size_t)n, s));
+  end(s);
   std::fill(live_host_.begin() + first, live_host_.begin() + first + n, 1);
   n_rows_ += n;
   n_live_ += n;
@@ -120,11 +128,14 @@ void Store::remove(const int64_t* rows, int64_t n) {
     SR_CHECK(rows[i] >= 0 && rows[i] < n_rows_ && live_host_[rows[i]],
              "store.delete: unknown or already deleted row " + std::to_string(rows[i]));
   DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
   scratch_.reserve((size_t)n * sizeof(int64_t));
   SR_HIP(hipMemcpyAsync(scratch_.p, rows, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
   hipLaunchKernelGGL(clear_flags_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream_,
                      live_.as<uint8_t>(), scratch_.as<int64_t>(), n);
   SR_LAUNCH_CHECK();
+  end(stream_);
   SR_HIP(hipStreamSynchronize(stream_));
   for (int64_t i = 0; i < n; ++i) {
     if (live_host_[rows[i]]) {
@@ -139,6 +150,8 @@ void Store::get(const int64_t* rows, int64_t n, float* out) {
   for (int64_t i = 0; i < n; ++i)
     SR_CHECK(rows[i] >= 0 && rows[i] < n_rows_, "store.get: row out of range");
   DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
   scratch_.reserve((size_t)n * (sizeof(int64_t) + dim_ * sizeof(float)));
   int64_t* drows = scratch_.as<int64_t>();
   float* dout = reinterpret_cast<float*>(drows + n);
@@ -147,12 +160,14 @@ void Store::get(const int64_t* rows, int64_t n, float* out) {
                      corpus_.as<half_t>(), ld_, drows, n, dim_, dout);
   SR_LAUNCH_CHECK();
   SR_HIP(hipMemcpyAsync(out, dout, (size_t)n * dim_ * sizeof(float), hipMemcpyDeviceToHost, stream_));
+  end(stream_);
   SR_HIP(hipStreamSynchronize(stream_));
 }
 
 void Store::ensure_query_ws(int B) {
   const int nq = (int)round_up(std::max(B, 1), kQueryBlock);
   if (nq <= ws_queries_) return;
+  SR_HIP(hipEventSynchronize(done_));  // the previous search may still use the old workspace
   const int cap = select_capacity();
   qbuf_.reserve((size_t)nq * ld_ * sizeof(half_t));
   SR_HIP(hipMemsetAsync(qbuf_.p, 0, qbuf_.bytes, stream_));
@@ -201,7 +216,8 @@ void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
   SR_CHECK(k <= select_capacity() / 4, "store.search: top_k too large");
   if (B == 0) return;
   DeviceGuard g(device_);
-  if (!s) s = stream_;
+  // s == nullptr is the HIP null stream (what torch reports for its default stream): use as-is.
+  begin(s);
   ensure_query_ws(B);
   half_t* qn = qbuf_.as<half_t>();
   launch_normalize_rows(q, q_dtype, B, dim_, qn, ld_, s);
@@ -213,6 +229,7 @@ void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
   }
   int ovf = 0;
   SR_HIP(hipMemcpyAsync(&ovf, overflow_.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  end(s);
   SR_HIP(hipStreamSynchronize(s));
   if (ovf) {
     // Rare: a candidate list overflowed (row order adversarial to the threshold).  Redo exactly.
@@ -221,6 +238,7 @@ void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
       search_block(qn + (int64_t)b0 * ld_, bb, k, out_sim + (int64_t)b0 * k,
                    out_rows + (int64_t)b0 * k, row_offset, s, true);
     }
+    end(s);
   }
 }
 
@@ -247,6 +265,8 @@ void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* 
 // (normalised rows, unpadded), n_rows bytes of live flags.
 void Store::save(const char* path) {
   DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
   std::ofstream f(path, std::ios::binary);
   if (!f) throw Error(SR_ERR_IO, std::string("store.save: cannot open ") + path);
   f.write("SRMISTO1", 8);
@@ -310,6 +330,8 @@ Store* Store::load(const char* path, int device) {
 
 void Store::compact(int64_t* old_to_new) {
   DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
   std::vector<int64_t> keep;
   keep.reserve((size_t)n_live_);
   for (int64_t r = 0; r < n_rows_; ++r) {
@@ -332,6 +354,7 @@ void Store::compact(int64_t* old_to_new) {
   }
   SR_HIP(hipMemsetAsync(live_.p, 0, (size_t)capacity_, stream_));
   if (m > 0) SR_HIP(hipMemsetAsync(live_.p, 1, (size_t)m, stream_));
+  end(stream_);
   SR_HIP(hipStreamSynchronize(stream_));
   std::swap(corpus_.p, nc.p);
   std::swap(corpus_.bytes, nc.bytes);
