@@ -130,6 +130,9 @@ typedef struct sr_encoder_config {
   int classifier;       /* 0: none; 1: RoBERTa classification head (dense+tanh+out_proj)       */
   int num_labels;       /* classifier outputs (1 for bge-reranker)                             */
   int max_tokens;       /* workspace size in tokens per launch chunk (0 = default 262144)      */
+  int residual_fp16;    /* 0: fp32 residual stream (embeddings, <= 1e-3 rel error);
+                           1: fp16 residual stream (cross-encoders: ~2.5x less LayerNorm and
+                              epilogue traffic, ranking-level fidelity)                         */
 } sr_encoder_config;
 
 int sr_encoder_create(const sr_encoder_config* cfg, int device, sr_encoder** out);

@@ -10,7 +10,9 @@
 //   f    = GELU(GEMM(h16, W1) + b1)               fp16  [M, F]      (K4, GELU epilogue)
 //   y32  = GEMM(f, W2) + b2 + h32                 fp32              (K4, residual epilogue)
 //   h    = LayerNorm(y32)                         fp16 + fp32       (K6)
-// The residual stream stays fp32 (fp16 residuals cost ~2x the embedding error).
+// The residual stream is fp32 by default (fp16 residuals cost ~2x the embedding error,
+// DESIGN.md); cross-encoders may run it in fp16 (config.residual_fp16).  With CLS pooling or a
+// classification head the last layer is computed for the CLS rows only.
 // Embedding mode pools (CLS / masked mean) and L2-normalises (K7); cross-encoder mode applies the
 // RoBERTa classification head: tanh(GEMM(h16[CLS rows], Wc) + bc) (fp32) . Wout + bout (K4 + K8).
 #include <algorithm>
@@ -168,9 +170,17 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
   float* h32 = h32_.as<float>();
   half_t* qkv = qkv_.as<half_t>();
   half_t* ctx = ctx_.as<half_t>();
-  float* y32 = y32_.as<float>();
+  void* y = y32_.p;  // bias + residual sum: fp32, or fp16 with an fp16 residual stream
   half_t* ffn = ffn_.as<half_t>();
   int32_t* pos = pos_.as<int32_t>();
+  const bool res16 = cfg_.residual_fp16 != 0;
+  const void* hres = res16 ? (const void*)h16 : (const void*)h32;  // residual operand
+  float* h32w = res16 ? nullptr : h32;
+  const int epi_res = res16 ? EPI_BIAS_RES_F16 : EPI_BIAS_RES_F32;
+  // Only the first token's final state is consumed (CLS pooling / classification head): the last
+  // layer runs attention for query row 0 only and its O-projection, LayerNorms and FFN on the
+  // B CLS rows (exact: every other row of the last layer is dead).
+  const bool cls_only = (mode == 1) || (pool == SR_POOL_CLS);
 
   for (int64_t b0 = 0; b0 < B; b0 += seqs_per_chunk) {
     const int nb = (int)std::min<int64_t>(seqs_per_chunk, B - b0);
@@ -181,28 +191,34 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
     launch_positions(cids, pos, nb, S, cfg_.position_offset, s);
     launch_embed_ln(cids, pos, ctypes, wemb_.as<half_t>(), pemb_.as<half_t>(), temb_.as<half_t>(),
                     embg_.as<float>(), embb_.as<float>(), cfg_.ln_eps, M, d, cfg_.vocab_size,
-                    cfg_.max_position, cfg_.type_vocab, h16, h32, s);
-    for (const Layer& L : layers_) {
+                    cfg_.max_position, cfg_.type_vocab, h16, h32w, s);
+    for (size_t l = 0; l < layers_.size(); ++l) {
+      const Layer& L = layers_[l];
+      const bool last = cls_only && l + 1 == layers_.size();
       launch_gemm(EPI_BIAS_F16, h16, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
                   3 * d, M, 3 * d, d, s);
-      launch_attention(qkv, cmask, ctx, nb, S, d, H, s);
-      launch_gemm(EPI_BIAS_RES_F32, ctx, d, L.wo.as<half_t>(), L.bo.as<float>(), h32, d, y32, d,
-                  M, d, d, s);
-      launch_layernorm(y32, L.ln1g.as<float>(), L.ln1b.as<float>(), cfg_.ln_eps, M, d, h16, h32, s);
+      // rows of the rest of the block: all M tokens, or the nb CLS rows (compact) in the last layer
+      const int Mr = last ? nb : M;
+      launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
+      launch_gemm(epi_res, ctx, d, L.wo.as<half_t>(), L.bo.as<float>(), hres,
+                  last ? (int64_t)S * d : d, y, d, Mr, d, d, s);
+      launch_layernorm(y, res16, L.ln1g.as<float>(), L.ln1b.as<float>(), cfg_.ln_eps, Mr, d, h16,
+                       h32w, s);
       launch_gemm(EPI_BIAS_GELU_F16, h16, d, L.w1.as<half_t>(), L.b1.as<float>(), nullptr, 0, ffn,
-                  F, M, F, d, s);
-      launch_gemm(EPI_BIAS_RES_F32, ffn, F, L.w2.as<half_t>(), L.b2.as<float>(), h32, d, y32, d, M,
-                  d, F, s);
-      launch_layernorm(y32, L.ln2g.as<float>(), L.ln2b.as<float>(), cfg_.ln_eps, M, d, h16, h32, s);
+                  F, Mr, F, d, s);
+      launch_gemm(epi_res, ffn, F, L.w2.as<half_t>(), L.b2.as<float>(), hres, d, y, d, Mr, d, F, s);
+      launch_layernorm(y, res16, L.ln2g.as<float>(), L.ln2b.as<float>(), cfg_.ln_eps, Mr, d, h16,
+                       h32w, s);
     }
+    // final states: row b*S of each sequence, or row b (compact) after a CLS-only last layer
+    const int Sf = cls_only ? 1 : S;
     if (mode == 0) {
       const size_t esz = out_dtype == SR_DTYPE_F32 ? sizeof(float) : sizeof(half_t);
-      launch_pool_l2(h32, cmask, nb, S, d, pool,
+      launch_pool_l2(res16 ? (const void*)h16 : (const void*)h32, res16, cmask, nb, Sf, d, pool,
                      reinterpret_cast<char*>(out) + (size_t)b0 * ld_out * esz, out_dtype, ld_out, s);
     } else {
       float* t = clst_.as<float>();
-      // CLS rows of h16 are rows b*S: a strided GEMM operand (lda = S*d).
-      launch_gemm(EPI_BIAS_TANH_F32, h16, (int64_t)S * d, wc_.as<half_t>(), bc_.as<float>(),
+      launch_gemm(EPI_BIAS_TANH_F32, h16, (int64_t)Sf * d, wc_.as<half_t>(), bc_.as<float>(),
                   nullptr, 0, t, d, nb, d, d, s);
       launch_cls_logits(t, wout_.as<float>(), bout_.as<float>(), nb, d, cfg_.num_labels,
                         reinterpret_cast<float*>(out) + b0 * cfg_.num_labels, s);

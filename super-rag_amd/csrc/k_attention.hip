@@ -24,8 +24,8 @@ constexpr int KT = 64;  // keys per tile
 template <int DH>
 __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict__ qkv,
                                                         const int32_t* __restrict__ mask,
-                                                        half_t* __restrict__ ctx, int S, int d,
-                                                        float scale_log2) {
+                                                        half_t* __restrict__ ctx, int S, int Sq,
+                                                        int d, float scale_log2) {
   constexpr int KS = DH + 8;    // K tile row stride (halfs), padded against bank conflicts
   constexpr int VS = KT + 8;    // V^T row stride (halfs)
   constexpr int NSUB = DH / 32; // k-substeps of the QK^T MFMA
@@ -139,8 +139,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict
   l_run += __shfl_xor(l_run, 32, 64);
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
   const int q = q0 + (lane & 15);
-  if (q < S) {
-    half_t* out = ctx + ((int64_t)b * S + q) * d + h * DH;
+  if (q < Sq) {
+    half_t* out = ctx + ((int64_t)b * Sq + q) * d + h * DH;
 #pragma unroll
     for (int t = 0; t < NDT; ++t) {
       const float4v v = o[t] * inv;
@@ -152,21 +152,24 @@ __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict
 
 }  // namespace
 
-void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int d,
-                      int heads, hipStream_t stream) {
+void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
+                      int d, int heads, hipStream_t stream) {
   const int dh = d / heads;
   SR_CHECK(dh * heads == d && (dh == 64 || dh == 32), "attention: head dim must be 32 or 64");
   if (B <= 0 || S <= 0) return;
-  const int nw = (int)std::min<int64_t>(4, ceil_div(S, 16));
-  dim3 grid((unsigned)ceil_div(S, 16 * nw), heads, B), block(64 * nw);
-  const double flops = 4.0 * B * heads * (double)S * S * dh;
-  const double bytes = 2.0 * B * (double)S * (3.0 * d + d);
+  SR_CHECK(Sq >= 1 && Sq <= S, "attention: query rows must be in [1, S]");
+  const int nw = (int)std::min<int64_t>(4, ceil_div(Sq, 16));
+  dim3 grid((unsigned)ceil_div(Sq, 16 * nw), heads, B), block(64 * nw);
+  const double flops = 4.0 * B * heads * (double)Sq * S * dh;
+  const double bytes = 2.0 * B * (double)S * 3.0 * d + 2.0 * B * (double)Sq * d;
   ProfScope prof("attention", stream, flops, bytes);
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)dh);
   if (dh == 64)
-    hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, stream, qkv, mask, ctx, S, d, scale_log2);
+    hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
+                       scale_log2);
   else
-    hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, stream, qkv, mask, ctx, S, d, scale_log2);
+    hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
+                       scale_log2);
   SR_LAUNCH_CHECK();
 }
 

@@ -58,7 +58,7 @@ __device__ __forceinline__ void ln_store(float4v (&x)[NV], int n4, const float* 
       const float4v g = reinterpret_cast<const float4v*>(gamma)[c];
       const float4v bb = reinterpret_cast<const float4v*>(beta)[c];
       const float4v y = (x[i] - mean) * rstd * g + bb;
-      reinterpret_cast<float4v*>(h32)[c] = y;
+      if (h32) reinterpret_cast<float4v*>(h32)[c] = y;
       half4 hy = {(half_t)y[0], (half_t)y[1], (half_t)y[2], (half_t)y[3]};
       reinterpret_cast<half4*>(h16)[c] = hy;
     }
@@ -93,29 +93,48 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
       for (int j = 0; j < 4; ++j) x[i][j] = (float)a[j] + (float)bp[j] + (float)ct[j];
     }
   }
-  ln_store<MAXV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 + m * d, lane);
+  ln_store<MAXV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 ? h32 + m * d : nullptr, lane);
 }
 
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ y,
-                                                        const float* __restrict__ gamma,
+// y (fp32 or fp16, the GEMM epilogue's bias + residual sum) -> LayerNorm -> h16 (+ h32).
+// Each lane loads its whole share of the row before the reductions, so the kernel may run in
+// place (y aliasing h16).
+template <bool YF16, int NV>
+__global__ __launch_bounds__(256) void layernorm_kernel(const void* y, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps,
-                                                        int M, int d, half_t* __restrict__ h16,
+                                                        int M, int d, half_t* h16,
                                                         float* __restrict__ h32) {
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   const int n4 = d >> 2;
-  float4v x[MAXV];
+  float4v x[NV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
-    if (c < n4) x[i] = reinterpret_cast<const float4v*>(y + m * d)[c];
+    if (c < n4) {
+      if constexpr (YF16) {
+        const half4 hv = reinterpret_cast<const half4*>(reinterpret_cast<const half_t*>(y) + m * d)[c];
+        x[i] = float4v{(float)hv[0], (float)hv[1], (float)hv[2], (float)hv[3]};
+      } else {
+        x[i] = reinterpret_cast<const float4v*>(reinterpret_cast<const float*>(y) + m * d)[c];
+      }
+    }
   }
-  ln_store<MAXV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 + m * d, lane);
+  ln_store<NV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 ? h32 + m * d : nullptr, lane);
 }
 
-// Pool (CLS row or attention-mask mean) of the fp32 hidden states, then L2-normalise.
-__global__ __launch_bounds__(64) void pool_l2_kernel(const float* __restrict__ h32,
+__device__ __forceinline__ float4v load4(const void* base, int64_t idx4, bool f16) {
+  if (f16) {
+    const half4 h = reinterpret_cast<const half4*>(base)[idx4];
+    return float4v{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+  return reinterpret_cast<const float4v*>(base)[idx4];
+}
+
+// Pool (CLS row or attention-mask mean) of the final hidden states (fp32, or fp16 for an fp16
+// residual stream), then L2-normalise.
+__global__ __launch_bounds__(64) void pool_l2_kernel(const void* __restrict__ h, int h_f16,
                                                      const int32_t* __restrict__ mask, int S,
                                                      int d, int pool, void* __restrict__ out,
                                                      int out_dtype, int ld_out) {
@@ -124,11 +143,11 @@ __global__ __launch_bounds__(64) void pool_l2_kernel(const float* __restrict__ h
   float4v x[MAXV];
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) x[i] = float4v{0.f, 0.f, 0.f, 0.f};
-  const float* seq = h32 + (int64_t)b * S * d;
+  const int64_t seq4 = (int64_t)b * S * n4;  // float4 index of the sequence's first row
   if (pool == SR_POOL_CLS) {
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)
-      if (lane + 64 * i < n4) x[i] = reinterpret_cast<const float4v*>(seq)[lane + 64 * i];
+      if (lane + 64 * i < n4) x[i] = load4(h, seq4 + lane + 64 * i, h_f16);
   } else {
     float cnt = 0.f;
     for (int s = 0; s < S; ++s) {
@@ -136,7 +155,7 @@ __global__ __launch_bounds__(64) void pool_l2_kernel(const float* __restrict__ h
       cnt += 1.f;
 #pragma unroll
       for (int i = 0; i < MAXV; ++i)
-        if (lane + 64 * i < n4) x[i] += reinterpret_cast<const float4v*>(seq + (int64_t)s * d)[lane + 64 * i];
+        if (lane + 64 * i < n4) x[i] += load4(h, seq4 + (int64_t)s * n4 + lane + 64 * i, h_f16);
     }
     const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
 #pragma unroll
@@ -238,22 +257,31 @@ void launch_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* type
   SR_LAUNCH_CHECK();
 }
 
-void launch_layernorm(const float* y, const float* gamma, const float* beta, float eps, int M,
-                      int d, half_t* h16, float* h32, hipStream_t s) {
+void launch_layernorm(const void* y, bool y_f16, const float* gamma, const float* beta, float eps,
+                      int M, int d, half_t* h16, float* h32, hipStream_t s) {
   SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "layernorm: hidden must be a multiple of 4, <= 2048");
   if (M <= 0) return;
-  ProfScope prof("layernorm", s, 0.0, (double)M * d * (4 + 4 + 2));
-  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, y, gamma,
-                     beta, eps, M, d, h16, h32);
+  ProfScope prof("layernorm", s, 0.0, (double)M * d * ((y_f16 ? 2 : 4) + 2 + (h32 ? 4 : 0)));
+  const dim3 grid((unsigned)ceil_div(M, 4)), block(256);
+  const int nv = (int)ceil_div(d / 4, 64);
+#define SR_LN(YF, NV)                                                                            \
+  hipLaunchKernelGGL((layernorm_kernel<YF, NV>), grid, block, 0, s, y, gamma, beta, eps, M, d, \
+                     h16, h32)
+  if (y_f16) {
+    if (nv <= 3) SR_LN(true, 3); else if (nv <= 4) SR_LN(true, 4); else SR_LN(true, MAXV);
+  } else {
+    if (nv <= 3) SR_LN(false, 3); else if (nv <= 4) SR_LN(false, 4); else SR_LN(false, MAXV);
+  }
+#undef SR_LN
   SR_LAUNCH_CHECK();
 }
 
-void launch_pool_l2(const float* h32, const int32_t* mask, int B, int S, int d, int pool,
+void launch_pool_l2(const void* h, bool h_f16, const int32_t* mask, int B, int S, int d, int pool,
                     void* out, int out_dtype, int ld_out, hipStream_t s) {
   SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "pool: hidden must be a multiple of 4, <= 2048");
   if (B <= 0) return;
   ProfScope prof("pool_l2", s, 0.0, (double)B * d * 4.0 * (pool == SR_POOL_CLS ? 1 : S));
-  hipLaunchKernelGGL(pool_l2_kernel, dim3(B), dim3(64), 0, s, h32, mask, S, d, pool, out,
+  hipLaunchKernelGGL(pool_l2_kernel, dim3(B), dim3(64), 0, s, h, h_f16 ? 1 : 0, mask, S, d, pool, out,
                      out_dtype, ld_out);
   SR_LAUNCH_CHECK();
 }

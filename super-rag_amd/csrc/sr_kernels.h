@@ -9,27 +9,32 @@ enum Epilogue {
   EPI_BIAS_F16 = 0,       // y = acc + b                 -> fp16
   EPI_BIAS_GELU_F16 = 1,  // y = gelu_erf(acc + b)       -> fp16
   EPI_BIAS_RES_F32 = 2,   // y = acc + b + R (fp32)      -> fp32
-  EPI_BIAS_TANH_F32 = 3   // y = tanh(acc + b)           -> fp32 (classifier head)
+  EPI_BIAS_TANH_F32 = 3,  // y = tanh(acc + b)           -> fp32 (classifier head)
+  EPI_BIAS_RES_F16 = 4    // y = acc + b + R (fp16)      -> fp16
 };
 
 // k_gemm.hip — Y = epi(X . W^T + bias (+ R)); K % 64 == 0, N % 128 == 0.
 void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
-                 const float* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
+                 const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream);
+void gemm_force_tile(int t);  // test hook: -1 auto, 0 = 128x128 tile, 1 = 256x256 tile
 
-// k_attention.hip — ctx = MHA(qkv, key padding mask).
-void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int d,
-                      int heads, hipStream_t stream);
+// k_attention.hip — ctx = MHA(qkv, key padding mask) for the first Sq query rows of each
+// sequence; ctx rows are laid out [B][Sq][d].
+void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
+                      int d, int heads, hipStream_t stream);
 
 // k_encoder_misc.hip
 void launch_positions(const int32_t* ids, int32_t* pos, int B, int S, int offset, hipStream_t s);
+// h32 may be null (fp16 residual stream): then only the fp16 copy is written.
 void launch_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* types,
                      const half_t* wemb, const half_t* pemb, const half_t* temb,
                      const float* gamma, const float* beta, float eps, int M, int d, int vocab,
                      int max_pos, int type_vocab, half_t* h16, float* h32, hipStream_t s);
-void launch_layernorm(const float* y, const float* gamma, const float* beta, float eps, int M,
-                      int d, half_t* h16, float* h32, hipStream_t s);
-void launch_pool_l2(const float* h32, const int32_t* mask, int B, int S, int d, int pool,
+// y is fp32 (y_f16 = false) or fp16; h32 may be null.
+void launch_layernorm(const void* y, bool y_f16, const float* gamma, const float* beta, float eps,
+                      int M, int d, half_t* h16, float* h32, hipStream_t s);
+void launch_pool_l2(const void* h, bool h_f16, const int32_t* mask, int B, int S, int d, int pool,
                     void* out, int out_dtype, int ld_out, hipStream_t s);
 void launch_cls_logits(const float* t, const float* w, const float* bias, int P, int d,
                        int labels, float* out, hipStream_t s);

@@ -43,7 +43,7 @@ class EncoderConfigC(ctypes.Structure):
         ("vocab_size", c_int), ("hidden", c_int), ("layers", c_int), ("heads", c_int),
         ("intermediate", c_int), ("max_position", c_int), ("type_vocab", c_int),
         ("ln_eps", c_float), ("position_offset", c_int), ("classifier", c_int),
-        ("num_labels", c_int), ("max_tokens", c_int),
+        ("num_labels", c_int), ("max_tokens", c_int), ("residual_fp16", c_int),
     ]
 
 

@@ -38,6 +38,7 @@ class ModelSpec:
     eos_id: int = 102
     pad_id: int = 0
     max_length: int = 512
+    residual_fp16: bool = False  # fp16 residual stream (rerankers: ranking fidelity, less traffic)
 
     @property
     def pair_style(self) -> int:
@@ -58,10 +59,12 @@ MODELS = {
     "bge-base-en": _bert("bge-base-en", 768, 12, 12, 3072),
     "bge-large-en": _bert("bge-large-en", 1024, 24, 16, 4096),
     "bge-m3": _xlmr("bge-m3", 1024, 24, 16, 4096, max_pos=8194),
-    "bge-reranker-base": _xlmr("bge-reranker-base", 768, 12, 12, 3072, classifier=1),
-    "bge-reranker-large": _xlmr("bge-reranker-large", 1024, 24, 16, 4096, classifier=1),
+    "bge-reranker-base": _xlmr("bge-reranker-base", 768, 12, 12, 3072, classifier=1,
+                               residual_fp16=True),
+    "bge-reranker-large": _xlmr("bge-reranker-large", 1024, 24, 16, 4096, classifier=1,
+                                residual_fp16=True),
     "bge-reranker-v2-m3": _xlmr("bge-reranker-v2-m3", 1024, 24, 16, 4096, max_pos=8194,
-                                classifier=1),
+                                classifier=1, residual_fp16=True),
 }
 
 
@@ -167,7 +170,7 @@ class Encoder:
         cfg = N.EncoderConfigC(spec.vocab_size, spec.hidden, spec.layers, spec.heads,
                                spec.intermediate, spec.max_position, spec.type_vocab,
                                float(spec.ln_eps), spec.position_offset, spec.classifier,
-                               spec.num_labels, int(max_tokens))
+                               spec.num_labels, int(max_tokens), int(spec.residual_fp16))
         h = ctypes.c_void_p()
         N.call("sr_encoder_create", ctypes.byref(cfg), self.device, ctypes.byref(h))
         self._h = h

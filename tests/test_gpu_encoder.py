@@ -22,12 +22,13 @@ def _ref_cfg(spec):
                        spec.classifier, spec.num_labels)
 
 
-def _tiny(arch="bert", d=128, L=2, H=2, F=256, classifier=0, V=1000, P=80):
+def _tiny(arch="bert", d=128, L=2, H=2, F=256, classifier=0, V=1000, P=80, res16=False):
     from super_rag_amd.encoder import ModelSpec
     if arch == "bert":
-        return ModelSpec("tiny-bert", "bert", V, d, L, H, F, P, 2, 1e-12, 0, classifier=classifier)
+        return ModelSpec("tiny-bert", "bert", V, d, L, H, F, P, 2, 1e-12, 0, classifier=classifier,
+                         residual_fp16=res16)
     return ModelSpec("tiny-xlmr", "xlmr", V, d, L, H, F, P, 1, 1e-5, 1, classifier=classifier,
-                     bos_id=0, eos_id=2, pad_id=1)
+                     bos_id=0, eos_id=2, pad_id=1, residual_fp16=res16)
 
 
 def _batch(spec, B, S, seed, ragged=True):
@@ -72,17 +73,18 @@ def test_bge_base_shape_embedding_tolerance():
     assert err.max() <= 1e-3, err
 
 
+@pytest.mark.parametrize("res16", [False, True])
 @pytest.mark.parametrize("S", [16, 64, 130])
-def test_tiny_cross_encoder(S):
+def test_tiny_cross_encoder(S, res16):
     from super_rag_amd.encoder import Encoder, random_weights
-    spec = _tiny("xlmr", classifier=1, P=200)
+    spec = _tiny("xlmr", classifier=1, P=200, res16=res16)
     w = random_weights(spec, seed=4, style="test")
     w["classifier.out_proj.weight"] *= 50.0  # spread the logits
     enc = Encoder(spec, weights=w)
     ids, mask = _batch(spec, 37, S, seed=S)
     got = enc.cross_score(ids, mask)[:, 0]
     ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)[:, 0]
-    tol = 2e-3 * (1.0 + np.abs(ref).max())
+    tol = (4e-3 if res16 else 2e-3) * (1.0 + np.abs(ref).max())
     assert np.abs(got - ref).max() <= tol
     # ranking contract: top-10 of the 37 candidates agree modulo near-ties
     top_g = np.argsort(-got, kind="stable")[:10][None]
@@ -127,3 +129,37 @@ def test_device_pair_packing_and_rerank_select():
     for b in range(9):
         exp = sorted(range(100), key=lambda j: (-logits[b, j], j))[:10]
         assert idx[b].tolist() == exp
+
+
+@pytest.mark.parametrize("tile", ["small", "big"])
+@pytest.mark.parametrize("pool", ["cls", "mean"])
+def test_gemm_tiles_and_cls_only_last_layer(tile, pool, monkeypatch):
+    # d=256 / F=512 so the 256x256 MFMA tile is legal; SR_GEMM_TILE forces the tile choice.
+    # pool="cls" runs the CLS-only last layer, pool="mean" the full one: both must match.
+    from super_rag_amd.encoder import Encoder, random_weights
+    monkeypatch.setenv("SR_GEMM_TILE", tile)
+    spec = _tiny("bert", d=256, H=4, F=512, L=3)
+    w = random_weights(spec, seed=8, style="test")
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 40, 50, seed=9)   # M = 2000 rows: ragged last tiles
+    got = enc.embed(ids, mask, pool=pool)
+    ref = R.embed(_ref_cfg(spec), w, ids, mask, pool=pool)
+    assert _rel(got, ref).max() <= 2e-3
+
+
+def test_bge_reranker_shape_fp16_residual_ranking():
+    # bge-reranker-base shape (XLM-R base, fp16 residual stream as shipped): logits within band,
+    # candidate top-10 identical modulo near-ties.
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    spec = MODELS["bge-reranker-base"]
+    w = random_weights(spec, seed=21, style="test")
+    w["classifier.out_proj.weight"] *= 50.0
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 48, 64, seed=4, ragged=True)
+    got = enc.cross_score(ids, mask)[:, 0]
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)[:, 0]
+    tol = 1e-2 * (1.0 + np.abs(ref).max())
+    assert np.abs(got - ref).max() <= tol
+    top_g = np.argsort(-got, kind="stable")[:10][None]
+    top_r = np.argsort(-ref, kind="stable")[:10][None]
+    assert same_topk_modulo_ties(top_g, got[top_g], top_r, ref[top_r], 2 * tol)
