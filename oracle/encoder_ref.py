@@ -105,9 +105,28 @@ def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None) -> np.ndarra
     return (t @ _t(w, "classifier.out_proj.weight").T + _t(w, "classifier.out_proj.bias")).numpy()
 
 
+def longest_first(a: int, b: int, budget: int):
+    """Lengths kept by Hugging Face fast tokenizers' LongestFirst pair truncation
+    (tokenizers utils/truncation.rs): the shorter side is kept whole when it fits in half the
+    budget, otherwise both are cut to half and the longer side (the second on ties) gets the odd
+    token.  bge rerankers load the fast tokenizer and call tokenizer(pairs, truncation=True)."""
+    budget = max(budget, 0)
+    if a + b <= budget:
+        return a, b
+    swap = a > b
+    n1, n2 = (b, a) if swap else (a, b)
+    n2 = n1 if n1 > budget else max(n1, budget - n1)
+    if n1 + n2 > budget:
+        n1 = budget // 2
+        n2 = n1 + budget % 2
+    if swap:
+        n1, n2 = n2, n1
+    return min(a, n1), min(b, n2)
+
+
 def pack_pairs(q_tok, q_len, p_tok, p_len, rows, S, style, bos, eos, pad):
     """Reference packing of (query, passage) pairs — HF tokenizer pair layout with 'longest_first'
-    truncation (FlagEmbedding's reranker calls tokenizer(pairs, truncation=True)).
+    truncation (see longest_first).
     style 0: <s> q </s></s> p </s>;  style 1: [CLS] q [SEP] p [SEP] (token type 1 on the passage)."""
     B, K = rows.shape
     ids = np.full((B * K, S), pad, dtype=np.int32)
@@ -119,11 +138,8 @@ def pack_pairs(q_tok, q_len, p_tok, p_len, rows, S, style, bos, eos, pad):
             r = int(rows[b, j])
             q = list(q_tok[b][: q_len[b]])
             p = list(p_tok[r][: p_len[r]]) if r >= 0 else []
-            while len(q) + len(p) > S - nspec:
-                if len(q) > len(p):
-                    q.pop()
-                else:
-                    p.pop()
+            lq2, lp2 = longest_first(len(q), len(p), S - nspec)
+            q, p = q[:lq2], p[:lp2]
             if style == 0:
                 seq = [bos] + q + [eos, eos] + p + [eos]
                 tps = [0] * len(seq)

@@ -324,7 +324,7 @@ __global__ void fill_float_kernel(float* __restrict__ p, int n, float v) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Cross-encoder pair packing (HF tokenizer pair layout, 'longest_first' truncation).
+// Cross-encoder pair packing (HF fast-tokenizer pair layout, LongestFirst truncation).
 __global__ __launch_bounds__(256) void build_pairs_kernel(
     const int32_t* __restrict__ q_tok, const int32_t* __restrict__ q_len, int lq_max,
     const int32_t* __restrict__ p_tok, const int32_t* __restrict__ p_len, int lp_max,
@@ -340,21 +340,20 @@ __global__ __launch_bounds__(256) void build_pairs_kernel(
   int lp = row >= 0 ? min(max(p_len[row], 0), lp_max) : 0;
   const int nspec = style == 0 ? 4 : 3;
   const int budget = max(S - nspec, 0);
-  // longest_first: drop from the longer side, from the passage on ties (HF truncate_sequences).
-  int excess = lq + lp - budget;
-  if (excess > 0) {
-    const int diff = lp - lq;
-    if (diff >= 0) {
-      const int cut = min(diff, excess);
-      lp -= cut;
-      excess -= cut;
-    } else {
-      const int cut = min(-diff, excess);
-      lq -= cut;
-      excess -= cut;
+  // LongestFirst truncation as Hugging Face fast tokenizers do it (tokenizers truncation.rs):
+  // the shorter side stays whole if it fits in half the budget, else both get half and the longer
+  // side (the passage on ties) gets the odd token.
+  if (lq + lp > budget) {
+    const bool swap = lq > lp;
+    int n1 = swap ? lp : lq;
+    int n2 = n1 > budget ? n1 : max(n1, budget - n1);
+    if (n1 + n2 > budget) {
+      n1 = budget / 2;
+      n2 = n1 + budget % 2;
     }
-    lp -= (excess + 1) / 2;
-    lq -= excess / 2;
+    const int tq = swap ? n2 : n1, tp = swap ? n1 : n2;
+    lq = min(lq, tq);
+    lp = min(lp, tp);
   }
   const int32_t* qt = q_tok + (int64_t)b * lq_max;
   const int32_t* pt = row >= 0 ? p_tok + row * lp_max : nullptr;

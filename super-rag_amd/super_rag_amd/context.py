@@ -1,0 +1,46 @@
+"""ContextManager (super_rag/context/context.py:7-111) on the ``"mi355x"`` vector store."""
+from __future__ import annotations
+
+from typing import Any, List, Optional
+
+from .models import QueryWithEmbedding
+from .vectorstore import VectorStoreConnectorAdaptor
+
+
+class ContextManager:
+    def __init__(self, collection_name, embedding_model, vectordb_type, vectordb_ctx):
+        self.collection_name = collection_name
+        self.embedding_model = embedding_model
+        self.vectordb_type = vectordb_type
+        self.adaptor = VectorStoreConnectorAdaptor(vectordb_type, vectordb_ctx)
+
+    def query(self, query, score_threshold=0.5, topk=3, vector=None, index_types=None, chat_id=None):
+        if vector is None:
+            vector = self.embedding_model.embed_query(query)
+        filter_condition = self._create_combined_filter(index_types, chat_id)
+        query_embedding = QueryWithEmbedding(query=query, top_k=topk, embedding=vector)
+        # Same kwargs as context.py:37-47; the store ignores all but top_k, as SeekDB's did.
+        results = self.adaptor.connector.search(
+            query_embedding,
+            collection_name=self.collection_name,
+            query_vector=query_embedding.embedding,
+            with_vectors=True,
+            limit=query_embedding.top_k,
+            consistency="majority",
+            search_params={"hnsw_ef": 128, "exact": False},
+            score_threshold=score_threshold,
+            filter=filter_condition,
+        )
+        return results.results
+
+    def _create_combined_filter(self, index_types: Optional[List[str]] = None,
+                                chat_id: Optional[str] = None) -> Optional[Any]:
+        if not index_types and not chat_id:
+            return None
+        clauses = []
+        if index_types:
+            clauses.append({"or": [{"indexer": {"$in": index_types}},
+                                   {"indexer": {"$exists": False}}]})
+        if chat_id:
+            clauses.append({"chat_id": chat_id})
+        return clauses[0] if len(clauses) == 1 else {"and": clauses}

@@ -31,7 +31,8 @@ class PipelineResult:
 class SearchPipeline:
     def __init__(self, embedder: Encoder, reranker: Encoder, store: NativeStore,
                  passage_tok: torch.Tensor, passage_len: torch.Tensor, k_candidates: int = 100,
-                 k_final: int = 10, pair_len: int = 128, shard_offset: int = 0, group=None):
+                 k_final: int = 10, pair_len: int = 128, shard_offset: int = 0, group=None,
+                 merge_fn=topk_merge_dev):
         self.embedder = embedder
         self.reranker = reranker
         self.store = store
@@ -42,6 +43,7 @@ class SearchPipeline:
         self.S = int(pair_len)
         self.offset = int(shard_offset)
         self.group = group
+        self.merge_fn = merge_fn
         import torch.distributed as dist
         self.world = dist.get_world_size(group) if (group is not None or
                                                      (dist.is_available() and dist.is_initialized())) else 1
@@ -62,8 +64,8 @@ class SearchPipeline:
         rr = torch.empty_like(rows)
         dist.all_to_all_single(rs, sims, group=self.group)
         dist.all_to_all_single(rr, rows, group=self.group)
-        return topk_merge_dev(rs.view(self.world, B, self.K), rr.view(self.world, B, self.K),
-                              self.K, device=q_emb.device.index or 0)
+        return self.merge_fn(rs.view(self.world, B, self.K), rr.view(self.world, B, self.K),
+                             self.K, device=q_emb.device.index or 0)
 
     def rerank(self, q_tok: torch.Tensor, q_len: torch.Tensor, cand_rows: torch.Tensor):
         B = cand_rows.shape[0]

@@ -1,0 +1,95 @@
+"""Drop-in RerankService (super_rag/llm/rerank/rerank_service.py:21-232) on the MI355X
+cross-encoder.
+
+Same constructor / ``max_documents`` / ``async_rerank`` / ``validate_configuration`` and error
+types.  ``_rank_texts`` scores the (query, passage) pairs in-process (XLM-R cross-encoder +
+classification head) instead of ``litellm.arerank`` and returns the indices ordered by relevance
+(logit desc, index asc), so ``async_rerank`` reorders the documents and keeps their original
+scores exactly as the reference does (:74).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+from typing import List, Optional
+
+import numpy as np
+
+from .errors import InvalidConfigurationError, InvalidDocumentError, RerankError, TooManyDocumentsError
+
+logger = logging.getLogger(__name__)
+
+
+class RerankService:
+    def __init__(self, rerank_provider: str, rerank_model: str, rerank_service_url: str,
+                 rerank_service_api_key: str, caching: bool = True, *, encoder=None,
+                 tokenizer=None, device: Optional[int] = None, device_batch: int = 1024):
+        self.rerank_provider = rerank_provider
+        self.model = rerank_model
+        self.api_base = rerank_service_url      # accepted for signature parity; unused
+        self.api_key = rerank_service_api_key   # accepted for signature parity; unused
+        self.caching = caching
+        self.max_documents = 1000
+        self.device_batch = max(1, int(device_batch))
+        if encoder is None:
+            from .registry import get_model
+            encoder, tokenizer = get_model(rerank_model, device)
+        self.encoder = encoder
+        self.tokenizer = tokenizer
+
+    def score(self, query: str, texts: List[str]) -> np.ndarray:
+        """Raw cross-encoder logits, one per text."""
+        out = np.empty(len(texts), dtype=np.float32)
+        with_types = self.encoder.spec.pair_style == 1
+        for s in range(0, len(texts), self.device_batch):
+            ids, mask, tt = self.tokenizer.encode_pairs(query, texts[s:s + self.device_batch])
+            out[s:s + len(ids)] = self.encoder.cross_score(ids, mask, tt if with_types else None)[:, 0]
+        return out
+
+    async def async_rerank(self, query: str, results: list) -> list:
+        try:
+            if not query or not query.strip():
+                raise InvalidDocumentError("Query cannot be empty")
+            if not results:
+                logger.info("No documents to rerank, returning empty list")
+                return []
+            if len(results) > self.max_documents:
+                raise TooManyDocumentsError(document_count=len(results),
+                                            max_documents=self.max_documents, model_name=self.model)
+            texts, invalid = [], []
+            for i, doc in enumerate(results):
+                if not doc or not hasattr(doc, "text") or not doc.text or not doc.text.strip():
+                    invalid.append(i)
+                    texts.append(" ")
+                else:
+                    texts.append(doc.text)
+            if invalid:
+                logger.warning("Found %d invalid documents at indices: %s", len(invalid), invalid)
+                if len(invalid) == len(results):
+                    raise InvalidDocumentError("All documents are empty or invalid",
+                                               document_count=len(results))
+            order = await self._rank_texts(query, texts)
+            return [results[i] for i in order if 0 <= i < len(results)]
+        except (InvalidDocumentError, TooManyDocumentsError, RerankError):
+            raise
+        except Exception as e:  # noqa: BLE001
+            raise RerankError(f"Rerank API error: {e}",
+                              {"provider": self.rerank_provider, "model": self.model}) from e
+
+    async def _rank_texts(self, query: str, texts: List[str]) -> List[int]:
+        try:
+            logits = await asyncio.to_thread(self.score, query, texts)
+        except Exception as e:  # noqa: BLE001
+            raise RerankError(f"Internal rerank operation failed: {e}",
+                              {"provider": self.rerank_provider, "model": self.model,
+                               "document_count": len(texts)}) from e
+        return sorted(range(len(texts)), key=lambda i: (-float(logits[i]), i))
+
+    def validate_configuration(self) -> None:
+        # provider / model as in rerank_service.py:219-232; key and base URL are not needed
+        # by the in-process model.
+        if not self.rerank_provider:
+            raise InvalidConfigurationError("rerank_provider", self.rerank_provider,
+                                            "Provider cannot be empty")
+        if not self.model:
+            raise InvalidConfigurationError("model", self.model, "Model name cannot be empty")

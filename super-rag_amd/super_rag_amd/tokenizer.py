@@ -1,0 +1,127 @@
+"""Host-side tokenisation for the in-process encoders.
+
+The reference never tokenises: text goes to remote servers (embedding_service.py:168-175,
+rerank_service.py:95-104).  In-process we need token ids.  With a Hugging Face ``tokenizer.json``
+(``SUPER_RAG_AMD_WEIGHTS/<model>/tokenizer.json`` or an explicit path) the real WordPiece /
+SentencePiece vocabulary is used through the ``tokenizers`` library.  No vocabulary ships
+offline, so otherwise a deterministic hashing tokenizer of the same id range is used (documented
+in DESIGN.md as synthetic: embeddings are then only self-consistent, not BGE-compatible).
+"""
+from __future__ import annotations
+
+import os
+import re
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+_WORD = re.compile(r"[぀-ヿ㐀-䶿一-鿿가-힯]|\w+|[^\w\s]",
+                   re.UNICODE)
+_FIRST_ID = 1000  # ids below are reserved for specials / control tokens
+
+
+def _fnv1a(s: str) -> int:
+    h = 0xCBF29CE484222325
+    for b in s.encode("utf-8"):
+        h ^= b
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def longest_first(a: int, b: int, budget: int):
+    """Pair lengths kept by Hugging Face fast tokenizers' LongestFirst truncation
+    (tokenizers utils/truncation.rs), the tokenizer bge rerankers load."""
+    budget = max(budget, 0)
+    if a + b <= budget:
+        return a, b
+    swap = a > b
+    n1, n2 = (b, a) if swap else (a, b)
+    n2 = n1 if n1 > budget else max(n1, budget - n1)
+    if n1 + n2 > budget:
+        n1 = budget // 2
+        n2 = n1 + budget % 2
+    if swap:
+        n1, n2 = n2, n1
+    return min(a, n1), min(b, n2)
+
+
+class Tokenizer:
+    def __init__(self, spec, path: str | None = None):
+        self.spec = spec
+        self.max_length = spec.max_length
+        self._hf = None
+        if path is None:
+            root = os.environ.get("SUPER_RAG_AMD_WEIGHTS")
+            cand = os.path.join(root, spec.name, "tokenizer.json") if root else None
+            path = cand if cand and os.path.exists(cand) else None
+        if path:
+            from tokenizers import Tokenizer as HFTokenizer
+            self._hf = HFTokenizer.from_file(path)
+        self.synthetic = self._hf is None
+
+    # -- content tokens (no specials) -------------------------------------------------------------
+    def content_ids(self, text: str) -> List[int]:
+        if self._hf is not None:
+            return list(self._hf.encode(text, add_special_tokens=False).ids)
+        span = self.spec.vocab_size - _FIRST_ID
+        return [_FIRST_ID + _fnv1a(w.lower()) % span for w in _WORD.findall(text)]
+
+    def content_batch(self, texts: Sequence[str], max_len: int) -> Tuple[np.ndarray, np.ndarray]:
+        """[N, max_len] int32 content tokens (truncated, zero padded) and [N] lengths."""
+        out = np.zeros((len(texts), max_len), dtype=np.int32)
+        lens = np.zeros(len(texts), dtype=np.int32)
+        for i, t in enumerate(texts):
+            ids = self.content_ids(t)[:max_len]
+            out[i, : len(ids)] = ids
+            lens[i] = len(ids)
+        return out, lens
+
+    # -- single sequences: [CLS] text [SEP] / <s> text </s> ---------------------------------------
+    def encode_batch(self, texts: Sequence[str], max_length: int | None = None):
+        """(ids, mask) int32 [B, S], padded to the longest sequence (dynamic padding)."""
+        L = min(max_length or self.max_length, self.max_length)
+        seqs = []
+        for t in texts:
+            c = self.content_ids(t)[: L - 2]
+            seqs.append([self.spec.bos_id] + c + [self.spec.eos_id])
+        S = max(len(s) for s in seqs)
+        ids = np.full((len(seqs), S), self.spec.pad_id, dtype=np.int32)
+        mask = np.zeros((len(seqs), S), dtype=np.int32)
+        for i, s in enumerate(seqs):
+            ids[i, : len(s)] = s
+            mask[i, : len(s)] = 1
+        return ids, mask
+
+    # -- (query, passage) pairs for cross-encoders ------------------------------------------------
+    def encode_pairs(self, query: str, passages: Sequence[str], max_length: int | None = None):
+        """(ids, mask, type_ids) [P, S] with the model's pair layout and 'longest_first'
+        truncation (the behaviour of tokenizer(pairs, truncation=True) used by bge rerankers);
+        an empty passage is a pair with no passage tokens, like the " " placeholder of
+        rerank_service.py:61."""
+        L = min(max_length or self.max_length, self.max_length)
+        q = self.content_ids(query)
+        style = self.spec.pair_style
+        nspec = 4 if style == 0 else 3
+        bos, eos = self.spec.bos_id, self.spec.eos_id
+        seqs, types = [], []
+        for p in passages:
+            a, b = list(q), self.content_ids(p)
+            na, nb = longest_first(len(a), len(b), L - nspec)
+            a, b = a[:na], b[:nb]
+            if style == 0:
+                s = [bos] + a + [eos, eos] + b + [eos]
+                t = [0] * len(s)
+            else:
+                s = [bos] + a + [eos] + b + [eos]
+                t = [0] * (len(a) + 2) + [1] * (len(b) + 1)
+            seqs.append(s)
+            types.append(t)
+        S = max(len(s) for s in seqs)
+        ids = np.full((len(seqs), S), self.spec.pad_id, dtype=np.int32)
+        mask = np.zeros((len(seqs), S), dtype=np.int32)
+        tt = np.zeros((len(seqs), S), dtype=np.int32)
+        for i, (s, t) in enumerate(zip(seqs, types)):
+            ids[i, : len(s)] = s
+            mask[i, : len(s)] = 1
+            tt[i, : len(t)] = t
+        return ids, mask, tt

@@ -1,0 +1,233 @@
+"""Drop-in vector-store connector: the SeekDB collection replaced by the in-HBM cosine store.
+
+Mirrors SeekDBVectorStoreConnector (super_rag/vectorstore/seekdb_connector.py:31-155):
+  * ``__init__(ctx, **kw)`` with ``ctx["collection"]``; ``.store`` is the connector itself
+    (embedding_utils.py:95 calls ``connector.store.add``); ``.collection_name``;
+  * ``create_collection(vector_size=...)``  (HNSW cosine -> exact cosine, :56-66)
+  * ``add(nodes) -> uuid4 string ids``        (:68-85)
+  * ``delete(ids=[...])`` / ValueError("ids is required") (:90-96), ``delete_collection()``
+  * ``search(QueryWithEmbedding, **kw) -> QueryResult`` with ``score = cosine distance``
+    ascending and no ids in the documents (:98-155); the extra kwargs the reference passes
+    (limit, score_threshold, filter, search_params, ...) are accepted and ignored, as there.
+Collections are process-wide (like a server): every connector object for the same collection
+name sees the same rows.  Row ids <-> uuid strings, texts and metadata live on the host; vectors
+live in HBM.  With ``ctx["snapshot_dir"]`` a collection is reloaded at construction and
+re-snapshotted after every add/delete (checkpoint/resume; SeekDB persisted server-side).
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import threading
+import uuid
+from typing import Any, Callable, Dict, List, Optional
+
+import numpy as np
+
+from .models import DocumentWithScore, QueryResult
+
+logger = logging.getLogger(__name__)
+
+VECTOR_DB_TYPE = "mi355x"
+
+
+def _native_store(dim: int, device: int):
+    from .store import NativeStore
+    return NativeStore(dim, device=device)
+
+
+def _native_load(path: str, device: int):
+    from .store import NativeStore
+    return NativeStore.load(path, device=device)
+
+
+_store_factory: Callable = _native_store
+_store_loader: Callable = _native_load
+
+
+def set_store_backend(factory: Callable, loader: Callable | None = None) -> None:
+    """Test seam: replace how per-collection stores are created / loaded."""
+    global _store_factory, _store_loader
+    _store_factory = factory
+    _store_loader = loader or _native_load
+
+
+class _Collection:
+    def __init__(self, name: str, dim: int, device: int, store=None):
+        self.name = name
+        self.dim = dim
+        self.device = device
+        self.store = store if store is not None else _store_factory(dim, device)
+        self.ids: List[Optional[str]] = []       # row -> uuid (None once deleted)
+        self.row_of: Dict[str, int] = {}
+        self.texts: List[Optional[str]] = []
+        self.metadatas: List[Optional[dict]] = []
+        self.lock = threading.RLock()
+
+    def snapshot(self, directory: str) -> None:
+        os.makedirs(directory, exist_ok=True)
+        base = os.path.join(directory, self.name)
+        self.store.save(base + ".srmi")
+        with open(base + ".json.tmp", "w", encoding="utf-8") as f:
+            json.dump({"dim": self.dim, "ids": self.ids, "texts": self.texts,
+                       "metadatas": self.metadatas}, f)
+        os.replace(base + ".json.tmp", base + ".json")
+
+    @classmethod
+    def restore(cls, name: str, directory: str, device: int) -> Optional["_Collection"]:
+        base = os.path.join(directory, name)
+        if not (os.path.exists(base + ".srmi") and os.path.exists(base + ".json")):
+            return None
+        with open(base + ".json", encoding="utf-8") as f:
+            meta = json.load(f)
+        c = cls(name, int(meta["dim"]), device, store=_store_loader(base + ".srmi", device))
+        c.ids = meta["ids"]
+        c.texts = meta["texts"]
+        c.metadatas = meta["metadatas"]
+        c.row_of = {u: i for i, u in enumerate(c.ids) if u is not None}
+        return c
+
+
+_registry_lock = threading.Lock()
+_collections: Dict[str, _Collection] = {}
+
+
+def _get(name: str) -> Optional[_Collection]:
+    with _registry_lock:
+        return _collections.get(name)
+
+
+class MI355XVectorStoreConnector:
+    def __init__(self, ctx: Dict[str, Any], **kwargs: Any):
+        self.ctx = ctx
+        self.collection_name = ctx["collection"]
+        self.vector_size = ctx.get("vector_size", 1024)
+        self.distance = ctx.get("distance", "cosine")
+        if self.distance != "cosine":
+            raise ValueError(f"unsupported distance '{self.distance}' (only cosine)")
+        self.device = int(ctx.get("device", os.environ.get("SUPER_RAG_AMD_DEVICE", 0)))
+        self.snapshot_dir = ctx.get("snapshot_dir")
+        self.compact_ratio = float(ctx.get("compact_ratio", 0.5))
+        self.store = self
+        if self.snapshot_dir and _get(self.collection_name) is None:
+            c = _Collection.restore(self.collection_name, self.snapshot_dir, self.device)
+            if c is not None:
+                with _registry_lock:
+                    _collections.setdefault(self.collection_name, c)
+
+    # -- collection lifecycle ---------------------------------------------------------------------
+    def _get_or_create(self, dim: int) -> _Collection:
+        with _registry_lock:
+            c = _collections.get(self.collection_name)
+            if c is None:
+                c = _Collection(self.collection_name, int(dim), self.device)
+                _collections[self.collection_name] = c
+            return c
+
+    def create_collection(self, **kwargs: Any):
+        vector_size = int(kwargs.get("vector_size") or self.vector_size)
+        c = self._get_or_create(vector_size)
+        if c.dim != vector_size:
+            raise ValueError(f"collection {self.collection_name} exists with dimension {c.dim}, "
+                             f"not {vector_size}")
+
+    def delete_collection(self):
+        with _registry_lock:
+            c = _collections.pop(self.collection_name, None)
+        if c is not None and hasattr(c.store, "close"):
+            c.store.close()
+        if self.snapshot_dir:
+            for ext in (".srmi", ".json"):
+                p = os.path.join(self.snapshot_dir, self.collection_name + ext)
+                if os.path.exists(p):
+                    os.remove(p)
+
+    def _persist(self, c: _Collection) -> None:
+        if self.snapshot_dir:
+            c.snapshot(self.snapshot_dir)
+
+    # -- mutation ---------------------------------------------------------------------------------
+    def add(self, nodes) -> List[str]:
+        if not nodes:
+            return []
+        vecs = np.asarray([n.embedding for n in nodes], dtype=np.float32)
+        if vecs.ndim != 2:
+            raise ValueError("every node needs an embedding of the same dimension")
+        c = self._get_or_create(vecs.shape[1])
+        if vecs.shape[1] != c.dim:
+            raise ValueError(f"embedding dimension {vecs.shape[1]} != collection dimension {c.dim}")
+        ids = [str(uuid.uuid4()) for _ in nodes]
+        with c.lock:
+            rows = c.store.add(vecs)
+            for u, r, n in zip(ids, rows, nodes):
+                assert int(r) == len(c.ids)
+                c.ids.append(u)
+                c.row_of[u] = int(r)
+                c.texts.append(n.text)
+                c.metadatas.append(copy.deepcopy(n.metadata) if n.metadata is not None else None)
+            self._persist(c)
+        logger.debug("Added %d documents to collection %s", len(ids), self.collection_name)
+        return ids
+
+    def delete(self, **delete_kwargs: Any):
+        ids = delete_kwargs.get("ids")
+        if not ids:
+            raise ValueError("ids is required")
+        c = _get(self.collection_name)
+        if c is None:
+            return
+        with c.lock:
+            rows = [c.row_of.pop(u) for u in ids if u in c.row_of]
+            if rows:
+                c.store.remove(np.asarray(rows, dtype=np.int64))
+                for r in rows:
+                    c.ids[r] = None
+                    c.texts[r] = None
+                    c.metadatas[r] = None
+                n_rows, n_live = c.store.count()
+                if n_rows and n_live < (1.0 - self.compact_ratio) * n_rows:
+                    self._compact(c)
+            self._persist(c)
+
+    def _compact(self, c: _Collection) -> None:
+        remap = c.store.compact()
+        keep = [i for i, r in enumerate(remap) if r >= 0]
+        c.ids = [c.ids[i] for i in keep]
+        c.texts = [c.texts[i] for i in keep]
+        c.metadatas = [c.metadatas[i] for i in keep]
+        c.row_of = {u: i for i, u in enumerate(c.ids)}
+
+    # -- query ------------------------------------------------------------------------------------
+    def search(self, query, **kwargs):
+        c = _get(self.collection_name)
+        if c is None or query.top_k is None or query.top_k <= 0:
+            return QueryResult(query=query.query, results=[])
+        q = np.asarray(query.embedding, dtype=np.float32)[None]
+        with c.lock:
+            dist, rows = c.store.search(q, int(query.top_k))
+            results = [DocumentWithScore(text=c.texts[r], score=float(d),
+                                         metadata=copy.deepcopy(c.metadatas[r]))
+                       for d, r in zip(dist[0].tolist(), rows[0].tolist()) if r >= 0]
+        return QueryResult(query=query.query, results=results)
+
+    def get_vectors(self, ids: List[str]) -> np.ndarray:
+        """Stored (normalised, fp16-rounded) vectors for uuids (with_vectors=True support)."""
+        c = _get(self.collection_name)
+        if c is None:
+            raise KeyError(self.collection_name)
+        with c.lock:
+            return c.store.get(np.asarray([c.row_of[u] for u in ids], dtype=np.int64))
+
+
+class VectorStoreConnectorAdaptor:
+    """vectorstore/connector.py:4-15 with the ``"mi355x"`` arm."""
+
+    def __init__(self, vector_store_type, ctx: Dict[str, Any], **kwargs: Any) -> None:
+        self.ctx = ctx
+        self.vector_store_type = vector_store_type
+        if vector_store_type == VECTOR_DB_TYPE:
+            self.connector = MI355XVectorStoreConnector(ctx, **kwargs)
+        else:
+            raise ValueError("unsupported vector store type:", vector_store_type)

@@ -1,0 +1,126 @@
+"""Test doubles for the CPU (not gpu) suite: they stand in for the HIP objects so the host-side
+boundary logic can be replayed against the reference's recorded behaviour without a GPU.
+They are never used by the product path."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+
+def hash_vec(text: str, dim: int = 8):
+    h = hashlib.sha256(text.encode("utf-8")).digest()
+    return [round((b - 128) / 128.0, 6) for b in h[:dim]]
+
+
+def relevance(query: str, text: str) -> float:
+    return len(set(query) & set(text)) - 0.001 * len(text)
+
+
+class NumpyStore:
+    """Exact fp64 cosine store with the NativeStore method surface."""
+
+    def __init__(self, dim: int, device: int = 0):
+        self.dim = dim
+        self.rows = np.zeros((0, dim))
+        self.live = np.zeros(0, bool)
+
+    def add(self, vecs):
+        v = np.asarray(vecs, dtype=np.float64)
+        first = len(self.rows)
+        self.rows = np.concatenate([self.rows, v])
+        self.live = np.concatenate([self.live, np.ones(len(v), bool)])
+        return np.arange(first, first + len(v))
+
+    def remove(self, rows):
+        rows = np.asarray(rows)
+        assert self.live[rows].all()
+        self.live[rows] = False
+
+    def count(self):
+        return len(self.rows), int(self.live.sum())
+
+    def compact(self):
+        m = np.full(len(self.rows), -1, dtype=np.int64)
+        keep = np.nonzero(self.live)[0]
+        m[keep] = np.arange(len(keep))
+        self.rows, self.live = self.rows[keep], self.live[keep]
+        return m
+
+    def get(self, rows):
+        return self.rows[np.asarray(rows)]
+
+    def save(self, path):
+        np.savez(path + ".npz", rows=self.rows, live=self.live)
+        import os
+        os.replace(path + ".npz", path)
+
+    @classmethod
+    def load(cls, path, device=0):
+        with np.load(path) as z:
+            s = cls(z["rows"].shape[1])
+            s.rows, s.live = z["rows"], z["live"]
+        return s
+
+    def search(self, q, k):
+        q = np.asarray(q, np.float64)
+        qn = q / np.linalg.norm(q, axis=1, keepdims=True)
+        rn = self.rows / np.maximum(np.linalg.norm(self.rows, axis=1, keepdims=True), 1e-300)
+        dist = np.full((len(q), k), np.inf)
+        out = np.full((len(q), k), -1, dtype=np.int64)
+        for b in range(len(q)):
+            d = 1.0 - rn @ qn[b]
+            order = [i for i in np.lexsort((np.arange(len(d)), d)) if self.live[i]][:k]
+            dist[b, : len(order)] = d[order]
+            out[b, : len(order)] = order
+        return dist, out
+
+
+class _Spec:
+    def __init__(self, hidden=8, pair_style=0):
+        self.hidden = hidden
+        self.pair_style = pair_style
+
+
+class TextTokenizer:
+    """Tokenizer double: 'token ids' are indices into the list of texts it has seen."""
+
+    def __init__(self):
+        self.seen = []
+        self.pairs = []
+
+    def encode_batch(self, texts):
+        start = len(self.seen)
+        self.seen.extend(texts)
+        ids = np.arange(start, start + len(texts), dtype=np.int32)[:, None]
+        return ids, np.ones_like(ids)
+
+    def encode_pairs(self, query, passages):
+        start = len(self.pairs)
+        self.pairs.extend((query, p) for p in passages)
+        ids = np.arange(start, start + len(passages), dtype=np.int32)[:, None]
+        return ids, np.ones_like(ids), np.zeros_like(ids)
+
+
+class HashEncoder:
+    """Embedding double: the vector of text i is hash_vec(text)."""
+
+    def __init__(self, tok: TextTokenizer, dim: int = 8):
+        self.tok = tok
+        self.spec = _Spec(dim)
+
+    def embed(self, ids, mask):
+        return np.asarray([hash_vec(self.tok.seen[int(i)], self.spec.hidden) for i in ids[:, 0]],
+                          dtype=np.float32)
+
+
+class RelevanceEncoder:
+    """Cross-encoder double: logit of pair i is relevance(query, passage)."""
+
+    def __init__(self, tok: TextTokenizer):
+        self.tok = tok
+        self.spec = _Spec(8, pair_style=0)
+
+    def cross_score(self, ids, mask, types=None):
+        return np.asarray([[relevance(*self.tok.pairs[int(i)])] for i in ids[:, 0]],
+                          dtype=np.float32)

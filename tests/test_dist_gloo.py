@@ -1,0 +1,78 @@
+"""CPU, world_size 2 (gloo): the sharded retrieve exchange of SearchPipeline — all_gather of the
+query embeddings (C1), per-shard top-K, all_to_all of the per-shard lists (C2) and the merge —
+returns exactly the single-process top-K for every rank's own queries.  The shard search and the
+merge are CPU doubles with the semantics of sr_store_search_dev / sr_topk_merge_dev (row offset,
+similarity desc, row asc); on the GPU box the same code runs over RCCL with the HIP kernels."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class ShardStoreDouble:
+    def __init__(self, rows: torch.Tensor):
+        self.rows = torch.nn.functional.normalize(rows.double(), dim=1)
+
+    def search_dev(self, q, k, row_offset=0):
+        s = torch.nn.functional.normalize(q.double(), dim=1) @ self.rows.T
+        idx = torch.arange(self.rows.shape[0]).expand_as(s)
+        order = np.lexsort((idx.numpy(), -s.numpy()), axis=1)[:, :k]
+        order = torch.from_numpy(order)
+        return s.gather(1, order).float(), (order + row_offset).long()
+
+
+def merge_double(sims, rows, k, device=0):
+    P, B, K = sims.shape
+    s = sims.permute(1, 0, 2).reshape(B, P * K).double()
+    r = rows.permute(1, 0, 2).reshape(B, P * K)
+    order = torch.from_numpy(np.lexsort((r.numpy(), -s.numpy()), axis=1)[:, :k])
+    return s.gather(1, order).float(), r.gather(1, order)
+
+
+def _worker(rank, world, port, corpus, queries, k, out_q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "super-rag_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from super_rag_amd.pipeline import SearchPipeline
+    n = corpus.shape[0]
+    per = (n + world - 1) // world
+    r0, r1 = rank * per, min(n, (rank + 1) * per)
+    pipe = SearchPipeline(None, None, ShardStoreDouble(corpus[r0:r1]), None, None, k_candidates=k,
+                          shard_offset=r0, merge_fn=merge_double)
+    B = queries.shape[0] // world
+    mine = queries[rank * B:(rank + 1) * B]
+    sims, rows = pipe.retrieve(mine)
+    out_q.put((rank, sims.numpy(), rows.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_retrieve_matches_single_process(world):
+    g = torch.Generator().manual_seed(0)
+    corpus = torch.randn(1001, 16, generator=g)
+    queries = torch.randn(6, 16, generator=g)
+    k = 7
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, world, port, corpus, queries, k, out_q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, rr)) for r, s, rr in (out_q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full_s, full_r = ShardStoreDouble(corpus).search_dev(queries, k)
+    B = queries.shape[0] // world
+    for r in range(world):
+        s, rows = res[r]
+        assert np.array_equal(rows, full_r[r * B:(r + 1) * B].numpy())
+        np.testing.assert_allclose(s, full_s[r * B:(r + 1) * B].numpy(), atol=1e-6)

@@ -1,0 +1,69 @@
+"""GPU parity of the whole batched hot path (SearchPipeline: embed -> exact top-K -> pair packing
+-> cross-encoder -> top-k) against the oracle composition, stage by stage, on one GPU."""
+import numpy as np
+import pytest
+
+from oracle import encoder_ref as R
+from oracle.cosine_topk import cosine_topk, quantize_like_store, same_topk_modulo_ties
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(s):
+    return R.RefConfig(s.vocab_size, s.hidden, s.layers, s.heads, s.intermediate, s.max_position,
+                       s.type_vocab, s.ln_eps, s.position_offset, s.classifier, s.num_labels)
+
+
+@pytest.mark.parametrize("res16", [False, True])
+def test_pipeline_stages_match_oracle(res16):
+    import torch
+    from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
+    from super_rag_amd.pipeline import SearchPipeline
+    from super_rag_amd.store import NativeStore
+
+    es = ModelSpec("e", "bert", 2000, 128, 2, 2, 256, 64, 2, 1e-12, 0)
+    rs = ModelSpec("r", "xlmr", 2000, 128, 2, 2, 256, 80, 1, 1e-5, 1, classifier=1, bos_id=0,
+                   eos_id=2, pad_id=1, residual_fp16=res16)
+    we, wr = random_weights(es, 1, "test"), random_weights(rs, 2, "test")
+    wr["classifier.out_proj.weight"] *= 50.0
+    emb, rer = Encoder(es, weights=we), Encoder(rs, weights=wr)
+    rng = np.random.default_rng(0)
+    N, B, K, k, S, Lq, Lp = 20000, 12, 20, 5, 48, 10, 40
+    corpus = rng.standard_normal((N, 128)).astype(np.float32)
+    store = NativeStore(128)
+    store.add(corpus)
+    p_tok = rng.integers(5, 2000, (N, Lp)).astype(np.int32)
+    p_len = rng.integers(1, Lp + 1, N).astype(np.int32)
+    q_ids = rng.integers(5, 2000, (B, 16)).astype(np.int32)
+    q_ids[:, 0] = 101
+    q_mask = np.ones_like(q_ids)
+    q_tok = rng.integers(5, 2000, (B, Lq)).astype(np.int32)
+    q_len = rng.integers(1, Lq + 1, B).astype(np.int32)
+    t = lambda a: torch.from_numpy(a).cuda()
+    pipe = SearchPipeline(emb, rer, store, t(p_tok), t(p_len), k_candidates=K, k_final=k, pair_len=S)
+    res = pipe.run(t(q_ids), t(q_mask), t(q_tok), t(q_len))
+    q16 = pipe.embed(t(q_ids), t(q_mask)).float().cpu().numpy()
+    torch.cuda.synchronize()
+
+    # stage 1: embeddings vs the fp32 oracle
+    e_ref = R.embed(_cfg(es), we, q_ids, q_mask)
+    assert (np.linalg.norm(q16 - e_ref, axis=1) <= 2e-3).all()
+    # stage 2: candidates = exact top-K of the store rows for the GPU's own (fp16) query vectors
+    stored = store.get(np.arange(N))
+    d_ref, r_ref = cosine_topk(stored, quantize_like_store(q16), K, normalize=False)
+    cand = res.cand_rows.cpu().numpy()
+    sims = res.cand_sims.cpu().numpy()
+    assert same_topk_modulo_ties(cand, sims, r_ref, 1.0 - d_ref, 1e-4)
+    # stage 3+4: pair packing and cross-encoder logits on the GPU's candidates
+    ids, mask, _ = R.pack_pairs(q_tok, q_len, p_tok, p_len, cand, S, 0, 0, 2, 1)
+    lg_ref = R.cross_logits(_cfg(rs), wr, ids, mask)[:, 0].reshape(B, K)
+    tol = (4e-3 if res16 else 2e-3) * (1.0 + np.abs(lg_ref).max())
+    final = res.rows.cpu().numpy()
+    flog = res.logits.cpu().numpy()
+    for b in range(B):
+        order = sorted(range(K), key=lambda j: (-lg_ref[b, j], j))[:k]
+        exp_rows = cand[b, order]
+        assert same_topk_modulo_ties(final[b:b + 1], flog[b:b + 1], exp_rows[None],
+                                     lg_ref[b, order][None], 2 * tol)
+        got = dict(zip(cand[b].tolist(), range(K)))
+        np.testing.assert_allclose(flog[b], lg_ref[b, [got[r] for r in final[b]]], atol=tol)

@@ -1,0 +1,53 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and fails loudly (no
+silent CPU fallback) when no GPU is visible."""
+import glob
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(sr_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    from super_rag_amd import _native
+    lib = _native.load()
+    declared = _declared()
+    assert len(declared) >= 30
+    missing = [n for n in declared if not hasattr(lib, n)]
+    assert not missing, missing
+    assert declared == set(_native.SIGNATURES), declared ^ set(_native.SIGNATURES)
+    assert lib.sr_version() >= 100
+
+
+def test_no_gpu_fails_loudly():
+    from super_rag_amd import _native
+    if _native.device_count() > 0:
+        pytest.skip("GPU visible: covered by the gpu suite")
+    from super_rag_amd.store import NativeStore
+    with pytest.raises(_native.NativeUnavailableError):
+        NativeStore(64)
+    from super_rag_amd.encoder import MODELS, Encoder
+    with pytest.raises(_native.NativeUnavailableError):
+        Encoder(MODELS["bge-small-en"])
+
+
+def test_error_codes_and_messages_without_device():
+    import ctypes
+    from super_rag_amd import _native
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    rc = lib.sr_store_create(0, 0, 16, ctypes.byref(h))   # invalid dim: checked before any HIP call
+    assert rc == _native.SR_ERR_INVALID
+    assert b"dim" in lib.sr_last_error()
+    assert lib.sr_store_count(None, None, None) == _native.SR_ERR_INVALID
+    stats = _native.profile_read()
+    assert isinstance(stats, dict)
