@@ -399,6 +399,24 @@ int sr_rerank_select_dev(const float* logits, int B, int K, int k_out, int32_t* 
   SR_API_END
 }
 
+// ---- diagnostics -----------------------------------------------------------------------------
+int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W, const float* bias,
+                 const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, int device,
+                 void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(Y);
+  SR_CHECK(epi >= 0 && epi <= 4, "diag_gemm: epi must be 0..4");
+  SR_CHECK((epi != 2 && epi != 4) || R, "diag_gemm: residual epilogue needs R");
+  sr::DeviceGuard g(device);
+  sr::launch_gemm_variant(variant, epi, reinterpret_cast<const sr::half_t*>(X), lda,
+                          reinterpret_cast<const sr::half_t*>(W), bias, R, ldr, Y, ldy, M, N, K,
+                          reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
 // ---- profiling -------------------------------------------------------------------------------
 int sr_profile_enable(int on) {
   SR_API_BEGIN

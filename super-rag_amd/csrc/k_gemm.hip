@@ -56,12 +56,170 @@ __device__ __forceinline__ half8 read_frag(const half_t* lds_tile, int row, int 
   return *reinterpret_cast<const half8*>(lds_tile + off);
 }
 
+// Exact-GELU x * Phi(x) with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
+// the fp16 rounding of the output): branch-free, one v_rcp + one v_exp + 7 FMA per element,
+// about a third of the instructions of the library erff in this VALU-heavy epilogue.
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = 1.0f - p * __expf(-z * z);   // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + copysignf(e, x));
 }
 
-template <int EPI, int BN, int BM, int WN, int WM>
-__global__ __launch_bounds__(64 * WN * WM, 2) void gemm_f16_kernel(
+// Epilogue: lane owns D[n = nw0 + 16i + 4(lane>>4) + r][m = mw0 + 16j + (lane&15)] of the wave's
+// FN x FM 16x16 tiles; bias (+ residual) (+ activation), one 8/16-byte store per tile.
+template <int EPI, int FN, int FM>
+__device__ __forceinline__ void store_tile(float4v (&acc)[FN][FM], int nw0, int mw0, int lane, int M,
+                                           const float* __restrict__ bias,
+                                           const void* __restrict__ R, int64_t ldr,
+                                           void* __restrict__ Y, int64_t ldy) {
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n = nw0 + i * 16 + 4 * (lane >> 4);
+    const float4v bv = *reinterpret_cast<const float4v*>(bias + n);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = mw0 + j * 16 + (lane & 15);
+      if (m >= M) continue;
+      float4v v = acc[i][j] + bv;
+      if constexpr (EPI == EPI_BIAS_RES_F32) {
+        v += *reinterpret_cast<const float4v*>(reinterpret_cast<const float*>(R) + (int64_t)m * ldr + n);
+        *reinterpret_cast<float4v*>(reinterpret_cast<float*>(Y) + (int64_t)m * ldy + n) = v;
+      } else if constexpr (EPI == EPI_BIAS_TANH_F32) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = tanhf(v[r]);
+        *reinterpret_cast<float4v*>(reinterpret_cast<float*>(Y) + (int64_t)m * ldy + n) = v;
+      } else {
+        if constexpr (EPI == EPI_BIAS_GELU_F16) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+        } else if constexpr (EPI == EPI_BIAS_RES_F16) {
+          const half4 rv =
+              *reinterpret_cast<const half4*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+        }
+        half4 h = {(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+        *reinterpret_cast<half4*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + n) = h;
+      }
+    }
+  }
+}
+
+// ---- "deep" variant: 256 x 256 tile, K-step 32, 4-slot LDS ring, 3 K-steps in flight ------------
+// The 2-slot ring above drains every glds at each K-step barrier (vmcnt(0)): with W / X served
+// from MALL / HBM the load latency (1-2 us) exceeds one K-step of MFMA work and stalls the
+// workgroup.  Here each K-step issues the loads of step kt+3 into the slot read at kt-1, waits
+// with a COUNTED vmcnt for step kt+1 only, and synchronises with a raw s_barrier (a
+// __syncthreads() would add vmcnt(0) and drain the ring).  Rows are 64 B (32 fp16): the 16-byte
+// chunk c of row r is stored at chunk c ^ ((r >> 2) & 2), conflict-free for ds_read_b128
+// (exhaustively checked for the four lane groups).
+constexpr int DBK = 32;
+constexpr int DSLOTS = 4;
+
+__device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((row >> 2) & 2); }
+
+// NI wave-instructions of one 64-B-row tile: instruction i fills LDS rows prow..prow+15.
+template <int NI>
+__device__ __forceinline__ void stage_rows64(const half_t* __restrict__ g, int64_t ld, int row0,
+                                             int row_max, int k0, half_t* lds_tile, int wave,
+                                             int lane) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int prow = (wave * NI + i) * 16;
+    const int r = prow + (lane >> 2);
+    int gr = row0 + r;
+    gr = gr < row_max ? gr : row_max - 1;
+    const half_t* src = g + (int64_t)gr * ld + k0 + swz64(r, lane & 3) * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, SR_LDS(lds_tile + prow * DBK), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ half8 read_frag64(const half_t* lds_tile, int row, int chunk) {
+  return *reinterpret_cast<const half8*>(lds_tile + row * DBK + swz64(row, chunk) * 8);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm_deep_kernel(
+    const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
+    const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
+    void* __restrict__ Y, int64_t ldy, int M, int N, int K) {
+  constexpr int BN = 256, BM = 256, WN = 2, WM = 4, WAVES = 8;
+  constexpr int FN = BN / WN / 16, FM = BM / WM / 16;   // 8 x 4 tiles of 16x16 per wave
+  constexpr int NI = BN / 16 / WAVES;                   // 2 glds per operand per wave
+  constexpr int SLOT = (BN + BM) * DBK;                 // halfs per ring slot (32 KiB)
+  __shared__ __attribute__((aligned(16))) half_t lds[DSLOTS * SLOT];  // 128 KiB
+
+  const int tiles_n = N / BN;
+  const int nwg = tiles_n * ((M + BM - 1) / BM);
+  const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (blockIdx.x >> 3);
+  const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave / WM, wm = wave % WM;
+  const int nk = K / DBK;
+
+  auto stage = [&](int kt) {
+    half_t* s = lds + (kt % DSLOTS) * SLOT;
+    stage_rows64<NI>(W, K, n0, N, kt * DBK, s, wave, lane);
+    stage_rows64<NI>(X, lda, m0, M, kt * DBK, s + BN * DBK, wave, lane);
+  };
+
+  float4v acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: slots 0..2 in flight (4 glds per wave each); wait for slot 0
+  stage(0);
+  if (nk > 1) stage(1);
+  if (nk > 2) stage(2);
+  if (nk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 3 < nk) stage(kt + 3);  // slot (kt+3)%4 == slot read at kt-1: freed by its barrier
+    const half_t* As = lds + (kt % DSLOTS) * SLOT;
+    const half_t* Bs = As + BN * DBK;
+    half8 a[FN], b[FM];
+    const int chunk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) a[i] = read_frag64(As, wn * (BN / WN) + i * 16 + (lane & 15), chunk);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) b[j] = read_frag64(Bs, wm * (BM / WM) + j * 16 + (lane & 15), chunk);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // retire step kt+1 (its glds were issued two steps ago); later steps stay in flight
+    const int ahead = nk - 2 - kt;  // steps issued after kt+1
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  store_tile<EPI, FN, FM>(acc, n0 + wn * (BN / WN), m0 + wm * (BM / WM), lane, M, bias, R, ldr, Y,
+                          ldy);
+}
+
+// PERSIST: a grid of 8 * G blocks walks the tiles; XCD group x = blockIdx & 7 owns a contiguous
+// tile range (X panels stay in that XCD's L2) and the next tile's first K-step is staged by
+// LDS-DMA while the current tile's epilogue runs, hiding the per-tile load latency.
+template <int EPI, int BN, int BM, int WN, int WM, bool PERSIST>
+__global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) void gemm_f16_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
     void* __restrict__ Y, int64_t ldy, int M, int N, int K) {
@@ -75,28 +233,41 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void gemm_f16_kernel(
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
   const int nwg = tiles_n * tiles_m;
-  // XCD-aware bijective remap: blocks b and b+8 share an XCD; give each XCD a contiguous range.
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (orig >> 3);
-  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int t, t_end, t_step;
+  {
+    // blocks b and b+8 share an XCD: give each XCD a contiguous range of tiles (n fastest).
+    const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
+    const int lo = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+    if constexpr (PERSIST) {
+      t = lo + (blockIdx.x >> 3);
+      t_end = lo + q + (xcd < rem ? 1 : 0);
+      t_step = gridDim.x >> 3;
+    } else {
+      t = lo + (blockIdx.x >> 3);
+      t_end = t + 1;
+      t_step = 1;
+    }
+  }
+  int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (LDS-DMA base in M0)
   const int wn = wave / WM, wm = wave % WM;
+  const int nk = K / GBK;
 
+  // stage buffer b: W tile (BN rows) at lds + b*STAGE, X tile (BM rows) right after it.
+  if (t < t_end) {
+    stage_tile<NIA>(W, K, n0, N, 0, lds, wave, lane);
+    stage_tile<NIB>(X, lda, m0, M, 0, lds + BN * GBK, wave, lane);
+  }
+  __syncthreads();
+
+  for (; t < t_end; t += t_step) {
   float4v acc[FN][FM];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / GBK;
-  // stage buffer b: W tile (BN rows) at lds + b*STAGE, X tile (BM rows) right after it.
-  stage_tile<NIA>(W, K, n0, N, 0, lds, wave, lane);
-  stage_tile<NIB>(X, lda, m0, M, 0, lds + BN * GBK, wave, lane);
-  __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
@@ -126,68 +297,44 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void gemm_f16_kernel(
     __syncthreads();
   }
 
-  // Epilogue: lane owns D[n = n0 + wn*BN/WN + 16i + 4(lane>>4) + r][m = m0 + wm*BM/WM + 16j + (lane&15)].
-#pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    const int n = n0 + wn * (BN / WN) + i * 16 + 4 * (lane >> 4);
-    const float4v bv = *reinterpret_cast<const float4v*>(bias + n);
-#pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const int m = m0 + wm * (BM / WM) + j * 16 + (lane & 15);
-      if (m >= M) continue;
-      float4v v = acc[i][j] + bv;
-      if constexpr (EPI == EPI_BIAS_RES_F32) {
-        v += *reinterpret_cast<const float4v*>(reinterpret_cast<const float*>(R) + (int64_t)m * ldr + n);
-        *reinterpret_cast<float4v*>(reinterpret_cast<float*>(Y) + (int64_t)m * ldy + n) = v;
-      } else if constexpr (EPI == EPI_BIAS_TANH_F32) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = tanhf(v[r]);
-        *reinterpret_cast<float4v*>(reinterpret_cast<float*>(Y) + (int64_t)m * ldy + n) = v;
-      } else {
-        if constexpr (EPI == EPI_BIAS_GELU_F16) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
-        } else if constexpr (EPI == EPI_BIAS_RES_F16) {
-          const half4 rv =
-              *reinterpret_cast<const half4*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr + n);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
-        }
-        half4 h = {(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
-        *reinterpret_cast<half4*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + n) = h;
-      }
-    }
+  // Next tile: its first K-step lands in buffer 0 while this tile's epilogue runs (every LDS read
+  // of this tile finished before the K-loop's last barrier).
+  const int tn_next = t + t_step;
+  const int m0_next = (tn_next / tiles_n) * BM, n0_next = (tn_next % tiles_n) * BN;
+  if (PERSIST && tn_next < t_end) {
+    stage_tile<NIA>(W, K, n0_next, N, 0, lds, wave, lane);
+    stage_tile<NIB>(X, lda, m0_next, M, 0, lds + BN * GBK, wave, lane);
   }
+
+  store_tile<EPI, FN, FM>(acc, n0 + wn * (BN / WN), m0 + wm * (BM / WM), lane, M, bias, R, ldr, Y,
+                          ldy);
+  if constexpr (PERSIST) {
+    __syncthreads();  // next tile's first K-step has landed in buffer 0
+    m0 = m0_next;
+    n0 = n0_next;
+  }
+  }  // tile loop
 }
 
-template <int BN, int BM, int WN, int WM>
+template <int BN, int BM, int WN, int WM, bool PERSIST>
 void launch_tile(int epi, dim3 grid, hipStream_t stream, const half_t* X, int64_t lda,
                  const half_t* W, const float* bias, const void* R, int64_t ldr, void* Y,
                  int64_t ldy, int M, int N, int K) {
   const dim3 block(64 * WN * WM);
+#define SR_GEMM_CASE(E)                                                                        \
+  case E:                                                                                      \
+    hipLaunchKernelGGL((gemm_f16_kernel<E, BN, BM, WN, WM, PERSIST>), grid, block, 0, stream, \
+                       X, lda, W, bias, R, ldr, Y, ldy, M, N, K);                              \
+    break;
   switch (epi) {
-    case EPI_BIAS_F16:
-      hipLaunchKernelGGL((gemm_f16_kernel<EPI_BIAS_F16, BN, BM, WN, WM>), grid, block, 0, stream,
-                         X, lda, W, bias, R, ldr, Y, ldy, M, N, K);
-      break;
-    case EPI_BIAS_GELU_F16:
-      hipLaunchKernelGGL((gemm_f16_kernel<EPI_BIAS_GELU_F16, BN, BM, WN, WM>), grid, block, 0,
-                         stream, X, lda, W, bias, R, ldr, Y, ldy, M, N, K);
-      break;
-    case EPI_BIAS_RES_F32:
-      hipLaunchKernelGGL((gemm_f16_kernel<EPI_BIAS_RES_F32, BN, BM, WN, WM>), grid, block, 0,
-                         stream, X, lda, W, bias, R, ldr, Y, ldy, M, N, K);
-      break;
-    case EPI_BIAS_RES_F16:
-      hipLaunchKernelGGL((gemm_f16_kernel<EPI_BIAS_RES_F16, BN, BM, WN, WM>), grid, block, 0,
-                         stream, X, lda, W, bias, R, ldr, Y, ldy, M, N, K);
-      break;
-    case EPI_BIAS_TANH_F32:
-      hipLaunchKernelGGL((gemm_f16_kernel<EPI_BIAS_TANH_F32, BN, BM, WN, WM>), grid, block, 0,
-                         stream, X, lda, W, bias, R, ldr, Y, ldy, M, N, K);
-      break;
+    SR_GEMM_CASE(EPI_BIAS_F16)
+    SR_GEMM_CASE(EPI_BIAS_GELU_F16)
+    SR_GEMM_CASE(EPI_BIAS_RES_F32)
+    SR_GEMM_CASE(EPI_BIAS_RES_F16)
+    SR_GEMM_CASE(EPI_BIAS_TANH_F32)
     default: SR_CHECK(false, "gemm: unknown epilogue");
   }
+#undef SR_GEMM_CASE
 }
 
 }  // namespace
@@ -209,12 +356,22 @@ static int forced_tile() {
   if (g_force_tile >= 0) return g_force_tile;
   const char* e = std::getenv("SR_GEMM_TILE");
   if (!e) return -1;
-  return std::strcmp(e, "big") == 0 ? 1 : (std::strcmp(e, "small") == 0 ? 0 : -1);
+  if (std::strcmp(e, "small") == 0) return GEMM_SMALL;
+  if (std::strcmp(e, "big") == 0) return GEMM_BIG;
+  if (std::strcmp(e, "persist") == 0) return GEMM_BIG_PERSIST;
+  if (std::strcmp(e, "deep") == 0) return GEMM_DEEP;
+  return -1;
 }
 
 void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream) {
+  launch_gemm_variant(-1, epi, X, lda, W, bias, R, ldr, Y, ldy, M, N, K, stream);
+}
+
+void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
+                         const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
+                         int M, int N, int K, hipStream_t stream) {
   SR_CHECK(K % GBK == 0, "gemm: K must be a multiple of 64");
   SR_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128");
   SR_CHECK(lda % 8 == 0 && ldy % 4 == 0, "gemm: leading dimensions must keep 16-byte rows");
@@ -224,17 +381,39 @@ void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const f
   const double bytes = 2.0 * ((double)M * K + (double)N * K) + (out_b + res_b) * (double)M * N;
   ProfScope prof(epi_name(epi), stream, 2.0 * M * (double)N * K, bytes);
   const int64_t big_tiles = (N % 256 == 0) ? (int64_t)(N / 256) * ceil_div(M, 256) : 0;
-  const int force = forced_tile();
-  const bool big = force >= 0 ? (force == 1 && N % 256 == 0) : big_tiles >= 512;
-  if (big) {
-    SR_CHECK(big_tiles < (1ll << 31), "gemm: too many tiles");
-    launch_tile<256, 256, 2, 4>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R, ldr,
-                                Y, ldy, M, N, K);
+  int v = variant >= 0 ? variant : forced_tile();
+  if (v < 0) v = big_tiles >= 512 ? GEMM_BIG : GEMM_SMALL;
+  if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
+  SR_CHECK(big_tiles < (1ll << 31), "gemm: too many tiles");
+  if (v == GEMM_BIG) {
+    launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
+                                       ldr, Y, ldy, M, N, K);
+  } else if (v == GEMM_DEEP) {
+    const dim3 grid((unsigned)big_tiles), block(512);
+#define SR_DEEP_CASE(E)                                                                          \
+  case E:                                                                                        \
+    hipLaunchKernelGGL(gemm_deep_kernel<E>, grid, block, 0, stream, X, lda, W, bias, R, ldr, Y, \
+                       ldy, M, N, K);                                                            \
+    break;
+    switch (epi) {
+      SR_DEEP_CASE(EPI_BIAS_F16)
+      SR_DEEP_CASE(EPI_BIAS_GELU_F16)
+      SR_DEEP_CASE(EPI_BIAS_RES_F32)
+      SR_DEEP_CASE(EPI_BIAS_RES_F16)
+      SR_DEEP_CASE(EPI_BIAS_TANH_F32)
+      default: SR_CHECK(false, "gemm: unknown epilogue");
+    }
+#undef SR_DEEP_CASE
+  } else if (v == GEMM_BIG_PERSIST) {
+    // one 8-wave workgroup per CU (128 KiB LDS): 32 per XCD
+    const int64_t per_xcd = std::min<int64_t>(32, ceil_div(big_tiles, 8));
+    launch_tile<256, 256, 2, 4, true>(epi, dim3((unsigned)(8 * per_xcd)), stream, X, lda, W, bias,
+                                      R, ldr, Y, ldy, M, N, K);
   } else {
     const int64_t tiles = (int64_t)(N / 128) * ceil_div(M, 128);
     SR_CHECK(tiles < (1ll << 31), "gemm: too many tiles");
-    launch_tile<128, 128, 2, 2>(epi, dim3((unsigned)tiles), stream, X, lda, W, bias, R, ldr, Y,
-                                ldy, M, N, K);
+    launch_tile<128, 128, 2, 2, false>(epi, dim3((unsigned)tiles), stream, X, lda, W, bias, R,
+                                       ldr, Y, ldy, M, N, K);
   }
   SR_LAUNCH_CHECK();
 }

@@ -17,7 +17,11 @@ enum Epilogue {
 void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream);
-void gemm_force_tile(int t);  // test hook: -1 auto, 0 = 128x128 tile, 1 = 256x256 tile
+enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_BIG_PERSIST = 2, GEMM_DEEP = 3 };
+void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
+                         const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
+                         int M, int N, int K, hipStream_t stream);
+void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 
 // k_attention.hip — ctx = MHA(qkv, key padding mask) for the first Sq query rows of each
 // sequence; ctx rows are laid out [B][Sq][d].

@@ -95,6 +95,8 @@ SIGNATURES = {
     "sr_rerank_select_dev": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "sr_profile_enable": (c_int, [c_int]),
     "sr_profile_read": (c_int, [POINTER(KernelStatC), c_int, P_I32]),
+    "sr_diag_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                             c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
 }
 
 _lib = None
