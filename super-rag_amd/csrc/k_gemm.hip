@@ -20,6 +20,7 @@
 // Workgroups are remapped so each XCD owns a contiguous range of tiles, n fastest: the X panel
 // of an m-tile is read from HBM once per XCD and re-served from that XCD's L2.
 #include <cstdlib>
+#include <type_traits>
 
 #include "sr_common.h"
 #include "sr_kernels.h"
@@ -215,6 +216,297 @@ __global__ __launch_bounds__(512, 2) void gemm_deep_kernel(
                           ldy);
 }
 
+// ---- "pipe" variant: 256 x 256 x 64, register-pipelined fragments, one barrier per K-step -------
+// A K-step is four MFMA phases of 16 MFMAs each (wave tile 128 n x 64 m = 8 x 4 16x16 tiles):
+//   p0: A[0..3]  x B  (k 0..31)     p1: A[4..7] x B (k 0..31)
+//   p2: A[0..3]  x B' (k 32..63)    p3: A[4..7] x B' (k 32..63)
+// The LDS fragments of phase p+1 are read while phase p's MFMAs run (two register sets, 64
+// VGPRs), so the LDS latency is hidden behind 16 MFMAs instead of exposed at every K-half.
+// Between p2 and p3 one raw s_barrier (behind vmcnt(0) lgkmcnt(0)) publishes K-step kt+1 (its
+// glds were issued a K-step earlier) and frees buffer kt&1, into which the glds of kt+2 are issued
+// before p3; p3 already reads K-step kt+1's first fragments from the other buffer.
+template <int EPI, bool CHECK, int FN, int FM>
+__device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0, int mw0, int lane,
+                                                int M, const float* __restrict__ bias,
+                                                const void* __restrict__ R, int64_t ldr,
+                                                void* __restrict__ Y, int64_t ldy) {
+  constexpr bool RES32 = EPI == EPI_BIAS_RES_F32, RES16 = EPI == EPI_BIAS_RES_F16;
+  constexpr bool OUT32 = EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32;
+  const int ng = nw0 + 4 * (lane >> 4);
+  float4v bv[FN];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) bv[i] = *reinterpret_cast<const float4v*>(bias + ng + i * 16);
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int m = mw0 + j * 16 + (lane & 15);
+    if (CHECK && m >= M) continue;
+    // the residual row segment first (all loads of the row group issued before its stores)
+    float4v r32[RES32 ? FN : 1];
+    half4 r16[RES16 ? FN : 1];
+    if constexpr (RES32) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        r32[i] = *reinterpret_cast<const float4v*>(reinterpret_cast<const float*>(R) + (int64_t)m * ldr + ng + i * 16);
+    }
+    if constexpr (RES16) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        r16[i] = *reinterpret_cast<const half4*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr + ng + i * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      float4v v = acc[i][j] + bv[i];
+      if constexpr (RES32) v += r32[i];
+      if constexpr (RES16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)r16[i][r];
+      }
+      if constexpr (EPI == EPI_BIAS_TANH_F32) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = tanhf(v[r]);
+      }
+      if constexpr (EPI == EPI_BIAS_GELU_F16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+      }
+      if constexpr (OUT32) {
+        *reinterpret_cast<float4v*>(reinterpret_cast<float*>(Y) + (int64_t)m * ldy + ng + i * 16) = v;
+      } else {
+        half4 h = {(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+        *reinterpret_cast<half4*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + ng + i * 16) = h;
+      }
+    }
+  }
+}
+
+// Buffer-resource LDS-DMA staging (buffer_load_dwordx4 ... lds): the tile's panel base lives in
+// the SGPR descriptor, the K offset in soffset, so a lane keeps ONE 32-bit VGPR offset per
+// instruction for the whole kernel; rows past num_records read as zero (no clamp needed).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t panel_rsrc(const half_t* base, int64_t bytes) {
+  const int nr = bytes > 0x7fffffffLL ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nr, 0x00020000);
+}
+template <int NI>
+__device__ __forceinline__ void stage_buf(__amdgpu_buffer_rsrc_t rs, const uint32_t (&voff)[NI],
+                                          int soff, half_t* lds_tile, int wave) {
+#if defined(__HIP_DEVICE_COMPILE__)  // device-only builtin: its host-pass instantiation made hipcc
+                                     // drop the host launch stubs of the kernel templates using it
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, SR_LDS(lds_tile + (wave * NI + i) * 8 * GBK), 16,
+                                             voff[i], soff, 0, 0);
+#endif
+}
+template <int NI>
+__device__ __forceinline__ void stage_offsets(uint32_t (&voff)[NI], int64_t ld, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = (wave * NI + i) * 8 + (lane >> 3);
+    voff[i] = (uint32_t)(((int64_t)r * ld + swz_chunk(r, lane & 7) * 8) * 2);
+  }
+}
+
+// Scheduling pin for one phase: R LDS fragment reads spread among its 16 MFMAs (the MFMAs of the
+// phase go first so the wait for the phase's own operands does not also wait for these reads).
+#define SR_INTERLEAVE(R)                                                   \
+  do {                                                                     \
+    _Pragma("unroll") for (int _r = 0; _r < (R); ++_r) {                   \
+      __builtin_amdgcn_sched_group_barrier(0x008, 16 / (R) / 2 > 0 ? 16 / (R) / 2 : 1, 0); \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                   \
+    }                                                                      \
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);                    \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+  } while (0)
+
+// PERSIST: one workgroup per CU walks a contiguous per-XCD tile range.  The next tile's first two
+// K-steps are staged (glds) right after the last K-step's barrier, before the epilogue, and the
+// epilogue's stores are left in flight: the next tile's first waits count them (vmcnt(8 + 32) /
+// vmcnt(32): the unchecked epilogue issues exactly FN * FM = 32 global stores per wave, checked in
+// the ISA), so the store drain overlaps the next tile's MFMAs instead of stalling the CU.
+template <int EPI, bool PERSIST>
+__global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
+    const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
+    const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
+    void* __restrict__ Y, int64_t ldy, int M, int N, int K) {
+  constexpr int BN = 256, BM = 256;
+  constexpr int STAGE = (BN + BM) * GBK;  // halfs per buffer (64 KiB)
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
+
+  const int tiles_n = N / BN;
+  const int nwg = tiles_n * ((M + BM - 1) / BM);
+  int t, t_end, t_step;
+  {
+    const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
+    const int lo = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+    t = lo + (blockIdx.x >> 3);
+    if constexpr (PERSIST) {
+      t_end = lo + q + (xcd < rem ? 1 : 0);
+      t_step = gridDim.x >> 3;
+    } else {
+      t_end = t + 1;
+      t_step = 1;
+    }
+  }
+  if (t >= t_end) return;
+  int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 2, wm = wave & 3;
+  const int nk = K / GBK;
+  const int arow = wn * 128 + (lane & 15), brow = wm * 64 + (lane & 15), c0 = lane >> 4;
+
+  uint32_t vw[4], vx[4];
+  stage_offsets<4>(vw, K, wave, lane);
+  stage_offsets<4>(vx, lda, wave, lane);
+  // tile panels: W rows [nn, nn+256) and X rows [mm, min(M, mm+256)) (a lambda may not carry the
+  // buffer-resource type through its signature: hipcc then drops the host stubs of this template)
+  auto stage = [&](int kt, half_t* s, int mm, int nn) {
+    stage_buf<4>(panel_rsrc(W + (int64_t)nn * K, (int64_t)BN * K * 2), vw, kt * GBK * 2, s, wave);
+    stage_buf<4>(panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2),
+                 vx, kt * GBK * 2, s + BN * GBK, wave);
+  };
+
+  float4v acc[8][4];
+  half8 aX[4], aY[4], bX[4], bY[4];
+
+  // prologue of the first tile
+  stage(0, lds, m0, n0);
+  if (nk > 1) {
+    stage(1, lds + STAGE, m0, n0);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  bool stores_pending = false;  // 32 unchecked epilogue stores of the previous tile in flight
+
+  // One K-step.  SN: 0 none, 1 stage kt+2 of this tile, 2 stage K-steps 0/1 of tile (mn, nn).
+  // RN: read kt+1's p0 fragments.  The barrier waits vmcnt(0), or vmcnt(32) when `lenient` (the
+  // only younger VMEM ops are the previous tile's epilogue stores).
+  // (a plain lambda with constant arguments, force-inlined: a generic lambda inside this kernel
+  // template made hipcc drop the host stubs of the other instantiations)
+  auto kstep = [&](int kt, const int SN, const bool RN, bool lenient, int mn, int nn,
+                   bool more_) __attribute__((always_inline)) {
+    half_t* cur = lds + (kt & 1) * STAGE;
+    const half_t* nxt = lds + ((kt + 1) & 1) * STAGE;
+    const half_t* Bc = cur + BN * GBK;
+    // p0: A[0..3] x B (k 0..31); reads A[4..7] (k 0..31)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aX[i] = read_frag(cur, arow + 16 * (4 + i), c0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bX[j], acc[i][j], 0, 0, 0);
+    SR_INTERLEAVE(4);
+    // p1: A[4..7] x B (k 0..31); reads A[0..3], B (k 32..63)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aY[i] = read_frag(cur, arow + 16 * i, c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bY[j] = read_frag(Bc, brow + 16 * j, c0 + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bX[j], acc[4 + i][j], 0, 0, 0);
+    SR_INTERLEAVE(8);
+    // p2: A[0..3] x B' (k 32..63); reads A[4..7] (k 32..63)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aX[i] = read_frag(cur, arow + 16 * (4 + i), c0 + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bY[j], acc[i][j], 0, 0, 0);
+    SR_INTERLEAVE(4);
+    // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
+    if (lenient)
+      asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (SN == 1) stage(kt + 2, cur, m0, n0);
+    if (SN == 2) {
+      if (more_) {
+        stage(0, lds, mn, nn);
+        stage(1, lds + STAGE, mn, nn);
+      }
+    }
+    // p3: A[4..7] x B' (k 32..63); reads K-step kt+1's p0 operands
+    if (RN) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) aY[i] = read_frag(nxt, arow + 16 * i, c0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bX[j] = read_frag(nxt + BN * GBK, brow + 16 * j, c0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bY[j], acc[4 + i][j], 0, 0, 0);
+    if (SN == 1) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    } else if (RN) {
+      SR_INTERLEAVE(8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aY[i] = read_frag(lds, arow + 16 * i, c0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bX[j] = read_frag(lds + BN * GBK, brow + 16 * j, c0);
+
+    const int t_next = t + t_step;
+    const bool more = PERSIST && t_next < t_end && nk > 1;
+    const int m0n = (t_next / tiles_n) * BM, n0n = (t_next % tiles_n) * BN;
+    int kt = 0;
+    bool lenient = stores_pending;
+    for (; kt + 2 < nk; ++kt) {
+      kstep(kt, 1, true, lenient, 0, 0, false);
+      lenient = false;
+    }
+    if (kt + 1 < nk) {
+      kstep(kt++, 0, true, lenient, 0, 0, false);
+      lenient = false;
+    }
+    if constexpr (PERSIST)
+      kstep(kt, 2, false, lenient, m0n, n0n, more);
+    else
+      kstep(kt, 0, false, lenient, 0, 0, false);
+
+    const bool full = m0 + BM <= M;
+    if (full)
+      store_tile_fast<EPI, false, 8, 4>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+    else
+      store_tile_fast<EPI, true, 8, 4>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+    if (!more) break;
+    // next tile: K-step 0 landed (younger: K-step 1's 8 glds + 32 stores when unchecked)
+    if (full)
+      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stores_pending = full;
+    t = t_next;
+    m0 = m0n;
+    n0 = n0n;
+  }
+}
+
 // PERSIST: a grid of 8 * G blocks walks the tiles; XCD group x = blockIdx & 7 owns a contiguous
 // tile range (X panels stay in that XCD's L2) and the next tile's first K-step is staged by
 // LDS-DMA while the current tile's epilogue runs, hiding the per-tile load latency.
@@ -360,6 +652,8 @@ static int forced_tile() {
   if (std::strcmp(e, "big") == 0) return GEMM_BIG;
   if (std::strcmp(e, "persist") == 0) return GEMM_BIG_PERSIST;
   if (std::strcmp(e, "deep") == 0) return GEMM_DEEP;
+  if (std::strcmp(e, "pipe") == 0) return GEMM_PIPE;
+  if (std::strcmp(e, "pipe_persist") == 0) return GEMM_PIPE_PERSIST;
   return -1;
 }
 
@@ -404,6 +698,27 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
       default: SR_CHECK(false, "gemm: unknown epilogue");
     }
 #undef SR_DEEP_CASE
+  } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
+    const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK;
+    const dim3 grid((unsigned)(persist ? std::min<int64_t>(256, big_tiles) : big_tiles)), block(512);
+#define SR_PIPE_CASE(E)                                                                          \
+  case E:                                                                                        \
+    if (persist)                                                                                 \
+      hipLaunchKernelGGL((gemm_pipe_kernel<E, true>), grid, block, 0, stream, X, lda, W, bias, R, \
+                         ldr, Y, ldy, M, N, K);                                                  \
+    else                                                                                         \
+      hipLaunchKernelGGL((gemm_pipe_kernel<E, false>), grid, block, 0, stream, X, lda, W, bias, R,\
+                         ldr, Y, ldy, M, N, K);                                                  \
+    break;
+    switch (epi) {
+      SR_PIPE_CASE(EPI_BIAS_F16)
+      SR_PIPE_CASE(EPI_BIAS_GELU_F16)
+      SR_PIPE_CASE(EPI_BIAS_RES_F32)
+      SR_PIPE_CASE(EPI_BIAS_RES_F16)
+      SR_PIPE_CASE(EPI_BIAS_TANH_F32)
+      default: SR_CHECK(false, "gemm: unknown epilogue");
+    }
+#undef SR_PIPE_CASE
   } else if (v == GEMM_BIG_PERSIST) {
     // one 8-wave workgroup per CU (128 KiB LDS): 32 per XCD
     const int64_t per_xcd = std::min<int64_t>(32, ceil_div(big_tiles, 8));

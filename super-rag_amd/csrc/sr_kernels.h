@@ -17,7 +17,7 @@ enum Epilogue {
 void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream);
-enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_BIG_PERSIST = 2, GEMM_DEEP = 3 };
+enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_BIG_PERSIST = 2, GEMM_DEEP = 3, GEMM_PIPE = 4, GEMM_PIPE_PERSIST = 5 };
 void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
                          const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
                          int M, int N, int K, hipStream_t stream);
