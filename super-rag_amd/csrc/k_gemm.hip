@@ -279,6 +279,79 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
   }
 }
 
+// fp16-output epilogue with 16-byte stores: tiles i = 2p and 2p + 1 of a row group are combined
+// with v_permlane16_swap (rows of 16 lanes: even row g keeps its 4 columns of tile 2p and takes
+// the odd partner's 4 columns of tile 2p, the odd row gets tile 2p + 1), so a lane owns 8
+// consecutive columns nb .. nb+7 and every store / residual load is one dwordx4 (half the store
+// instructions of the 8-byte layout; the store tail is issue-bound).
+template <int EPI, bool CHECK>
+__device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, int mw0, int lane,
+                                                int M, const float* __restrict__ bias,
+                                                const void* __restrict__ R, int64_t ldr,
+                                                void* __restrict__ Y, int64_t ldy) {
+  static_assert(EPI == EPI_BIAS_F16 || EPI == EPI_BIAS_GELU_F16 || EPI == EPI_BIAS_RES_F16,
+                "wide epilogue is for fp16 outputs");
+  const int g = lane >> 4, odd = g & 1;
+  const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
+  float4v b0[4], b1[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    b0[p] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p);
+    b1[p] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p + 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = mw0 + j * 16 + (lane & 15);
+    if (CHECK && m >= M) continue;
+    half8 r16[EPI == EPI_BIAS_RES_F16 ? 4 : 1];
+    if constexpr (EPI == EPI_BIAS_RES_F16) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        r16[p] = *reinterpret_cast<const half8*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr + nlane + 32 * p);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                         __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+        v[r] = __uint_as_float(sw[0]) + b0[p][r];
+        v[4 + r] = __uint_as_float(sw[1]) + b1[p][r];
+      }
+      if constexpr (EPI == EPI_BIAS_RES_F16) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] += (float)r16[p][r];
+      }
+      if constexpr (EPI == EPI_BIAS_GELU_F16) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
+      }
+      half8 h;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) h[r] = (half_t)v[r];
+      *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = h;
+    }
+  }
+}
+
+// One epilogue for the pipelined kernels; NSTORE = global store instructions per wave on the
+// unchecked path (the persistent kernel's counted vmcnt relies on it).
+template <int EPI>
+struct PipeEpi {
+  static constexpr bool WIDE = EPI == EPI_BIAS_F16 || EPI == EPI_BIAS_GELU_F16 || EPI == EPI_BIAS_RES_F16;
+  static constexpr int NSTORE = WIDE ? 16 : 32;
+  template <bool CHECK>
+  __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
+                                             const float* __restrict__ bias, const void* __restrict__ R,
+                                             int64_t ldr, void* __restrict__ Y, int64_t ldy) {
+    if constexpr (WIDE)
+      store_tile_wide<EPI, CHECK>(acc, nw0, mw0, lane, M, bias, R, ldr, Y, ldy);
+    else
+      store_tile_fast<EPI, CHECK, 8, 4>(acc, nw0, mw0, lane, M, bias, R, ldr, Y, ldy);
+  }
+};
+
 // Buffer-resource LDS-DMA staging (buffer_load_dwordx4 ... lds): the tile's panel base lives in
 // the SGPR descriptor, the K offset in soffset, so a lane keeps ONE 32-bit VGPR offset per
 // instruction for the whole kernel; rows past num_records read as zero (no clamp needed).
@@ -322,8 +395,11 @@ __device__ __forceinline__ void stage_offsets(uint32_t (&voff)[NI], int64_t ld, 
 // K-steps are staged (glds) right after the last K-step's barrier, before the epilogue, and the
 // epilogue's stores are left in flight: the next tile's first waits count them (vmcnt(8 + 32) /
 // vmcnt(32): the unchecked epilogue issues exactly FN * FM = 32 global stores per wave, checked in
-// the ISA), so the store drain overlaps the next tile's MFMAs instead of stalling the CU.
-template <int EPI, bool PERSIST>
+// the ISA; 16 dwordx4 stores for the fp16 outputs), so the store drain overlaps the next tile's
+// MFMAs instead of stalling the CU.
+// DIAG (timing experiments only, wrong results): 1 = no glds inside the K-loop (LDS re-read),
+// 2 = no epilogue (one masked store per lane keeps the accumulators live).
+template <int EPI, bool PERSIST, int DIAG = 0>
 __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
@@ -339,7 +415,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
     const int lo = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
     t = lo + (blockIdx.x >> 3);
-    if constexpr (PERSIST) {
+    if constexpr (PERSIST) {  // grid = 8 x G (host-checked), so every XCD group has G >= 1 walkers
       t_end = lo + q + (xcd < rem ? 1 : 0);
       t_step = gridDim.x >> 3;
     } else {
@@ -347,7 +423,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       t_step = 1;
     }
   }
-  if (t >= t_end) return;
+  if (t >= t_end || t_step <= 0) return;
   int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -421,13 +497,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bY[j], acc[i][j], 0, 0, 0);
     SR_INTERLEAVE(4);
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
-    if (lenient)
-      asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
-    else
+    if (lenient) {
+      if constexpr (PipeEpi<EPI>::NSTORE == 16)
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+    } else
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (SN == 1) stage(kt + 2, cur, m0, n0);
+    if (SN == 1 && DIAG != 1) stage(kt + 2, cur, m0, n0);
     if (SN == 2) {
       if (more_) {
         stage(0, lds, mn, nn);
@@ -489,16 +568,26 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       kstep(kt, 0, false, lenient, 0, 0, false);
 
     const bool full = m0 + BM <= M;
-    if (full)
-      store_tile_fast<EPI, false, 8, 4>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
-    else
-      store_tile_fast<EPI, true, 8, 4>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+    if constexpr (DIAG == 2) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (sacc == 12345.678f) reinterpret_cast<float*>(Y)[tid] = sacc;
+    } else if (full) {
+      PipeEpi<EPI>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+    } else {
+      PipeEpi<EPI>::template run<true>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+    }
     if (!more) break;
     // next tile: K-step 0 landed (younger: K-step 1's 8 glds + 32 stores when unchecked)
-    if (full)
-      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-    else
+    if (!full)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (PipeEpi<EPI>::NSTORE == 16)
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     stores_pending = full;
     t = t_next;
@@ -676,7 +765,7 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   ProfScope prof(epi_name(epi), stream, 2.0 * M * (double)N * K, bytes);
   const int64_t big_tiles = (N % 256 == 0) ? (int64_t)(N / 256) * ceil_div(M, 256) : 0;
   int v = variant >= 0 ? variant : forced_tile();
-  if (v < 0) v = big_tiles >= 512 ? GEMM_BIG : GEMM_SMALL;
+  if (v < 0) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_SMALL;
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
   SR_CHECK(big_tiles < (1ll << 31), "gemm: too many tiles");
   if (v == GEMM_BIG) {
@@ -698,9 +787,20 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
       default: SR_CHECK(false, "gemm: unknown epilogue");
     }
 #undef SR_DEEP_CASE
+  } else if (v == GEMM_DIAG_NOLOAD || v == GEMM_DIAG_NOEPI) {
+    const dim3 grid((unsigned)big_tiles), block(512);
+    if (v == GEMM_DIAG_NOLOAD)
+      hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, false, 1>), grid, block, 0, stream, X, lda,
+                         W, bias, R, ldr, Y, ldy, M, N, K);
+    else
+      hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, false, 2>), grid, block, 0, stream, X, lda,
+                         W, bias, R, ldr, Y, ldy, M, N, K);
   } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
     const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK;
-    const dim3 grid((unsigned)(persist ? std::min<int64_t>(256, big_tiles) : big_tiles)), block(512);
+    // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)
+    const int64_t g = persist ? 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8)) : big_tiles;
+    SR_CHECK(!persist || (g % 8 == 0 && g >= 8), "gemm: persistent grid must be a multiple of 8");
+    const dim3 grid((unsigned)g), block(512);
 #define SR_PIPE_CASE(E)                                                                          \
   case E:                                                                                        \
     if (persist)                                                                                 \

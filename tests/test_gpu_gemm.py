@@ -1,0 +1,62 @@
+"""GPU parity of the K4 MFMA GEMM variants (through the C-ABI diagnostic entry sr_diag_gemm)
+against a torch fp32 reference of the same op: Y = epi(X . W^T + b (+ R)).
+
+Covers every epilogue (bias, bias+GELU(erf), +fp32 residual, tanh, +fp16 residual) on every
+production variant (128x128, 256x256, pipelined 256x256, persistent pipelined), ragged M (partial
+last m-tile, where the buffer-load rows past M read as zero and are never stored) and grids where
+each persistent walker owns several tiles (the counted-vmcnt hand-over between tiles).
+Tolerance: |y - ref| <= 2e-3 * max(1, max|ref|) (fp16 operands / output, fp32 accumulation).
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {"small": 0, "big": 1, "pipe": 4, "pipe_persist": 5}
+
+
+def _run(variant, epi, M, N, K, seed=0):
+    import torch
+    from super_rag_amd import _native as NT
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    X = (torch.randn(M, K, device=dev, generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device=dev, generator=g) * 0.02).half()
+    b = torch.randn(N, device=dev, generator=g) * 0.1
+    R = None
+    if epi == 2:
+        R = torch.randn(M, N, device=dev, generator=g)
+    elif epi == 4:
+        R = torch.randn(M, N, device=dev, generator=g).half()
+    Y = torch.full((M, N), float("nan"), device=dev,
+                   dtype=torch.float32 if epi in (2, 3) else torch.float16)
+    NT.call("sr_diag_gemm", variant, epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
+            R.data_ptr() if R is not None else None, R.stride(0) if R is not None else 0,
+            Y.data_ptr(), Y.stride(0), M, N, K, 0, torch.cuda.current_stream().cuda_stream)
+    ref = X.float() @ W.float().T + b
+    if epi == 1:
+        ref = torch.nn.functional.gelu(ref)
+    elif epi in (2, 4):
+        ref = ref + R.float()
+    elif epi == 3:
+        ref = torch.tanh(ref)
+    torch.cuda.synchronize()
+    err = (Y.float() - ref).abs().max().item()
+    return err, 2e-3 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("variant", list(VARIANTS))
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+def test_gemm_variants_ragged(variant, epi):
+    for (M, N, K) in ((1000, 512, 768), (300, 256, 128), (4097, 768, 3072)):
+        err, tol = _run(VARIANTS[variant], epi, M, N, K, seed=M + epi)
+        assert err <= tol, f"{variant} epi{epi} {M}x{N}x{K}: max|err| {err:.3e} > {tol:.1e}"
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 4])
+def test_gemm_persistent_multi_tile(epi):
+    # 280 m-tiles x 3 n-tiles = 840 tiles > 256 walkers: every walker hands over >= 3 tiles
+    # (the last m-tile is ragged, so the checked epilogue runs mid-stream too)
+    err, tol = _run(VARIANTS["pipe_persist"], epi, 280 * 256 - 77, 768, 768, seed=7 + epi)
+    assert err <= tol, f"persistent epi{epi}: max|err| {err:.3e} > {tol:.1e}"
+    err, tol = _run(VARIANTS["pipe_persist"], epi, 96 * 256, 2304, 128, seed=11 + epi)
+    assert err <= tol, f"persistent K=128 epi{epi}: max|err| {err:.3e} > {tol:.1e}"
