@@ -417,6 +417,29 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
   SR_API_END
 }
 
+int sr_diag_attention(int variant, const void* qkv, const int32_t* mask, void* ctx, int B, int S,
+                      int Sq, int d, int heads, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(qkv);
+  SR_NONNULL(mask);
+  SR_NONNULL(ctx);
+  SR_CHECK(variant >= -1 && variant <= 1, "diag_attention: variant must be -1, 0 or 1");
+  SR_CHECK(variant != 1 || (heads > 0 && d == 64 * heads && S <= 512),
+           "diag_attention: variant 1 needs head dim 64 and S <= 512");
+  sr::DeviceGuard g(device);
+  sr::attention_force_variant(variant);
+  try {
+    sr::launch_attention(reinterpret_cast<const sr::half_t*>(qkv), mask,
+                         reinterpret_cast<sr::half_t*>(ctx), B, S, Sq, d, heads,
+                         reinterpret_cast<hipStream_t>(stream));
+  } catch (...) {
+    sr::attention_force_variant(-1);
+    throw;
+  }
+  sr::attention_force_variant(-1);
+  SR_API_END
+}
+
 // ---- profiling -------------------------------------------------------------------------------
 int sr_profile_enable(int on) {
   SR_API_BEGIN

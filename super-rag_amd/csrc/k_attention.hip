@@ -150,7 +150,200 @@ __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict
   }
 }
 
+// ---- K5b: one workgroup per (sequence, head, 128-query block), d_h = 64 -----------------------
+// The whole K and V of the head (S_pad = round_up(S, 32) rows of 128 B) are staged ONCE into LDS by
+// LDS-DMA (global_load_lds_dwordx4: 8 rows per wave-instruction) and shared by the 4 waves; each
+// wave owns 32 query rows (two 16-row tiles), so every K / V fragment read from LDS feeds two
+// MFMAs.  Scores are S^T = K Q^T (a lane holds one query's scores: in-lane max / sum plus two
+// xor-shuffles); P stays in registers as the B operand of O^T = V^T P^T, whose A operand (V^T) is
+// read straight from the row-major V image with ds_read_b64_tr_b16 (no transposing LDS writes).
+// LDS images (16-byte chunk c of row r):
+//   K: c ^ ((r >> 1) & 7)        -- conflict-free ds_read_b128 of 16 consecutive rows
+//   V: c ^ (((r >> 1) & 3) << 1) -- each 32-lane half of a transposed read touches 8 consecutive
+//                                   rows x one 32-byte column pair: 8 distinct 32-byte bank slots
+// Keys are processed in blocks of 128 with an online softmax (exact for any S <= 512).  Output
+// tiles t = 2p, 2p+1 are merged with v_permlane16_swap so each lane stores 8 consecutive dims
+// (16 B) of its query row.
+constexpr int A2_QB = 128;  // query rows per workgroup
+
+__device__ __forceinline__ int a2_kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+__device__ __forceinline__ int a2_vswz(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
+
+__device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
+  typedef short short4_t __attribute__((ext_vector_type(4)));
+  short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) short4_t*)(p));
+  return __builtin_bit_cast(half4, v);
+}
+
+__global__ __launch_bounds__(256) void attention64_kernel(const half_t* __restrict__ qkv,
+                                                          const int32_t* __restrict__ mask,
+                                                          half_t* __restrict__ ctx, int S, int Sq,
+                                                          int d, float scale_log2) {
+  constexpr int DH = 64;
+  extern __shared__ __attribute__((aligned(16))) char a2_smem[];
+  const int S_pad = (S + 31) & ~31;
+  half_t* Ks = reinterpret_cast<half_t*>(a2_smem);
+  half_t* Vs = Ks + S_pad * DH;
+  float* kbias = reinterpret_cast<float*>(Vs + S_pad * DH);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int64_t ld = 3 * (int64_t)d;
+  const half_t* base = qkv + (int64_t)b * S * ld + h * DH;
+
+  // ---- stage K and V (rows >= S replicate row S-1; their keys are masked) ----
+  for (int piece = wave; piece < S_pad / 8; piece += 4) {
+    const int r = piece * 8 + (lane >> 3);
+    const int rr = r < S ? r : S - 1;
+    const half_t* rowp = base + (int64_t)rr * ld;
+    __builtin_amdgcn_global_load_lds((const void*)(rowp + d + a2_kswz(r, lane & 7) * 8),
+                                     SR_LDS(Ks + piece * 8 * DH), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(rowp + 2 * d + a2_vswz(r, lane & 7) * 8),
+                                     SR_LDS(Vs + piece * 8 * DH), 16, 0, 0);
+  }
+  for (int r = tid; r < S_pad; r += 256)
+    kbias[r] = (r < S && mask[(int64_t)b * S + r] != 0) ? 0.f : -INFINITY;
+
+  // ---- Q fragments (B operand of S^T): lane holds Q[q][8 (lane>>4) + 32 s .. +7] ----
+  const int qw = blockIdx.x * A2_QB + wave * 32;  // first query row of this wave
+  const bool active = qw < Sq;
+  half8 qf[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    int qr = qw + 16 * u + (lane & 15);
+    qr = qr < S ? qr : S - 1;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      qf[u][s2] = *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + 8 * (lane >> 4) + 32 * s2);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!active) return;  // no barrier follows
+
+  const int g = lane >> 4;
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  float4v o[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[u][t] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < S_pad; k0 += 128) {
+    const int nkt = (S_pad - k0) >= 128 ? 8 : (S_pad - k0) / 16;  // 16-key tiles in this block
+    float p[2][8][4];
+    float tmax[2] = {-INFINITY, -INFINITY};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      if (kt < nkt) {
+        const int kr = k0 + 16 * kt + (lane & 15);
+        const half8 k0f = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+        const half8 k1f = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float4v acc = {0.f, 0.f, 0.f, 0.f};
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0f, qf[u][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1f, qf[u][1], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[r] * scale_log2 + kbias[k0 + 16 * kt + 4 * g + r];
+            p[u][kt][r] = v;
+            tmax[u] = fmaxf(tmax[u], v);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[u][kt][r] = -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float tm = fmaxf(tmax[u], __shfl_xor(tmax[u], 16, 64));
+      tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      const float m_new = fmaxf(m_run[u], tm);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run[u] - m_use);
+      m_run[u] = m_new;
+      l_run[u] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[u][t] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(p[u][kt][r] - m_use);
+          p[u][kt][r] = e;
+          l_run[u] += e;
+        }
+    }
+    // ---- O^T += V^T P^T over 32-key chunks (key order of the B operand: 32c + 4g + j, then
+    //      32c + 16 + 4g + j; the transposed V reads use the same order) ----
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (2 * c < nkt) {
+        half8 pb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pb[u][j] = (half_t)p[u][2 * c][j];
+            pb[u][4 + j] = (half_t)p[u][2 * c + 1][j];
+          }
+        // lane 4q+p of group g: V row k0 + 32c + 16hh + 4g + q, dims 16t + 4p .. +3
+        const int q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          half4 lo, hi;
+          {
+            const int r = k0 + 32 * c + 4 * g + q;
+            const int ch = a2_vswz(r, 2 * t + (pp >> 1));
+            lo = tr_read_b64(Vs + r * DH + ch * 8 + 4 * (pp & 1));
+          }
+          {
+            const int r = k0 + 32 * c + 16 + 4 * g + q;
+            const int ch = a2_vswz(r, 2 * t + (pp >> 1));
+            hi = tr_read_b64(Vs + r * DH + ch * 8 + 4 * (pp & 1));
+          }
+          const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            o[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[u], o[u][t], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- normalise and store: permlane16_swap merges d-tiles (2p, 2p+1) -> 8 dims per lane ----
+  const int odd = g & 1;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float l = l_run[u] + __shfl_xor(l_run[u], 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = qw + 16 * u + (lane & 15);
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      half8 hv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[u][2 * pp][r]),
+                                                         __float_as_uint(o[u][2 * pp + 1][r]), false, false);
+        hv[r] = (half_t)(__uint_as_float(sw[0]) * inv);
+        hv[4 + r] = (half_t)(__uint_as_float(sw[1]) * inv);
+      }
+      if (q < Sq)
+        *reinterpret_cast<half8*>(ctx + ((int64_t)b * Sq + q) * d + h * DH + 32 * pp + 16 * odd + 4 * (g & 2)) = hv;
+    }
+  }
+}
+
 }  // namespace
+
+static int g_attn_variant = -1;  // test hook: -1 auto, 0 = K5 (64-key tiles), 1 = K5b
+void attention_force_variant(int v) { g_attn_variant = v; }
 
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
                       int d, int heads, hipStream_t stream) {
@@ -158,18 +351,27 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
   SR_CHECK(dh * heads == d && (dh == 64 || dh == 32), "attention: head dim must be 32 or 64");
   if (B <= 0 || S <= 0) return;
   SR_CHECK(Sq >= 1 && Sq <= S, "attention: query rows must be in [1, S]");
-  const int nw = (int)std::min<int64_t>(4, ceil_div(Sq, 16));
-  dim3 grid((unsigned)ceil_div(Sq, 16 * nw), heads, B), block(64 * nw);
   const double flops = 4.0 * B * heads * (double)Sq * S * dh;
   const double bytes = 2.0 * B * (double)S * 3.0 * d + 2.0 * B * (double)Sq * d;
   ProfScope prof("attention", stream, flops, bytes);
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)dh);
-  if (dh == 64)
-    hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
+  const bool use_b = dh == 64 && S <= 512 && g_attn_variant != 0;
+  if (use_b) {
+    const int S_pad = (S + 31) & ~31;
+    const size_t shmem = (size_t)2 * S_pad * 64 * sizeof(half_t) + (size_t)S_pad * sizeof(float);
+    dim3 grid((unsigned)ceil_div(Sq, A2_QB), heads, B), block(256);
+    hipLaunchKernelGGL(attention64_kernel, grid, block, shmem, stream, qkv, mask, ctx, S, Sq, d,
                        scale_log2);
-  else
-    hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
-                       scale_log2);
+  } else {
+    const int nw = (int)std::min<int64_t>(4, ceil_div(Sq, 16));
+    dim3 grid((unsigned)ceil_div(Sq, 16 * nw), heads, B), block(64 * nw);
+    if (dh == 64)
+      hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
+                         scale_log2);
+    else
+      hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
+                         scale_log2);
+  }
   SR_LAUNCH_CHECK();
 }
 

@@ -28,6 +28,7 @@ void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 // sequence; ctx rows are laid out [B][Sq][d].
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
                       int d, int heads, hipStream_t stream);
+void attention_force_variant(int v);  // test hook: -1 auto, 0 = 64-key-tile kernel, 1 = K5b
 
 // k_encoder_misc.hip
 void launch_positions(const int32_t* ids, int32_t* pos, int B, int S, int offset, hipStream_t s);

@@ -97,6 +97,8 @@ SIGNATURES = {
     "sr_profile_read": (c_int, [POINTER(KernelStatC), c_int, P_I32]),
     "sr_diag_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                              c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
+    "sr_diag_attention": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                  c_int, c_int, c_void_p]),
 }
 
 _lib = None
