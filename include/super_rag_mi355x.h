@@ -196,9 +196,9 @@ int sr_profile_read(sr_kernel_stat* out, int max, int* n);
 /* One encoder GEMM Y = epi(X W^T + bias (+R)) on device buffers: X M x K fp16 (row stride lda),
  * W N x K fp16, bias N fp32, R residual (epi 2: fp32, epi 4: fp16, row stride ldr), Y row stride
  * ldy (fp16 for epi 0/1/4, fp32 for 2/3).  epi: 0 bias, 1 bias+GELU, 2 bias+residual fp32,
- * 3 bias+tanh (fp32 out), 4 bias+residual fp16.  variant: -1 auto, 0 128x128, 1 256x256 (8 waves),
- * 2 256x256 persistent, 3 256x256 4-slot ring, 4 pipelined 256x256, 5 persistent pipelined
- * 256x256 (6 / 7: timing-only diagnostics with wrong results). */
+ * 3 bias+tanh (fp32 out), 4 bias+residual fp16.  variant: -1 auto, 0 128x128, 1 256x256 (8 waves,
+ * 2-stage), 4 pipelined 256x256, 5 persistent pipelined 256x256 (6 / 7: timing-only diagnostics
+ * with wrong results). */
 int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, int device,
                  void* stream);

@@ -16,6 +16,7 @@
 // Embedding mode pools (CLS / masked mean) and L2-normalises (K7); cross-encoder mode applies the
 // RoBERTa classification head: tanh(GEMM(h16[CLS rows], Wc) + bc) (fp32) . Wout + bout (K4 + K8).
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "sr_kernels.h"
@@ -67,6 +68,19 @@ Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(
     register_target(p + "output.LayerNorm.weight", L.ln2g, D, false);
     register_target(p + "output.LayerNorm.bias", L.ln2b, D, false);
   }
+  // fp32 masters of the weights that LayerNorm folding rescales (fp16 residual stream only)
+  if (cfg.residual_fp16) {
+    for (int l = 0; l < cfg.layers; ++l) {
+      Layer& L = layers_[l];
+      const std::string p = "encoder.layer." + std::to_string(l) + ".";
+      L.wqkv32.reserve((size_t)3 * D * D * sizeof(float));
+      L.w132.reserve((size_t)F * D * sizeof(float));
+      targets_[p + "attention.self.query.weight"].master = L.wqkv32.as<float>();
+      targets_[p + "attention.self.key.weight"].master = L.wqkv32.as<float>() + D * D;
+      targets_[p + "attention.self.value.weight"].master = L.wqkv32.as<float>() + 2 * D * D;
+      targets_[p + "intermediate.dense.weight"].master = L.w132.as<float>();
+    }
+  }
   if (cfg.classifier == 1) {
     register_target("classifier.dense.weight", wc_, D * D, true);
     register_target("classifier.dense.bias", bc_, D, false);
@@ -116,7 +130,49 @@ void Encoder::set_weight(const std::string& name, const float* data, int64_t num
   } else {
     SR_HIP(hipMemcpy(t.ptr, data, (size_t)numel * sizeof(float), hipMemcpyHostToDevice));
   }
+  if (t.master)
+    SR_HIP(hipMemcpy(t.master, data, (size_t)numel * sizeof(float), hipMemcpyHostToDevice));
   is_set_[name] = true;
+  fold_ready_ = false;
+}
+
+// LayerNorm folding: with an fp16 residual stream the two LayerNorms of a block are
+// never materialised.  The GEMM that produces a residual sum u also writes per-row Chan partial
+// statistics; the next GEMM consumes u itself with LN(u) = (u - mu) rstd gamma + beta folded in:
+//   LN(u) . W^T + b = rstd (u . (W diag gamma)^T - mu c) + (W beta + b),  c[n] = sum_k W'[n][k],
+// and the residual epilogues rebuild LN(u) element-wise.  SR_LN_FOLD=0 disables it (A/B tests).
+bool Encoder::fold_enabled() const {
+  if (!cfg_.residual_fp16) return false;
+  if (cfg_.hidden % 256 != 0 || cfg_.intermediate % 256 != 0) return false;
+  const char* e = std::getenv("SR_LN_FOLD");
+  return !(e && e[0] == '0');
+}
+
+void Encoder::prepare_fold(hipStream_t s) {
+  if (fold_ready_) return;
+  const int64_t D = cfg_.hidden, F = cfg_.intermediate;
+  for (size_t l = 0; l < layers_.size(); ++l) {
+    Layer& L = layers_[l];
+    L.w1_f.reserve((size_t)F * D * sizeof(half_t));
+    L.c1.reserve((size_t)F * sizeof(float));
+    L.d1.reserve((size_t)F * sizeof(float));
+    launch_fold_ln_weight(L.w132.as<float>(), L.ln1g.as<float>(), L.ln1b.as<float>(),
+                          L.b1.as<float>(), (int)F, (int)D, L.w1_f.as<half_t>(), L.c1.as<float>(),
+                          L.d1.as<float>(), s);
+    L.b2_f.reserve((size_t)D * sizeof(float));  // FFN2 bias + beta of LN1 (rebuilt residual)
+    launch_vec_add(L.b2.as<float>(), L.ln1b.as<float>(), L.b2_f.as<float>(), (int)D, s);
+    if (l == 0) continue;  // layer 0 reads the (normalised) embedding LayerNorm output
+    const Layer& P = layers_[l - 1];
+    L.bo_f.reserve((size_t)D * sizeof(float));  // O-proj bias + beta of the previous LN2
+    launch_vec_add(L.bo.as<float>(), P.ln2b.as<float>(), L.bo_f.as<float>(), (int)D, s);
+    L.wqkv_f.reserve((size_t)3 * D * D * sizeof(half_t));
+    L.cqkv.reserve((size_t)3 * D * sizeof(float));
+    L.dqkv.reserve((size_t)3 * D * sizeof(float));
+    launch_fold_ln_weight(L.wqkv32.as<float>(), P.ln2g.as<float>(), P.ln2b.as<float>(),
+                          L.bqkv.as<float>(), (int)(3 * D), (int)D, L.wqkv_f.as<half_t>(),
+                          L.cqkv.as<float>(), L.dqkv.as<float>(), s);
+  }
+  fold_ready_ = true;
 }
 
 std::string Encoder::missing() const {
@@ -139,6 +195,12 @@ void Encoder::ensure_ws(int64_t tokens, int B) {
   ctx_.reserve((size_t)tokens * d * sizeof(half_t));
   y32_.reserve((size_t)tokens * d * sizeof(float));
   ffn_.reserve((size_t)tokens * F * sizeof(half_t));
+  if (cfg_.residual_fp16) {
+    statA_.reserve((size_t)tokens * (d / 128 + 1) * 2 * sizeof(float));
+    statB_.reserve((size_t)tokens * (d / 128 + 1) * 2 * sizeof(float));
+    mrA_.reserve((size_t)tokens * 2 * sizeof(float));
+    mrB_.reserve((size_t)tokens * 2 * sizeof(float));
+  }
   (void)B;
   ws_tokens_ = tokens;
 }
@@ -182,6 +244,10 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
   // B CLS rows (exact: every other row of the last layer is dead).
   const bool cls_only = (mode == 1) || (pool == SR_POOL_CLS);
 
+  const bool fold = fold_enabled();
+  if (fold) prepare_fold(s);
+  const int nparts = d / 128;
+
   for (int64_t b0 = 0; b0 < B; b0 += seqs_per_chunk) {
     const int nb = (int)std::min<int64_t>(seqs_per_chunk, B - b0);
     const int M = nb * S;
@@ -192,7 +258,62 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
     launch_embed_ln(cids, pos, ctypes, wemb_.as<half_t>(), pemb_.as<half_t>(), temb_.as<half_t>(),
                     embg_.as<float>(), embb_.as<float>(), cfg_.ln_eps, M, d, cfg_.vocab_size,
                     cfg_.max_position, cfg_.type_vocab, h16, h32w, s);
-    for (size_t l = 0; l < layers_.size(); ++l) {
+    if (fold) {
+      // u (un-normalised residual sums) lives in h16 (in place); compact last-layer rows in y32_.
+      // sA / mrA: statistics of u after the O-projection, sB / mrB: after FFN2.
+      half_t* U = h16;
+      half_t* Uc = reinterpret_cast<half_t*>(y);
+      float* sA = statA_.as<float>();
+      float* sB = statB_.as<float>();
+      float* mA = mrA_.as<float>();
+      float* mB = mrB_.as<float>();
+      for (size_t l = 0; l < layers_.size(); ++l) {
+        const Layer& L = layers_[l];
+        const bool last = cls_only && l + 1 == layers_.size();
+        const Layer* P = l > 0 ? &layers_[l - 1] : nullptr;
+        if (l == 0) {
+          launch_gemm(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
+                      3 * d, M, 3 * d, d, s);
+        } else {  // A = u of the previous block, its LN2 folded into W'
+          LnFold lq;
+          lq.mr = mB;
+          lq.colsum = L.cqkv.as<float>();
+          launch_gemm(EPI_LNF_F16, U, d, L.wqkv_f.as<half_t>(), L.dqkv.as<float>(), nullptr, 0, qkv,
+                      3 * d, M, 3 * d, d, s, &lq);
+        }
+        const int Mr = last ? nb : M;
+        launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
+        // O-projection + residual LN2(l-1)(u) -> u1 (in place, or compact rows) + partials sA
+        half_t* Uo = last ? Uc : U;
+        LnFold lo;
+        lo.mr = mB;
+        lo.stat_ld = last ? S : 1;
+        lo.gamma = P ? P->ln2g.as<float>() : nullptr;
+        lo.stat_out = sA;
+        launch_gemm(l == 0 ? EPI_RES16_STATS : EPI_LNR16_STATS, ctx, d, L.wo.as<half_t>(),
+                    (l == 0 ? L.bo : L.bo_f).as<float>(), U, last ? (int64_t)S * d : d, Uo, d, Mr,
+                    d, d, s, &lo);
+        launch_ln_stats_finalize(sA, nparts, cfg_.ln_eps, Mr, mA, s);
+        // FFN1 on LN1(u1) folded; FFN2 + residual LN1(u1) -> u2 (in place) + partials sB
+        LnFold l1;
+        l1.mr = mA;
+        l1.colsum = L.c1.as<float>();
+        launch_gemm(EPI_LNF_GELU_F16, Uo, d, L.w1_f.as<half_t>(), L.d1.as<float>(), nullptr, 0, ffn,
+                    F, Mr, F, d, s, &l1);
+        LnFold l2;
+        l2.mr = mA;
+        l2.gamma = L.ln1g.as<float>();
+        l2.stat_out = sB;
+        launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo, d,
+                    Mr, d, F, s, &l2);
+        launch_ln_stats_finalize(sB, nparts, cfg_.ln_eps, Mr, mB, s);
+      }
+      // final LayerNorm (LN2 of the last block) of the rows that are consumed -> h16
+      const Layer& Lz = layers_.back();
+      launch_ln_apply(cls_only ? Uc : U, d, mB, Lz.ln2g.as<float>(), Lz.ln2b.as<float>(),
+                      cls_only ? nb : M, d, h16, s);
+    }
+    for (size_t l = 0; l < (fold ? 0 : layers_.size()); ++l) {
       const Layer& L = layers_[l];
       const bool last = cls_only && l + 1 == layers_.size();
       launch_gemm(EPI_BIAS_F16, h16, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,

@@ -236,6 +236,98 @@ __global__ void convert_f32_f16_kernel(const float* __restrict__ in, half_t* __r
   if (i < n) out[i] = (half_t)in[i];
 }
 
+// LayerNorm folding of a projection weight (one workgroup per output row n):
+//   w16[n][k] = fp16(W[n][k] * gamma[k]);  colsum[n] = sum_k float(w16[n][k]);
+//   bias_out[n] = sum_k W[n][k] * beta[k] + bias[n]      (fp32 master weights)
+__global__ __launch_bounds__(256) void fold_ln_weight_kernel(const float* __restrict__ w32,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta,
+                                                             const float* __restrict__ bias, int K,
+                                                             half_t* __restrict__ w16,
+                                                             float* __restrict__ colsum,
+                                                             float* __restrict__ bias_out) {
+  __shared__ float red[2][4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  float cs = 0.f, bs = 0.f;
+  for (int k = tid; k < K; k += 256) {
+    const float w = w32[(int64_t)n * K + k];
+    const half_t h = (half_t)(w * gamma[k]);
+    w16[(int64_t)n * K + k] = h;
+    cs += (float)h;
+    bs = fmaf(w, beta[k], bs);
+  }
+  cs = wave_sum(cs);
+  bs = wave_sum(bs);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = cs;
+    red[1][tid >> 6] = bs;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    colsum[n] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    bias_out[n] = red[1][0] + red[1][1] + red[1][2] + red[1][3] + bias[n];
+  }
+}
+
+// (mu, rstd) per row from Chan partials (n = 128 each): mu = sum S_i / n,
+// M2 = sum M2_i + 128 sum (S_i / 128 - mu)^2, rstd = 1 / sqrt(M2 / n + eps).  One thread per row.
+__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ stat,
+                                                                int nparts, float eps, int M,
+                                                                float* __restrict__ mr) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const float* p = stat + m * nparts * 2;
+  float sum[16], m2s = 0.f, s = 0.f;
+  for (int i = 0; i < nparts; ++i) {
+    const float2 v = reinterpret_cast<const float2*>(p)[i];
+    sum[i & 15] = v.x;
+    s += v.x;
+    m2s += v.y;
+  }
+  const float ntot = 128.f * (float)nparts;
+  const float mu = s / ntot;
+  for (int i = 0; i < nparts; ++i) {
+    const float dm = sum[i & 15] * (1.f / 128.f) - mu;
+    m2s += 128.f * dm * dm;
+  }
+  float2 o;
+  o.x = mu;
+  o.y = 1.f / sqrtf(m2s / ntot + eps);
+  reinterpret_cast<float2*>(mr)[m] = o;
+}
+
+// h16 = LayerNorm(u) with (mu, rstd) from mr (one wave per row).
+template <int NV>
+__global__ __launch_bounds__(256) void ln_apply_kernel(const half_t* __restrict__ u, int64_t ldu,
+                                                       const float* __restrict__ mr,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, int M, int d,
+                                                       half_t* __restrict__ h16) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const float mu = mr[2 * m], rstd = mr[2 * m + 1];
+  const int n4 = d >> 2;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n4) {
+      const half4 hv = reinterpret_cast<const half4*>(u + m * ldu)[c];
+      const float4v g = reinterpret_cast<const float4v*>(gamma)[c];
+      const float4v bb = reinterpret_cast<const float4v*>(beta)[c];
+      half4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (half_t)fmaf(((float)hv[j] - mu) * rstd, g[j], bb[j]);
+      reinterpret_cast<half4*>(h16 + m * d)[c] = o;
+    }
+  }
+}
+
+__global__ void vec_add_kernel(const float* a, const float* b, float* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
 }  // namespace
 
 void launch_positions(const int32_t* ids, int32_t* pos, int B, int S, int offset, hipStream_t s) {
@@ -307,6 +399,45 @@ void launch_convert_f32_f16(const float* in, half_t* out, int64_t n, hipStream_t
   if (n <= 0) return;
   hipLaunchKernelGGL(convert_f32_f16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
                      in, out, n);
+  SR_LAUNCH_CHECK();
+}
+
+}  // namespace sr
+
+namespace sr {
+
+void launch_fold_ln_weight(const float* w32, const float* gamma, const float* beta,
+                           const float* bias, int N, int K, half_t* w16, float* colsum,
+                           float* bias_out, hipStream_t s) {
+  if (N <= 0) return;
+  hipLaunchKernelGGL(fold_ln_weight_kernel, dim3(N), dim3(256), 0, s, w32, gamma, beta, bias, K,
+                     w16, colsum, bias_out);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_ln_stats_finalize(const float* stat, int nparts, float eps, int M, float* mr,
+                              hipStream_t s) {
+  SR_CHECK(nparts >= 1 && nparts <= 16, "ln_stats_finalize: 1..16 partials per row");
+  if (M <= 0) return;
+  ProfScope prof("ln_stats_finalize", s, 0.0, (double)M * (nparts * 8.0 + 8.0));
+  hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256), 0, s,
+                     stat, nparts, eps, M, mr);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float* gamma,
+                     const float* beta, int M, int d, half_t* h16, hipStream_t s) {
+  SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "ln_apply: hidden must be a multiple of 4, <= 2048");
+  if (M <= 0) return;
+  ProfScope prof("ln_apply", s, 0.0, (double)M * d * 4.0);
+  hipLaunchKernelGGL(ln_apply_kernel<MAXV>, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, u, ldu,
+                     mr, gamma, beta, M, d, h16);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(vec_add_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, a, b, out, n);
   SR_LAUNCH_CHECK();
 }
 

@@ -112,110 +112,6 @@ __device__ __forceinline__ void store_tile(float4v (&acc)[FN][FM], int nw0, int 
   }
 }
 
-// ---- "deep" variant: 256 x 256 tile, K-step 32, 4-slot LDS ring, 3 K-steps in flight ------------
-// The 2-slot ring above drains every glds at each K-step barrier (vmcnt(0)): with W / X served
-// from MALL / HBM the load latency (1-2 us) exceeds one K-step of MFMA work and stalls the
-// workgroup.  Here each K-step issues the loads of step kt+3 into the slot read at kt-1, waits
-// with a COUNTED vmcnt for step kt+1 only, and synchronises with a raw s_barrier (a
-// __syncthreads() would add vmcnt(0) and drain the ring).  Rows are 64 B (32 fp16): the 16-byte
-// chunk c of row r is stored at chunk c ^ ((r >> 2) & 2), conflict-free for ds_read_b128
-// (exhaustively checked for the four lane groups).
-constexpr int DBK = 32;
-constexpr int DSLOTS = 4;
-
-__device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((row >> 2) & 2); }
-
-// NI wave-instructions of one 64-B-row tile: instruction i fills LDS rows prow..prow+15.
-template <int NI>
-__device__ __forceinline__ void stage_rows64(const half_t* __restrict__ g, int64_t ld, int row0,
-                                             int row_max, int k0, half_t* lds_tile, int wave,
-                                             int lane) {
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int prow = (wave * NI + i) * 16;
-    const int r = prow + (lane >> 2);
-    int gr = row0 + r;
-    gr = gr < row_max ? gr : row_max - 1;
-    const half_t* src = g + (int64_t)gr * ld + k0 + swz64(r, lane & 3) * 8;
-    __builtin_amdgcn_global_load_lds((const void*)src, SR_LDS(lds_tile + prow * DBK), 16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ half8 read_frag64(const half_t* lds_tile, int row, int chunk) {
-  return *reinterpret_cast<const half8*>(lds_tile + row * DBK + swz64(row, chunk) * 8);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void gemm_deep_kernel(
-    const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
-    const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
-    void* __restrict__ Y, int64_t ldy, int M, int N, int K) {
-  constexpr int BN = 256, BM = 256, WN = 2, WM = 4, WAVES = 8;
-  constexpr int FN = BN / WN / 16, FM = BM / WM / 16;   // 8 x 4 tiles of 16x16 per wave
-  constexpr int NI = BN / 16 / WAVES;                   // 2 glds per operand per wave
-  constexpr int SLOT = (BN + BM) * DBK;                 // halfs per ring slot (32 KiB)
-  __shared__ __attribute__((aligned(16))) half_t lds[DSLOTS * SLOT];  // 128 KiB
-
-  const int tiles_n = N / BN;
-  const int nwg = tiles_n * ((M + BM - 1) / BM);
-  const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
-  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (blockIdx.x >> 3);
-  const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave / WM, wm = wave % WM;
-  const int nk = K / DBK;
-
-  auto stage = [&](int kt) {
-    half_t* s = lds + (kt % DSLOTS) * SLOT;
-    stage_rows64<NI>(W, K, n0, N, kt * DBK, s, wave, lane);
-    stage_rows64<NI>(X, lda, m0, M, kt * DBK, s + BN * DBK, wave, lane);
-  };
-
-  float4v acc[FN][FM];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: slots 0..2 in flight (4 glds per wave each); wait for slot 0
-  stage(0);
-  if (nk > 1) stage(1);
-  if (nk > 2) stage(2);
-  if (nk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 3 < nk) stage(kt + 3);  // slot (kt+3)%4 == slot read at kt-1: freed by its barrier
-    const half_t* As = lds + (kt % DSLOTS) * SLOT;
-    const half_t* Bs = As + BN * DBK;
-    half8 a[FN], b[FM];
-    const int chunk = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < FN; ++i) a[i] = read_frag64(As, wn * (BN / WN) + i * 16 + (lane & 15), chunk);
-#pragma unroll
-    for (int j = 0; j < FM; ++j) b[j] = read_frag64(Bs, wm * (BM / WM) + j * 16 + (lane & 15), chunk);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int j = 0; j < FM; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // retire step kt+1 (its glds were issued two steps ago); later steps stay in flight
-    const int ahead = nk - 2 - kt;  // steps issued after kt+1
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  store_tile<EPI, FN, FM>(acc, n0 + wn * (BN / WN), m0 + wm * (BM / WM), lane, M, bias, R, ldr, Y,
-                          ldy);
-}
-
 // ---- "pipe" variant: 256 x 256 x 64, register-pipelined fragments, one barrier per K-step -------
 // A K-step is four MFMA phases of 16 MFMAs each (wave tile 128 n x 64 m = 8 x 4 16x16 tiles):
 //   p0: A[0..3]  x B  (k 0..31)     p1: A[4..7] x B (k 0..31)
@@ -284,13 +180,23 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
 // the odd partner's 4 columns of tile 2p, the odd row gets tile 2p + 1), so a lane owns 8
 // consecutive columns nb .. nb+7 and every store / residual load is one dwordx4 (half the store
 // instructions of the 8-byte layout; the store tail is issue-bound).
+//
+// LayerNorm folding (EPI_LNF_* / EPI_LNR16_STATS / EPI_RES16_STATS): (mu, rstd) of a row come
+// from mr (launch_ln_stats_finalize of the producer's partials).  The *_STATS epilogues write the
+// Chan partials of their own fp16-rounded outputs: per 128-column wave span the sum over the 4
+// lane groups (xor-shuffles 16 / 32), then M2 around that span's mean.
 template <int EPI, bool CHECK>
 __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, int mw0, int lane,
-                                                int M, const float* __restrict__ bias,
+                                                int M, int N, const float* __restrict__ bias,
                                                 const void* __restrict__ R, int64_t ldr,
-                                                void* __restrict__ Y, int64_t ldy) {
-  static_assert(EPI == EPI_BIAS_F16 || EPI == EPI_BIAS_GELU_F16 || EPI == EPI_BIAS_RES_F16,
-                "wide epilogue is for fp16 outputs");
+                                                void* __restrict__ Y, int64_t ldy,
+                                                const LnFold& lf) {
+  constexpr bool LNF = EPI == EPI_LNF_F16 || EPI == EPI_LNF_GELU_F16;
+  constexpr bool RESN = EPI == EPI_BIAS_RES_F16 || EPI == EPI_RES16_STATS;
+  constexpr bool LNR = EPI == EPI_LNR16_STATS;
+  constexpr bool STATS = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS;
+  constexpr bool GELU = EPI == EPI_BIAS_GELU_F16 || EPI == EPI_LNF_GELU_F16;
+  static_assert(EPI == EPI_BIAS_F16 || GELU || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
   float4v b0[4], b1[4];
@@ -299,16 +205,41 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     b0[p] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p);
     b1[p] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p + 4);
   }
+  // LNF: column sums c[n]; LNR: the residual's LayerNorm weight (its beta is in the bias)
+  float4v c0[(LNF || LNR) ? 4 : 1], c1[(LNF || LNR) ? 4 : 1];
+  if constexpr (LNF || LNR) {
+    const float* cv = LNF ? lf.colsum : lf.gamma;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      c0[p] = *reinterpret_cast<const float4v*>(cv + nlane + 32 * p);
+      c1[p] = *reinterpret_cast<const float4v*>(cv + nlane + 32 * p + 4);
+    }
+  }
+  float2 mrj[(LNF || LNR) ? 4 : 1];
+  if constexpr (LNF || LNR) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int m = mw0 + j * 16 + (lane & 15);
+      m = (CHECK && m >= M) ? M - 1 : m;
+      mrj[j] = *reinterpret_cast<const float2*>(lf.mr + (int64_t)m * lf.stat_ld * 2);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int m = mw0 + j * 16 + (lane & 15);
     if (CHECK && m >= M) continue;
-    half8 r16[EPI == EPI_BIAS_RES_F16 ? 4 : 1];
-    if constexpr (EPI == EPI_BIAS_RES_F16) {
+    half8 r16[(RESN || LNR) ? 4 : 1];
+    if constexpr (RESN || LNR) {
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         r16[p] = *reinterpret_cast<const half8*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr + nlane + 32 * p);
     }
+    float mu = 0.f, rstd = 1.f;
+    if constexpr (LNF || LNR) {
+      mu = mrj[j].x;
+      rstd = mrj[j].y;
+    }
+    half8 hv[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       float v[8];
@@ -316,37 +247,85 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       for (int r = 0; r < 4; ++r) {
         const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
                                                          __float_as_uint(acc[2 * p + 1][j][r]), false, false);
-        v[r] = __uint_as_float(sw[0]) + b0[p][r];
-        v[4 + r] = __uint_as_float(sw[1]) + b1[p][r];
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
       }
-      if constexpr (EPI == EPI_BIAS_RES_F16) {
+      if constexpr (LNF) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = fmaf(rstd, v[r] - mu * c0[p][r], b0[p][r]);
+          v[4 + r] = fmaf(rstd, v[4 + r] - mu * c1[p][r], b1[p][r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] += b0[p][r];
+          v[4 + r] += b1[p][r];
+        }
+      }
+      if constexpr (RESN) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] += (float)r16[p][r];
       }
-      if constexpr (EPI == EPI_BIAS_GELU_F16) {
+      if constexpr (LNR) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = fmaf(((float)r16[p][r] - mu) * rstd, c0[p][r], v[r]);
+          v[4 + r] = fmaf(((float)r16[p][4 + r] - mu) * rstd, c1[p][r], v[4 + r]);
+        }
+      }
+      if constexpr (GELU) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
       }
-      half8 h;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) h[r] = (half_t)v[r];
-      *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = h;
+      for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
+      *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
+    }
+    if constexpr (STATS) {
+      // partner lanes (xor 16 / 32) share the row m, so they are active together
+      float sum = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) sum += (float)hv[p][r];
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      const float mw = sum * (1.f / 128.f);
+      float m2 = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float dx = (float)hv[p][r] - mw;
+          m2 = fmaf(dx, dx, m2);
+        }
+      m2 += __shfl_xor(m2, 16, 64);
+      m2 += __shfl_xor(m2, 32, 64);
+      if (g == 0) {
+        float2 st;
+        st.x = sum;
+        st.y = m2;
+        *reinterpret_cast<float2*>(lf.stat_out + ((int64_t)m * (N >> 7) + (nw0 >> 7)) * 2) = st;
+      }
     }
   }
 }
 
 // One epilogue for the pipelined kernels; NSTORE = global store instructions per wave on the
-// unchecked path (the persistent kernel's counted vmcnt relies on it).
+// unchecked path (the persistent kernel's counted vmcnt relies on it: extra stores, such as the
+// statistics of the *_STATS epilogues, only make its waits stricter).
 template <int EPI>
 struct PipeEpi {
-  static constexpr bool WIDE = EPI == EPI_BIAS_F16 || EPI == EPI_BIAS_GELU_F16 || EPI == EPI_BIAS_RES_F16;
+  static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
   static constexpr int NSTORE = WIDE ? 16 : 32;
   template <bool CHECK>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
-                                             const float* __restrict__ bias, const void* __restrict__ R,
-                                             int64_t ldr, void* __restrict__ Y, int64_t ldy) {
+                                             int N, const float* __restrict__ bias,
+                                             const void* __restrict__ R, int64_t ldr,
+                                             void* __restrict__ Y, int64_t ldy, const LnFold& lf) {
     if constexpr (WIDE)
-      store_tile_wide<EPI, CHECK>(acc, nw0, mw0, lane, M, bias, R, ldr, Y, ldy);
+      store_tile_wide<EPI, CHECK>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf);
     else
       store_tile_fast<EPI, CHECK, 8, 4>(acc, nw0, mw0, lane, M, bias, R, ldr, Y, ldy);
   }
@@ -403,7 +382,7 @@ template <int EPI, bool PERSIST, int DIAG = 0>
 __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
-    void* __restrict__ Y, int64_t ldy, int M, int N, int K) {
+    void* __restrict__ Y, int64_t ldy, int M, int N, int K, const LnFold lf) {
   constexpr int BN = 256, BM = 256;
   constexpr int STAGE = (BN + BM) * GBK;  // halfs per buffer (64 KiB)
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
@@ -576,9 +555,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
       if (sacc == 12345.678f) reinterpret_cast<float*>(Y)[tid] = sacc;
     } else if (full) {
-      PipeEpi<EPI>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+      PipeEpi<EPI>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr,
+                                        Y, ldy, lf);
     } else {
-      PipeEpi<EPI>::template run<true>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, R, ldr, Y, ldy);
+      PipeEpi<EPI>::template run<true>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr,
+                                       Y, ldy, lf);
     }
     if (!more) break;
     // next tile: K-step 0 landed (younger: K-step 1's 8 glds + 32 stores when unchecked)
@@ -726,6 +707,10 @@ static const char* epi_name(int epi) {
     case EPI_BIAS_GELU_F16: return "gemm_f16_bias_gelu";
     case EPI_BIAS_RES_F32: return "gemm_f16_bias_residual";
     case EPI_BIAS_RES_F16: return "gemm_f16_bias_residual16";
+    case EPI_LNF_F16: return "gemm_f16_lnfold";
+    case EPI_LNF_GELU_F16: return "gemm_f16_lnfold_gelu";
+    case EPI_RES16_STATS: return "gemm_f16_residual16_stats";
+    case EPI_LNR16_STATS: return "gemm_f16_lnres16_stats";
     default: return "gemm_f16_bias_tanh";
   }
 }
@@ -739,8 +724,6 @@ static int forced_tile() {
   if (!e) return -1;
   if (std::strcmp(e, "small") == 0) return GEMM_SMALL;
   if (std::strcmp(e, "big") == 0) return GEMM_BIG;
-  if (std::strcmp(e, "persist") == 0) return GEMM_BIG_PERSIST;
-  if (std::strcmp(e, "deep") == 0) return GEMM_DEEP;
   if (std::strcmp(e, "pipe") == 0) return GEMM_PIPE;
   if (std::strcmp(e, "pipe_persist") == 0) return GEMM_PIPE_PERSIST;
   return -1;
@@ -748,53 +731,53 @@ static int forced_tile() {
 
 void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
-                 hipStream_t stream) {
-  launch_gemm_variant(-1, epi, X, lda, W, bias, R, ldr, Y, ldy, M, N, K, stream);
+                 hipStream_t stream, const LnFold* lf) {
+  launch_gemm_variant(-1, epi, X, lda, W, bias, R, ldr, Y, ldy, M, N, K, stream, lf);
 }
 
 void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
                          const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
-                         int M, int N, int K, hipStream_t stream) {
+                         int M, int N, int K, hipStream_t stream, const LnFold* lf) {
   SR_CHECK(K % GBK == 0, "gemm: K must be a multiple of 64");
   SR_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128");
   SR_CHECK(lda % 8 == 0 && ldy % 4 == 0, "gemm: leading dimensions must keep 16-byte rows");
+  const bool fold = epi >= EPI_LNF_F16;
+  SR_CHECK(epi >= 0 && epi <= EPI_LNR16_STATS, "gemm: unknown epilogue");
+  SR_CHECK(!fold || (lf && N % 256 == 0), "gemm: LayerNorm-folded epilogues need LnFold, N % 256");
+  SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNR16_STATS) || lf->mr,
+           "gemm: LN-folded operand needs its row statistics");
+  SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16) || lf->colsum, "gemm: LNF needs colsum");
+  SR_CHECK(epi != EPI_LNR16_STATS || lf->gamma, "gemm: LNR needs the LayerNorm weight");
+  SR_CHECK(!(epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS) || lf->stat_out,
+           "gemm: *_STATS epilogue needs stat_out");
   if (M <= 0) return;
-  const double out_b = (epi == EPI_BIAS_RES_F32 || epi == EPI_BIAS_TANH_F32) ? 4.0 : 2.0;
-  const double res_b = epi == EPI_BIAS_RES_F32 ? 4.0 : (epi == EPI_BIAS_RES_F16 ? 2.0 : 0.0);
+  const bool out32 = epi == EPI_BIAS_RES_F32 || epi == EPI_BIAS_TANH_F32;
+  const double out_b = out32 ? 4.0 : 2.0;
+  const double res_b = epi == EPI_BIAS_RES_F32 ? 4.0
+                       : (epi == EPI_BIAS_RES_F16 || epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS) ? 2.0
+                                                                                                     : 0.0;
   const double bytes = 2.0 * ((double)M * K + (double)N * K) + (out_b + res_b) * (double)M * N;
   ProfScope prof(epi_name(epi), stream, 2.0 * M * (double)N * K, bytes);
   const int64_t big_tiles = (N % 256 == 0) ? (int64_t)(N / 256) * ceil_div(M, 256) : 0;
+  SR_CHECK(big_tiles < (1ll << 31), "gemm: too many tiles");
   int v = variant >= 0 ? variant : forced_tile();
   if (v < 0) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_SMALL;
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
-  SR_CHECK(big_tiles < (1ll << 31), "gemm: too many tiles");
+  if (fold && (v == GEMM_SMALL || v == GEMM_BIG)) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_PIPE;
+  const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) && !out32;
+  SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
+  const LnFold lfv = lf ? *lf : LnFold{};
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
                                        ldr, Y, ldy, M, N, K);
-  } else if (v == GEMM_DEEP) {
-    const dim3 grid((unsigned)big_tiles), block(512);
-#define SR_DEEP_CASE(E)                                                                          \
-  case E:                                                                                        \
-    hipLaunchKernelGGL(gemm_deep_kernel<E>, grid, block, 0, stream, X, lda, W, bias, R, ldr, Y, \
-                       ldy, M, N, K);                                                            \
-    break;
-    switch (epi) {
-      SR_DEEP_CASE(EPI_BIAS_F16)
-      SR_DEEP_CASE(EPI_BIAS_GELU_F16)
-      SR_DEEP_CASE(EPI_BIAS_RES_F32)
-      SR_DEEP_CASE(EPI_BIAS_RES_F16)
-      SR_DEEP_CASE(EPI_BIAS_TANH_F32)
-      default: SR_CHECK(false, "gemm: unknown epilogue");
-    }
-#undef SR_DEEP_CASE
   } else if (v == GEMM_DIAG_NOLOAD || v == GEMM_DIAG_NOEPI) {
     const dim3 grid((unsigned)big_tiles), block(512);
     if (v == GEMM_DIAG_NOLOAD)
       hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, false, 1>), grid, block, 0, stream, X, lda,
-                         W, bias, R, ldr, Y, ldy, M, N, K);
+                         W, bias, R, ldr, Y, ldy, M, N, K, lfv);
     else
       hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, false, 2>), grid, block, 0, stream, X, lda,
-                         W, bias, R, ldr, Y, ldy, M, N, K);
+                         W, bias, R, ldr, Y, ldy, M, N, K, lfv);
   } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
     const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK;
     // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)
@@ -805,10 +788,10 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   case E:                                                                                        \
     if (persist)                                                                                 \
       hipLaunchKernelGGL((gemm_pipe_kernel<E, true>), grid, block, 0, stream, X, lda, W, bias, R, \
-                         ldr, Y, ldy, M, N, K);                                                  \
+                         ldr, Y, ldy, M, N, K, lfv);                                             \
     else                                                                                         \
       hipLaunchKernelGGL((gemm_pipe_kernel<E, false>), grid, block, 0, stream, X, lda, W, bias, R,\
-                         ldr, Y, ldy, M, N, K);                                                  \
+                         ldr, Y, ldy, M, N, K, lfv);                                             \
     break;
     switch (epi) {
       SR_PIPE_CASE(EPI_BIAS_F16)
@@ -816,14 +799,13 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
       SR_PIPE_CASE(EPI_BIAS_RES_F32)
       SR_PIPE_CASE(EPI_BIAS_RES_F16)
       SR_PIPE_CASE(EPI_BIAS_TANH_F32)
+      SR_PIPE_CASE(EPI_LNF_F16)
+      SR_PIPE_CASE(EPI_LNF_GELU_F16)
+      SR_PIPE_CASE(EPI_RES16_STATS)
+      SR_PIPE_CASE(EPI_LNR16_STATS)
       default: SR_CHECK(false, "gemm: unknown epilogue");
     }
 #undef SR_PIPE_CASE
-  } else if (v == GEMM_BIG_PERSIST) {
-    // one 8-wave workgroup per CU (128 KiB LDS): 32 per XCD
-    const int64_t per_xcd = std::min<int64_t>(32, ceil_div(big_tiles, 8));
-    launch_tile<256, 256, 2, 4, true>(epi, dim3((unsigned)(8 * per_xcd)), stream, X, lda, W, bias,
-                                      R, ldr, Y, ldy, M, N, K);
   } else {
     const int64_t tiles = (int64_t)(N / 128) * ceil_div(M, 128);
     SR_CHECK(tiles < (1ll << 31), "gemm: too many tiles");

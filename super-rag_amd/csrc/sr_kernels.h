@@ -10,18 +10,38 @@ enum Epilogue {
   EPI_BIAS_GELU_F16 = 1,  // y = gelu_erf(acc + b)       -> fp16
   EPI_BIAS_RES_F32 = 2,   // y = acc + b + R (fp32)      -> fp32
   EPI_BIAS_TANH_F32 = 3,  // y = tanh(acc + b)           -> fp32 (classifier head)
-  EPI_BIAS_RES_F16 = 4    // y = acc + b + R (fp16)      -> fp16
+  EPI_BIAS_RES_F16 = 4,   // y = acc + b + R (fp16)      -> fp16
+  // LayerNorm folded into the GEMMs around it (fp16 residual stream; pipelined 256x256 kernels,
+  // N % 256 == 0).  The A operand / residual is the UN-normalised row u with LN(u) =
+  // (u - mu) * rstd * gamma + beta; mu / rstd come from per-row partial statistics written by the
+  // producing GEMM's epilogue (LnFold below).
+  EPI_LNF_F16 = 5,        // y = rstd * (acc - mu * c[n]) + b'[n], W' = W . diag(gamma) -> fp16
+  EPI_LNF_GELU_F16 = 6,   // y = gelu(same)                                              -> fp16
+  EPI_RES16_STATS = 7,    // y = acc + b + R (fp16, already normalised) -> fp16 + row statistics
+  EPI_LNR16_STATS = 8     // y = acc + b + LN(R) (R un-normalised)      -> fp16 + row statistics
+};
+
+// Per-row statistics hand-over between GEMMs (Chan-combinable partials over 128-column spans):
+// stat[row][part] = (sum, M2 = sum (x - sum/128)^2) of the fp16-rounded outputs in that span.
+// launch_ln_stats_finalize turns them into mr[row] = (mu, rstd), which the folded epilogues read.
+struct LnFold {
+  const float* mr = nullptr;       // (mu, rstd) of the A rows (LNF) / residual rows (LNR)
+  int64_t stat_ld = 1;             // row r of the operand reads mr row r * stat_ld
+  const float* colsum = nullptr;   // LNF: c[n] = sum_k W'[n][k] (fp32 sum of the fp16 W')
+  const float* gamma = nullptr;    // LNR: LayerNorm weight of the residual rows (its beta is
+                                   //      pre-added to the GEMM bias)
+  float* stat_out = nullptr;       // *_STATS: [M][N / 128] partials of the output rows
 };
 
 // k_gemm.hip — Y = epi(X . W^T + bias (+ R)); K % 64 == 0, N % 128 == 0.
 void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
-                 hipStream_t stream);
-enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_BIG_PERSIST = 2, GEMM_DEEP = 3, GEMM_PIPE = 4, GEMM_PIPE_PERSIST = 5,
+                 hipStream_t stream, const LnFold* lf = nullptr);
+enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_PIPE = 4, GEMM_PIPE_PERSIST = 5,
                    GEMM_DIAG_NOLOAD = 6, GEMM_DIAG_NOEPI = 7 /* timing only */ };
 void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
                          const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
-                         int M, int N, int K, hipStream_t stream);
+                         int M, int N, int K, hipStream_t stream, const LnFold* lf = nullptr);
 void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 
 // k_attention.hip — ctx = MHA(qkv, key padding mask) for the first Sq query rows of each
@@ -47,6 +67,18 @@ void launch_cls_logits(const float* t, const float* w, const float* bias, int P,
 void launch_normalize_rows(const void* x, int dtype, int64_t n, int dim, half_t* out, int ld,
                            hipStream_t s);
 void launch_convert_f32_f16(const float* in, half_t* out, int64_t n, hipStream_t s);
+// LayerNorm folding of a [N][K] fp32 weight behind LN(gamma, beta): w16 = fp16(W . diag(gamma)),
+// colsum[n] = sum_k float(w16[n][k]), bias_out[n] = sum_k W[n][k] beta[k] + bias[n].
+void launch_fold_ln_weight(const float* w32, const float* gamma, const float* beta,
+                           const float* bias, int N, int K, half_t* w16, float* colsum,
+                           float* bias_out, hipStream_t s);
+// mr[r] = (mu, rstd) of row r from its nparts Chan partials (n = 128 each), rstd = 1/sqrt(var+eps).
+void launch_ln_stats_finalize(const float* stat, int nparts, float eps, int M, float* mr,
+                              hipStream_t s);
+// h16 = LayerNorm(u) with (mu, rstd) from mr (no re-reduction).
+void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float* gamma,
+                     const float* beta, int M, int d, half_t* h16, hipStream_t s);
+void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s);
 
 // k_search.hip
 int scan_query_tiles(int B);

@@ -123,10 +123,15 @@ class Encoder {
     void* ptr;
     int64_t numel;
     bool f16;
+    float* master = nullptr;  // fp32 copy kept for LayerNorm folding (QKV / FFN1 weights)
   };
   struct Layer {
     DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, w1, b1, w2, b2, ln2g, ln2b;
+    // LayerNorm folding (fp16 residual stream): fp32 masters and the folded copies
+    DevBuf wqkv32, w132, wqkv_f, cqkv, dqkv, w1_f, c1, d1, bo_f, b2_f;
   };
+  bool fold_enabled() const;
+  void prepare_fold(hipStream_t s);
   void begin(hipStream_t s) { SR_HIP(hipStreamWaitEvent(s, done_, 0)); }
   void end(hipStream_t s) { SR_HIP(hipEventRecord(done_, s)); }
   void register_target(const std::string& name, DevBuf& buf, int64_t numel, bool f16,
@@ -144,6 +149,8 @@ class Encoder {
   std::map<std::string, bool> is_set_;
   // workspace
   DevBuf ids_, mask_, types_, pos_, h16_, h32_, qkv_, ctx_, y32_, ffn_, clst_, hostio_;
+  DevBuf statA_, statB_, mrA_, mrB_;  // per-row LayerNorm partials / (mu, rstd) (folded path)
+  bool fold_ready_ = false;  // folded weights match the current weights
   int64_t ws_tokens_ = 0;
 };
 

@@ -163,3 +163,38 @@ def test_bge_reranker_shape_fp16_residual_ranking():
     top_g = np.argsort(-got, kind="stable")[:10][None]
     top_r = np.argsort(-ref, kind="stable")[:10][None]
     assert same_topk_modulo_ties(top_g, got[top_g], top_r, ref[top_r], 2 * tol)
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("S", [16, 50, 130])
+def test_ln_folded_cross_encoder(fold, S, monkeypatch):
+    # fp16 residual stream with d % 256 == 0: the LayerNorms are folded into the GEMMs (per-row
+    # Chan statistics from the residual epilogues, gamma folded into W, LN rebuilt in the residual
+    # epilogue); SR_LN_FOLD=0 is the materialised-LayerNorm path.  Both match the fp32 oracle.
+    from super_rag_amd.encoder import Encoder, random_weights
+    monkeypatch.setenv("SR_LN_FOLD", fold)
+    spec = _tiny("xlmr", d=256, H=4, F=512, L=3, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=31, style="test")
+    for k in list(w):  # non-trivial LayerNorm affine parameters exercise the folding
+        if k.endswith("LayerNorm.weight"):
+            w[k] = (1.0 + 0.3 * np.random.default_rng(len(k)).standard_normal(w[k].shape)).astype(np.float32)
+        elif k.endswith("LayerNorm.bias"):
+            w[k] = (0.2 * np.random.default_rng(len(k) + 1).standard_normal(w[k].shape)).astype(np.float32)
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 33, S, seed=S)
+    got = enc.cross_score(ids, mask)
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)
+    tol = 4e-3 * (1.0 + np.abs(ref).max())
+    assert np.abs(got - ref).max() <= tol
+
+
+@pytest.mark.parametrize("pool", ["cls", "mean"])
+def test_ln_folded_embedder(pool):
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("bert", d=256, H=4, F=512, L=2, res16=True)
+    w = random_weights(spec, seed=41, style="test")
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 24, 40, seed=5)
+    got = enc.embed(ids, mask, pool=pool)
+    ref = R.embed(_ref_cfg(spec), w, ids, mask, pool=pool)
+    assert _rel(got, ref).max() <= 4e-3
