@@ -31,6 +31,12 @@ namespace {
 
 constexpr int GBK = 64;  // k per stage
 
+// s_waitcnt through the builtin (the compiler's own waitcnt pass then knows the counters are
+// satisfied; an asm waitcnt is invisible to it and it re-waits conservatively). gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
+#define SR_WAITCNT(vm, lgkm) \
+  __builtin_amdgcn_s_waitcnt(((vm) & 15) | (7 << 4) | (((lgkm) & 15) << 8) | (((vm) >> 4) << 14))
+
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 // Issue NI glds wave-instructions of one tile: instruction i of this wave fills LDS rows
@@ -405,6 +411,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   if (t >= t_end || t_step <= 0) return;
   int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
 
+
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wm = wave & 3;
@@ -429,9 +436,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   stage(0, lds, m0, n0);
   if (nk > 1) {
     stage(1, lds + STAGE, m0, n0);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    SR_WAITCNT(8, 15);
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SR_WAITCNT(0, 15);
   }
   __builtin_amdgcn_s_barrier();
   bool stores_pending = false;  // 32 unchecked epilogue stores of the previous tile in flight
@@ -478,11 +485,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
     if (lenient) {
       if constexpr (PipeEpi<EPI>::NSTORE == 16)
-        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+        SR_WAITCNT(16, 0);
       else
-        asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+        SR_WAITCNT(32, 0);
     } else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (SN == 1 && DIAG != 1) stage(kt + 2, cur, m0, n0);
@@ -564,11 +571,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     if (!more) break;
     // next tile: K-step 0 landed (younger: K-step 1's 8 glds + 32 stores when unchecked)
     if (!full)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      SR_WAITCNT(8, 15);
     else if constexpr (PipeEpi<EPI>::NSTORE == 16)
-      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      SR_WAITCNT(24, 15);
     else
-      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+      SR_WAITCNT(40, 15);
     __builtin_amdgcn_s_barrier();
     stores_pending = full;
     t = t_next;
@@ -580,6 +587,161 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 // PERSIST: a grid of 8 * G blocks walks the tiles; XCD group x = blockIdx & 7 owns a contiguous
 // tile range (X panels stay in that XCD's L2) and the next tile's first K-step is staged by
 // LDS-DMA while the current tile's epilogue runs, hiding the per-tile load latency.
+// ---- "pp" variant: 4-wave workgroups, 256 (n) x 128 (m) tile, K-step 32, 3-slot LDS ring ----------
+// 72 KiB of LDS and <= 256 VGPRs, so TWO workgroups share a CU: one's epilogue (bias / GELU /
+// LayerNorm VALU work and the output stores) runs beside the other's MFMA main loop instead of
+// idling the matrix pipe (the 256 x 256 single-workgroup kernels stall on every epilogue).
+// Per wave 128 x 64 outputs as before.  K-step kt: p0 = A[0..3] x B while A[4..7] is read;
+// vmcnt (step kt+1 landed; kt+2 stays in flight) + raw s_barrier; the glds of kt+3 go into the
+// slot just consumed; p1 = A[4..7] x B while kt+1's A[0..3] / B are read.  Rows are 64 B: 16-byte
+// chunk c of row r lives at c ^ ((r >> 2) & 2) (conflict-free ds_read_b128, simulated).
+__device__ __forceinline__ int swz_pp(int r, int c) { return c ^ ((r >> 2) & 2); }
+
+__device__ __forceinline__ half8 read_frag_pp(const half_t* t, int row, int chunk) {
+  return *reinterpret_cast<const half8*>(t + row * 32 + swz_pp(row, chunk) * 8);
+}
+
+template <int NI>
+__device__ __forceinline__ void pp_offsets(uint32_t (&voff)[NI], int64_t ld, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = (wave * NI + i) * 16 + (lane >> 2);
+    voff[i] = (uint32_t)(((int64_t)r * ld + swz_pp(r, lane & 3) * 8) * 2);
+  }
+}
+
+template <int NI>
+__device__ __forceinline__ void pp_stage(__amdgpu_buffer_rsrc_t rs, const uint32_t (&voff)[NI],
+                                         int soff, half_t* lds_tile, int wave) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (see stage_buf)
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, SR_LDS(lds_tile + (wave * NI + i) * 16 * 32), 16,
+                                             voff[i], soff, 0, 0);
+#endif
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_pp_kernel(
+    const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
+    const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
+    void* __restrict__ Y, int64_t ldy, int M, int N, int K, const LnFold lf) {
+  constexpr int BN = 256, BM = 128, KS = 32, NSLOT = 3;
+  constexpr int SLOT = (BN + BM) * KS;  // halfs (24 KiB)
+  constexpr int GW = 6;                 // glds per wave per K-step (4 W + 2 X)
+  __shared__ __attribute__((aligned(16))) half_t lds[NSLOT * SLOT];
+
+  const int tiles_n = N / BN;
+  const int nwg = tiles_n * ((M + BM - 1) / BM);
+  const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (blockIdx.x >> 3);
+  const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 1, wm = wave & 1;
+  const int nk = K / KS;
+
+  const int arow = wn * 128 + (lane & 15), brow = wm * 64 + (lane & 15), ch = lane >> 4;
+
+  uint32_t vw[4], vx[2];
+  pp_offsets<4>(vw, K, wave, lane);
+  pp_offsets<2>(vx, lda, wave, lane);
+  const __amdgpu_buffer_rsrc_t rw = panel_rsrc(W + (int64_t)n0 * K, (int64_t)BN * K * 2);
+  const __amdgpu_buffer_rsrc_t rx =
+      panel_rsrc(X + (int64_t)m0 * lda, (int64_t)(M - m0 < BM ? M - m0 : BM) * lda * 2);
+  auto stage = [&](int kt) {
+    half_t* sl = lds + (kt % NSLOT) * SLOT;
+    pp_stage<4>(rw, vw, kt * KS * 2, sl, wave);
+    pp_stage<2>(rx, vx, kt * KS * 2, sl + BN * KS, wave);
+  };
+
+  float4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+  half8 aX[4], aY[4], bX[4], bY[4];
+
+  stage(0);
+  if (nk > 1) stage(1);
+  if (nk > 2) stage(2);
+  if (nk > 2)
+    SR_WAITCNT(12, 15);
+  else if (nk > 1)
+    SR_WAITCNT(6, 15);
+  else
+    SR_WAITCNT(0, 15);
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) aY[i] = read_frag_pp(lds, arow + 16 * i, ch);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bX[j] = read_frag_pp(lds + BN * KS, brow + 16 * j, ch);
+
+  // K-step with fragments (a0 = A[0..3], b) in registers; reads the next step's into (a0n, bn)
+  auto kstep = [&](int kt, half8 (&a0)[4], half8 (&b)[4], half8 (&a0n)[4], half8 (&bn)[4],
+                   const bool st, const bool rd) __attribute__((always_inline)) {
+    const half_t* cur = lds + (kt % NSLOT) * SLOT;
+    const half_t* nxt = lds + ((kt + 1) % NSLOT) * SLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aX[i] = read_frag_pp(cur, arow + 16 * (4 + i), ch);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b[j], acc[i][j], 0, 0, 0);
+    SR_INTERLEAVE(4);
+    if (kt + 2 < nk)
+      SR_WAITCNT(6, 0);
+    else
+      SR_WAITCNT(0, 0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (st) stage(kt + 3);
+    if (rd) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a0n[i] = read_frag_pp(nxt, arow + 16 * i, ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bn[j] = read_frag_pp(nxt + BN * KS, brow + 16 * j, ch);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], b[j], acc[4 + i][j], 0, 0, 0);
+    if (st && rd) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // steady state (every step stages kt+3 and reads kt+1: no branches inside), then the tail;
+  // aY is consumed by p0 before p1 re-reads it, the B set alternates bX / bY
+  int kt = 0;
+  for (; kt + 4 < nk; kt += 2) {
+    kstep(kt, aY, bX, aY, bY, true, true);
+    kstep(kt + 1, aY, bY, aY, bX, true, true);
+  }
+  while (kt < nk) {
+    kstep(kt, aY, bX, aY, bY, kt + 3 < nk, kt + 1 < nk);
+    if (++kt >= nk) break;
+    kstep(kt, aY, bY, aY, bX, kt + 3 < nk, kt + 1 < nk);
+    ++kt;
+  }
+
+  const int nw0 = n0 + wn * 128, mw0 = m0 + wm * 64;
+  if (m0 + BM <= M)
+    PipeEpi<EPI>::template run<false>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf);
+  else
+    PipeEpi<EPI>::template run<true>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf);
+}
+
 template <int EPI, int BN, int BM, int WN, int WM, bool PERSIST>
 __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) void gemm_f16_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
@@ -726,6 +888,7 @@ static int forced_tile() {
   if (std::strcmp(e, "big") == 0) return GEMM_BIG;
   if (std::strcmp(e, "pipe") == 0) return GEMM_PIPE;
   if (std::strcmp(e, "pipe_persist") == 0) return GEMM_PIPE_PERSIST;
+  if (std::strcmp(e, "pp") == 0) return GEMM_PP;
   return -1;
 }
 
@@ -763,8 +926,9 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   int v = variant >= 0 ? variant : forced_tile();
   if (v < 0) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_SMALL;
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
+  if (v == GEMM_PP && K % 32 != 0) v = GEMM_PIPE;
   if (fold && (v == GEMM_SMALL || v == GEMM_BIG)) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_PIPE;
-  const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) && !out32;
+  const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST || v == GEMM_PP) && !out32;
   SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
   const LnFold lfv = lf ? *lf : LnFold{};
   if (v == GEMM_BIG) {
@@ -778,6 +942,27 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
     else
       hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, false, 2>), grid, block, 0, stream, X, lda,
                          W, bias, R, ldr, Y, ldy, M, N, K, lfv);
+  } else if (v == GEMM_PP) {
+    const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 128);
+    const dim3 grid((unsigned)tiles), block(256);
+#define SR_PP_CASE(E)                                                                            \
+  case E:                                                                                        \
+    hipLaunchKernelGGL((gemm_pp_kernel<E>), grid, block, 0, stream, X, lda, W, bias, R, ldr, Y,  \
+                       ldy, M, N, K, lfv);                                                       \
+    break;
+    switch (epi) {
+      SR_PP_CASE(EPI_BIAS_F16)
+      SR_PP_CASE(EPI_BIAS_GELU_F16)
+      SR_PP_CASE(EPI_BIAS_RES_F32)
+      SR_PP_CASE(EPI_BIAS_RES_F16)
+      SR_PP_CASE(EPI_BIAS_TANH_F32)
+      SR_PP_CASE(EPI_LNF_F16)
+      SR_PP_CASE(EPI_LNF_GELU_F16)
+      SR_PP_CASE(EPI_RES16_STATS)
+      SR_PP_CASE(EPI_LNR16_STATS)
+      default: SR_CHECK(false, "gemm: unknown epilogue");
+    }
+#undef SR_PP_CASE
   } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
     const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK;
     // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)

@@ -38,7 +38,7 @@ void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const f
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream, const LnFold* lf = nullptr);
 enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_PIPE = 4, GEMM_PIPE_PERSIST = 5,
-                   GEMM_DIAG_NOLOAD = 6, GEMM_DIAG_NOEPI = 7 /* timing only */ };
+                   GEMM_DIAG_NOLOAD = 6, GEMM_DIAG_NOEPI = 7 /* timing only */, GEMM_PP = 8 };
 void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
                          const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
                          int M, int N, int K, hipStream_t stream, const LnFold* lf = nullptr);

@@ -11,7 +11,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = {"small": 0, "big": 1, "pipe": 4, "pipe_persist": 5}
+VARIANTS = {"small": 0, "big": 1, "pipe": 4, "pipe_persist": 5, "pp": 8}
 
 
 def _run(variant, epi, M, N, K, seed=0):
