@@ -159,6 +159,8 @@ void Encoder::prepare_fold(hipStream_t s) {
     launch_fold_ln_weight(L.w132.as<float>(), L.ln1g.as<float>(), L.ln1b.as<float>(),
                           L.b1.as<float>(), (int)F, (int)D, L.w1_f.as<half_t>(), L.c1.as<float>(),
                           L.d1.as<float>(), s);
+    L.w2h.reserve((size_t)D * F * sizeof(half_t));  // 0.5 W2: FFN1 stores 2 GELU (exact scale)
+    launch_scale_f16(L.w2.as<half_t>(), 0.5f, L.w2h.as<half_t>(), D * F, s);
     L.b2_f.reserve((size_t)D * sizeof(float));  // FFN2 bias + beta of LN1 (rebuilt residual)
     launch_vec_add(L.b2.as<float>(), L.ln1b.as<float>(), L.b2_f.as<float>(), (int)D, s);
     if (l == 0) continue;  // layer 0 reads the (normalised) embedding LayerNorm output
@@ -304,7 +306,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         l2.mr = mA;
         l2.gamma = L.ln1g.as<float>();
         l2.stat_out = sB;
-        launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo, d,
+        launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2h.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo, d,
                     Mr, d, F, s, &l2);
         launch_ln_stats_finalize(sB, nparts, cfg_.ln_eps, Mr, mB, s);
       }

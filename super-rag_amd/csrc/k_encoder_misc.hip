@@ -323,6 +323,11 @@ __global__ __launch_bounds__(256) void ln_apply_kernel(const half_t* __restrict_
   }
 }
 
+__global__ void scale_f16_kernel(const half_t* in, float scale, half_t* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = (half_t)((float)in[i] * scale);
+}
+
 __global__ void vec_add_kernel(const float* a, const float* b, float* out, int n) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) out[i] = a[i] + b[i];
@@ -432,6 +437,13 @@ void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float*
   ProfScope prof("ln_apply", s, 0.0, (double)M * d * 4.0);
   hipLaunchKernelGGL(ln_apply_kernel<MAXV>, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, u, ldu,
                      mr, gamma, beta, M, d, h16);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_scale_f16(const half_t* in, float scale, half_t* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scale_f16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, in, scale,
+                     out, n);
   SR_LAUNCH_CHECK();
 }
 

@@ -78,6 +78,21 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + copysignf(e, x));
 }
 
+// 2 * GELU(x) = x + |x| erf(|x| / sqrt 2) with the same erf (A&S 7.1.26): no copysign and no final
+// halving (the consumer's weight carries the 0.5, exact in fp16), 4 VALU fewer per element than
+// gelu_erf.  Used by the LayerNorm-folded FFN1 epilogue (EPI_LNF_GELU_F16).
+__device__ __forceinline__ float gelu2_erf(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float w = __builtin_amdgcn_exp2f(x * (x * -0.72134752044448170f));  // exp(-x^2 / 2)
+  return fmaf(ax, fmaf(-p, w, 1.0f), x);
+}
+
 // Epilogue: lane owns D[n = nw0 + 16i + 4(lane>>4) + r][m = mw0 + 16j + (lane&15)] of the wave's
 // FN x FM 16x16 tiles; bias (+ residual) (+ activation), one 8/16-byte store per tile.
 template <int EPI, int FN, int FM>
@@ -201,8 +216,9 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   constexpr bool RESN = EPI == EPI_BIAS_RES_F16 || EPI == EPI_RES16_STATS;
   constexpr bool LNR = EPI == EPI_LNR16_STATS;
   constexpr bool STATS = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS;
-  constexpr bool GELU = EPI == EPI_BIAS_GELU_F16 || EPI == EPI_LNF_GELU_F16;
-  static_assert(EPI == EPI_BIAS_F16 || GELU || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
+  constexpr bool GELU = EPI == EPI_BIAS_GELU_F16;
+  constexpr bool GELU2 = EPI == EPI_LNF_GELU_F16;  // stores 2 * GELU (consumer weight halved)
+  static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
   float4v b0[4], b1[4];
@@ -283,6 +299,10 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       if constexpr (GELU) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
+      }
+      if constexpr (GELU2) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = gelu2_erf(v[r]);
       }
 #pragma unroll
       for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
@@ -554,7 +574,45 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       kstep(kt, 0, false, lenient, 0, 0, false);
 
     const bool full = m0 + BM <= M;
-    if constexpr (DIAG == 2) {
+    if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
+      const int g = lane >> 4, odd = g & 1;
+      const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          half8 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                             __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+            h[r] = (half_t)__uint_as_float(sw[0]);
+            h[4 + r] = (half_t)__uint_as_float(sw[1]);
+          }
+          if (m < M) *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nl + 32 * p) = h;
+        }
+      }
+    } else if constexpr (DIAG == 3) {  // epilogue math (bias + GELU, wide layout), no stores
+      const int g = lane >> 4, odd = g & 1;
+      const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
+      float sacc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const float4v b0 = *reinterpret_cast<const float4v*>(bias + nl + 32 * p);
+          const float4v b1 = *reinterpret_cast<const float4v*>(bias + nl + 32 * p + 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                             __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+            sacc += (float)(half_t)gelu_erf(__uint_as_float(sw[0]) + b0[r]);
+            sacc += (float)(half_t)gelu_erf(__uint_as_float(sw[1]) + b1[r]);
+          }
+        }
+      if (sacc == 12345.678f) reinterpret_cast<float*>(Y)[tid] = sacc;
+    } else if constexpr (DIAG == 2) {
       float sacc = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -934,6 +992,18 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
                                        ldr, Y, ldy, M, N, K);
+  } else if (v >= GEMM_DIAG_P_NOEPI && v <= GEMM_DIAG_P_STOREONLY) {
+    const int64_t g = 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8));
+    const dim3 grid((unsigned)g), block(512);
+    if (v == GEMM_DIAG_P_NOEPI)
+      hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, true, 2>), grid, block, 0, stream, X, lda,
+                         W, bias, R, ldr, Y, ldy, M, N, K, lfv);
+    else if (v == GEMM_DIAG_P_MATHONLY)
+      hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, true, 3>), grid, block, 0, stream, X, lda,
+                         W, bias, R, ldr, Y, ldy, M, N, K, lfv);
+    else
+      hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, true, 4>), grid, block, 0, stream, X, lda,
+                         W, bias, R, ldr, Y, ldy, M, N, K, lfv);
   } else if (v == GEMM_DIAG_NOLOAD || v == GEMM_DIAG_NOEPI) {
     const dim3 grid((unsigned)big_tiles), block(512);
     if (v == GEMM_DIAG_NOLOAD)

@@ -16,7 +16,7 @@ enum Epilogue {
   // (u - mu) * rstd * gamma + beta; mu / rstd come from per-row partial statistics written by the
   // producing GEMM's epilogue (LnFold below).
   EPI_LNF_F16 = 5,        // y = rstd * (acc - mu * c[n]) + b'[n], W' = W . diag(gamma) -> fp16
-  EPI_LNF_GELU_F16 = 6,   // y = gelu(same)                                              -> fp16
+  EPI_LNF_GELU_F16 = 6,   // y = 2 gelu(same) (the FFN2 weight carries the 0.5)          -> fp16
   EPI_RES16_STATS = 7,    // y = acc + b + R (fp16, already normalised) -> fp16 + row statistics
   EPI_LNR16_STATS = 8     // y = acc + b + LN(R) (R un-normalised)      -> fp16 + row statistics
 };
@@ -38,7 +38,8 @@ void launch_gemm(int epi, const half_t* X, int64_t lda, const half_t* W, const f
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream, const LnFold* lf = nullptr);
 enum GemmVariant { GEMM_SMALL = 0, GEMM_BIG = 1, GEMM_PIPE = 4, GEMM_PIPE_PERSIST = 5,
-                   GEMM_DIAG_NOLOAD = 6, GEMM_DIAG_NOEPI = 7 /* timing only */, GEMM_PP = 8 };
+                   GEMM_DIAG_NOLOAD = 6, GEMM_DIAG_NOEPI = 7 /* timing only */, GEMM_PP = 8,
+                   GEMM_DIAG_P_NOEPI = 9, GEMM_DIAG_P_MATHONLY = 10, GEMM_DIAG_P_STOREONLY = 11 };
 void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, const half_t* W,
                          const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
                          int M, int N, int K, hipStream_t stream, const LnFold* lf = nullptr);
@@ -79,6 +80,7 @@ void launch_ln_stats_finalize(const float* stat, int nparts, float eps, int M, f
 void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float* gamma,
                      const float* beta, int M, int d, half_t* h16, hipStream_t s);
 void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s);
+void launch_scale_f16(const half_t* in, float scale, half_t* out, int64_t n, hipStream_t s);
 
 // k_search.hip
 int scan_query_tiles(int B);

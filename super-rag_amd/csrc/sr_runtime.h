@@ -128,7 +128,7 @@ class Encoder {
   struct Layer {
     DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, w1, b1, w2, b2, ln2g, ln2b;
     // LayerNorm folding (fp16 residual stream): fp32 masters and the folded copies
-    DevBuf wqkv32, w132, wqkv_f, cqkv, dqkv, w1_f, c1, d1, bo_f, b2_f;
+    DevBuf wqkv32, w132, wqkv_f, cqkv, dqkv, w1_f, c1, d1, bo_f, b2_f, w2h;
   };
   bool fold_enabled() const;
   void prepare_fold(hipStream_t s);

@@ -78,7 +78,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in a.variants.split(",")]
-    all_ok = all(parity(v, dev) for v in variants if v >= 0 and v not in (6, 7))
+    all_ok = all(parity(v, dev) for v in variants if v >= 0 and v not in (6, 7, 9, 10, 11))
     M = a.M
     shapes = [("qkv", 2304, 768, 0), ("ffn1_gelu", 3072, 768, 1), ("ffn2_res16", 768, 3072, 4),
               ("oproj_res16", 768, 768, 4), ("ffn2_res32", 768, 3072, 2)]

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round profile on the GPU box (run from the repo root via gpurun):
+#   1. kernel-trace + stats of the default bench command
+#   2. FETCH_SIZE and WRITE_SIZE in separate PMC passes (MI355X_MICROARCH.md: one TCC counter
+#      group per pass) over a 1-step bench
+# Outputs under gpurun_out/prof_<tag>/.
+set -e
+TAG=${1:-r01}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
+  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_trace.log 2>&1
+timeout -k 10 600 rocprofv3 -i tools/pmc_fetch.txt -d $OUT/fetch -o run --output-format csv -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_fetch.log 2>&1
+timeout -k 10 600 rocprofv3 -i tools/pmc_write.txt -d $OUT/write -o run --output-format csv -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_write.log 2>&1
