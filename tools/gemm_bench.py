@@ -69,6 +69,27 @@ def parity(variant, dev):
     return ok
 
 
+def parity_big(variant, dev):
+    """Multi-tile persistent shapes (every walker hands over several tiles), epilogues 0/1/4."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    ok = True
+    for (M, Nn, K) in ((70000, 768, 768), (40000, 2304, 768), (20000, 768, 3072)):
+        X = (torch.randn(M, K, device=dev, generator=g) * 0.5).half()
+        W = (torch.randn(Nn, K, device=dev, generator=g) * 0.02).half()
+        b = torch.randn(Nn, device=dev, generator=g) * 0.1
+        for epi in (0, 1, 4):
+            R = torch.randn(M, Nn, device=dev, generator=g).half() if epi == 4 else None
+            Y = torch.full((M, Nn), float("nan"), device=dev, dtype=torch.float16)
+            gemm(variant, epi, X, W, b, R, Y)
+            ref = reference(epi, X, W, b, R)
+            err = (Y.float() - ref).abs().max().item()
+            tol = 2e-3 * max(1.0, ref.abs().max().item())
+            ok = ok and err <= tol
+            print(f"  parity-big v{variant} epi{epi} {M}x{Nn}x{K}: max|err| {err:.2e} (tol {tol:.1e})"
+                  f"{'' if err <= tol else '  FAIL'}")
+    return ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="1,2")
@@ -79,6 +100,7 @@ def main():
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in a.variants.split(",")]
     all_ok = all(parity(v, dev) for v in variants if v >= 0 and v not in (6, 7, 9, 10, 11))
+    all_ok = all_ok and all(parity_big(v, dev) for v in variants if v in (4, 5))
     M = a.M
     shapes = [("qkv", 2304, 768, 0), ("ffn1_gelu", 3072, 768, 1), ("ffn2_res16", 768, 3072, 4),
               ("oproj_res16", 768, 768, 4), ("ffn2_res32", 768, 3072, 2)]
