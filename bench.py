@@ -193,7 +193,9 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None}
     roof.update({"kernel": dom_name, "launches": dom["launches"], "avg_ms": round(avg_ms, 4),
                  "per_launch": (f"{dom['flops'] / dom['launches']:.4g} FLOP" if roof["bound"] == "mfma"
-                                else f"{dom['bytes'] / dom['launches']:.4g} B")})
+                                else f"{dom['bytes'] / dom['launches']:.4g} B"),
+                 "algorithmic_B_per_launch": round(dom["bytes"] / dom["launches"])})
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(dom_name)
     step_ms = dt / a.steps * 1e3
     kern = {k: {"ms_per_step": round(v["total_ms"] / a.steps, 3), "launches": v["launches"],
                 ("tflops" if v["flops"] > 0 else "gbs"):
@@ -206,6 +208,7 @@ def main():
         search_roof = {"bound": "hbm", "achieved": round(sb / (sm * 1e-3) / 1e9, 1),
                        "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+        search_roof["traffic"], search_roof["traffic_source"] = pmc_traffic("cosine_scan")
     else:
         search_roof = None
 
@@ -236,6 +239,23 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes over this same bench command, gfx950 fetch correction applied).
+    Counters cannot be read live inside the timed region, so the value is the profiled run's."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        k = json.load(f)["kernels"].get(kernel)
+    if not k:
+        return None, None
+    return k["traffic_B"], (f"{os.path.relpath(files[-1], ROOT)}: fetch {k['fetch_B']} B + write "
+                            f"{k['write_B']} B per launch (mean over {k['launches']} launches)")
 
 
 def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total):

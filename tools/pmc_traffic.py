@@ -1,0 +1,78 @@
+"""Per-kernel HBM traffic from rocprofv3 PMC passes (diagnostic tool, runs here on the merged
+gpurun_out/ files; not part of the product).
+
+    python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles/<round>_pmc_traffic.json
+
+Reads the FETCH_SIZE pass (fetch/pmc_1/run_counter_collection.csv) and the WRITE_SIZE pass
+(write/pmc_1/...), each collected in its own run as MI355X_MICROARCH.md §HBM prescribes, and writes
+per logical kernel (the names `sr_profile_*` / bench.py use) the mean bytes per launch:
+  fetch_B = FETCH_SIZE (KiB) x 1024 x 2   (gfx950: FETCH_SIZE counts half the bytes of a wide
+                                           coalesced streaming read — 128-B requests tallied as 64 B)
+  write_B = WRITE_SIZE (KiB) x 1024        (exact for 16-B-per-lane stores)
+Both counters come from the L2 memory-side request counters, so Infinity-Cache hits are included.
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+EPI_NAMES = {0: "gemm_f16_bias", 1: "gemm_f16_bias_gelu", 2: "gemm_f16_bias_residual",
+             3: "gemm_f16_bias_tanh", 4: "gemm_f16_bias_residual16", 5: "gemm_f16_lnfold",
+             6: "gemm_f16_lnfold_gelu", 7: "gemm_f16_residual16_stats",
+             8: "gemm_f16_lnres16_stats"}
+
+
+def logical(name):
+    """Mangled HIP kernel name -> the library's logical kernel name (None for foreign kernels)."""
+    if "_ZN2sr" not in name and not name.startswith("sr::"):
+        return None
+    m = re.search(r"gemm_\w*?kernelILi(\d+)E", name)
+    if m:
+        return EPI_NAMES.get(int(m.group(1)), f"gemm_epi{m.group(1)}")
+    m = re.search(r"\d+([a-z0-9_]+?)_kernel", name) or re.search(r"::(\w+?)_kernel", name)
+    base = m.group(1) if m else name
+    if base.startswith("attention"):
+        return "attention"
+    return base
+
+
+def read(path, counter):
+    tot = defaultdict(float)
+    n = defaultdict(int)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            k = logical(row["Kernel_Name"])
+            if k is None:
+                continue
+            tot[k] += float(row["Counter_Value"])
+            n[k] += 1
+    return tot, n
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    f_tot, f_n = read(f"{src}/fetch/pmc_1/run_counter_collection.csv", "FETCH_SIZE")
+    w_tot, w_n = read(f"{src}/write/pmc_1/run_counter_collection.csv", "WRITE_SIZE")
+    out = {"source": src,
+           "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over "
+                     "`bench.py --steps 1 --warmup 1`; FETCH_SIZE x2 (gfx950 correction), "
+                     "KiB -> bytes; mean per launch",
+           "kernels": {}}
+    for k in sorted(set(f_tot) | set(w_tot)):
+        fb = f_tot.get(k, 0.0) / max(f_n.get(k, 1), 1) * 1024 * 2
+        wb = w_tot.get(k, 0.0) / max(w_n.get(k, 1), 1) * 1024
+        out["kernels"][k] = {"launches": f_n.get(k, 0), "fetch_B": round(fb),
+                             "write_B": round(wb), "traffic_B": round(fb + wb)}
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    for k, v in sorted(out["kernels"].items(),
+                       key=lambda kv: -kv[1]["traffic_B"] * kv[1]["launches"]):
+        print(f"{k:32s} launches {v['launches']:5d}  fetch {v['fetch_B'] / 1e6:10.2f} MB  "
+              f"write {v['write_B'] / 1e6:10.2f} MB  per launch")
+
+
+if __name__ == "__main__":
+    main()
