@@ -24,7 +24,7 @@ class EmbeddingService:
     def __init__(self, embedding_provider: str, embedding_model: str, embedding_service_url: str,
                  embedding_service_api_key: str, embedding_max_chunks_in_batch: int,
                  multimodal: bool = False, caching: bool = True, *, encoder=None, tokenizer=None,
-                 device: Optional[int] = None, device_batch: int = 256):
+                 device: Optional[int] = None, device_batch: int = 256, coalesce: bool = True):
         self.embedding_provider = embedding_provider
         self.model = embedding_model
         self.api_base = embedding_service_url          # accepted for signature parity; unused
@@ -34,6 +34,7 @@ class EmbeddingService:
         self.multimodal = multimodal
         self.caching = caching
         self.device_batch = max(1, int(device_batch))
+        self.coalesce = bool(coalesce)
         if encoder is None:
             from .registry import get_model
             encoder, tokenizer = get_model(embedding_model, device)
@@ -44,17 +45,21 @@ class EmbeddingService:
     def dimension(self) -> int:
         return int(self.encoder.spec.hidden)
 
-    def _embed_clean(self, texts: Sequence[str]) -> np.ndarray:
+    @staticmethod
+    def _embed_with(encoder, tokenizer, device_batch: int, texts: Sequence[str]) -> np.ndarray:
         order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
-        out = np.empty((len(texts), self.dimension), dtype=np.float32)
-        for s in range(0, len(order), self.device_batch):
-            idx = order[s:s + self.device_batch]
+        out = np.empty((len(texts), int(encoder.spec.hidden)), dtype=np.float32)
+        for s in range(0, len(order), device_batch):
+            idx = order[s:s + device_batch]
             try:
-                ids, mask = self.tokenizer.encode_batch([texts[i] for i in idx])
-                out[idx] = self.encoder.embed(ids, mask)
+                ids, mask = tokenizer.encode_batch([texts[i] for i in idx])
+                out[idx] = encoder.embed(ids, mask)
             except Exception as e:  # noqa: BLE001 - a failed device batch, as in :94-99
                 raise BatchProcessingError(batch_size=len(idx), reason=f"device batch failed: {e}") from e
         return out
+
+    def _embed_clean(self, texts: Sequence[str]) -> np.ndarray:
+        return self._embed_with(self.encoder, self.tokenizer, self.device_batch, texts)
 
     def embed_documents(self, contents: List[str]) -> List[List[float]]:
         if not contents:
@@ -79,7 +84,26 @@ class EmbeddingService:
     def embed_query(self, content: str) -> List[float]:
         if not content or not content.strip():
             raise EmptyTextError(1)
-        return self.embed_documents([content])[0]
+        if not self.coalesce:
+            return self.embed_documents([content])[0]
+        # concurrent single-query calls (one per search request, embedding_service.py:114) are
+        # coalesced into one device batch per encoder (coalesce.py); results are per query
+        coal = getattr(self.encoder, "_query_coalescer", None)
+        if coal is None:
+            from .coalesce import Coalescer
+            enc, tok, dev_b = self.encoder, self.tokenizer, self.device_batch
+
+            def run(texts):
+                return list(EmbeddingService._embed_with(enc, tok, dev_b, texts))
+            coal = Coalescer(run, max_batch=self.device_batch)
+            setattr(self.encoder, "_query_coalescer", coal)
+        try:
+            return coal(content.replace("\n", " ")).tolist()
+        except BatchProcessingError:
+            raise
+        except Exception as e:  # noqa: BLE001
+            raise EmbeddingError(f"Embedding API error: {e}",
+                                 {"provider": self.embedding_provider, "model": self.model}) from e
 
     async def aembed_query(self, content: str) -> List[float]:
         return await asyncio.to_thread(self.embed_query, content)

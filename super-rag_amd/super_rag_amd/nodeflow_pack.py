@@ -18,6 +18,7 @@ is used, so the pack can be exercised standalone (tests/test_boundary.py).
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import logging
 import os
@@ -185,9 +186,15 @@ class VectorSearchService:
             ctx = vector_db_context()
             ctx["collection"] = name
             cm = ContextManager(name, embedding_model, VECTOR_DB_TYPE, ctx)
-            vector = embedding_model.embed_query(query)
-            results = cm.query(query, score_threshold=similarity_threshold, topk=top_k,
-                               vector=vector, index_types=["vector"], chat_id=chat_id)
+
+            def embed_and_query():
+                vector = embedding_model.embed_query(query)
+                return cm.query(query, score_threshold=similarity_threshold, topk=top_k,
+                                vector=vector, index_types=["vector"], chat_id=chat_id)
+            # The reference runs these synchronously on the event loop (vector_search.py:76-86);
+            # a worker thread keeps the loop free and lets concurrent requests coalesce into
+            # device batches (coalesce.py).  Same calls, same results.
+            results = await asyncio.to_thread(embed_and_query)
             for item in results:
                 if item.metadata is None:
                     item.metadata = {}

@@ -23,7 +23,8 @@ logger = logging.getLogger(__name__)
 class RerankService:
     def __init__(self, rerank_provider: str, rerank_model: str, rerank_service_url: str,
                  rerank_service_api_key: str, caching: bool = True, *, encoder=None,
-                 tokenizer=None, device: Optional[int] = None, device_batch: int = 1024):
+                 tokenizer=None, device: Optional[int] = None, device_batch: int = 1024,
+                 coalesce: bool = True):
         self.rerank_provider = rerank_provider
         self.model = rerank_model
         self.api_base = rerank_service_url      # accepted for signature parity; unused
@@ -31,6 +32,7 @@ class RerankService:
         self.caching = caching
         self.max_documents = 1000
         self.device_batch = max(1, int(device_batch))
+        self.coalesce = bool(coalesce)
         if encoder is None:
             from .registry import get_model
             encoder, tokenizer = get_model(rerank_model, device)
@@ -38,13 +40,43 @@ class RerankService:
         self.tokenizer = tokenizer
 
     def score(self, query: str, texts: List[str]) -> np.ndarray:
-        """Raw cross-encoder logits, one per text."""
-        out = np.empty(len(texts), dtype=np.float32)
-        with_types = self.encoder.spec.pair_style == 1
-        for s in range(0, len(texts), self.device_batch):
-            ids, mask, tt = self.tokenizer.encode_pairs(query, texts[s:s + self.device_batch])
-            out[s:s + len(ids)] = self.encoder.cross_score(ids, mask, tt if with_types else None)[:, 0]
-        return out
+        """Raw cross-encoder logits, one per text.  Concurrent calls (one per search request)
+        are coalesced into shared device batches per cross-encoder (coalesce.py)."""
+        if not self.coalesce:
+            return self._score_many(self.encoder, self.tokenizer, self.device_batch, [(query, texts)])[0]
+        coal = getattr(self.encoder, "_pair_coalescer", None)
+        if coal is None:
+            from .coalesce import Coalescer
+            enc, tok, dev_b = self.encoder, self.tokenizer, self.device_batch
+            coal = Coalescer(lambda items: RerankService._score_many(enc, tok, dev_b, items),
+                             max_batch=max(1, dev_b // 100))
+            setattr(self.encoder, "_pair_coalescer", coal)
+        return coal((query, list(texts)))
+
+    @staticmethod
+    def _score_many(encoder, tokenizer, device_batch: int, items) -> List[np.ndarray]:
+        """[(query, texts)] -> per item logits; the pairs of all items share device batches
+        (each batch padded to its longest pair; the padding is masked, so logits do not depend on
+        the batch composition)."""
+        with_types = encoder.spec.pair_style == 1
+        enc = [tokenizer.encode_pairs(q, t) for q, t in items]
+        n = [e[0].shape[0] for e in enc]
+        S = max(e[0].shape[1] for e in enc)
+
+        def pad(a, v):
+            return np.pad(a, ((0, 0), (0, S - a.shape[1])), constant_values=v)
+        ids = np.concatenate([pad(e[0], encoder.spec.pad_id) for e in enc])
+        mask = np.concatenate([pad(e[1], 0) for e in enc])
+        tt = np.concatenate([pad(e[2], 0) for e in enc])
+        out = np.empty(ids.shape[0], dtype=np.float32)
+        for s in range(0, ids.shape[0], device_batch):
+            sl = slice(s, s + device_batch)
+            out[sl] = encoder.cross_score(ids[sl], mask[sl], tt[sl] if with_types else None)[:, 0]
+        res, o = [], 0
+        for k in n:
+            res.append(out[o:o + k])
+            o += k
+        return res
 
     async def async_rerank(self, query: str, results: list) -> list:
         try:

@@ -65,6 +65,7 @@ class _Collection:
         self.texts: List[Optional[str]] = []
         self.metadatas: List[Optional[dict]] = []
         self.lock = threading.RLock()
+        self.coalescer = None   # created on first coalesced search (coalesce.py)
 
     def snapshot(self, directory: str) -> None:
         os.makedirs(directory, exist_ok=True)
@@ -109,6 +110,8 @@ class MI355XVectorStoreConnector:
             raise ValueError(f"unsupported distance '{self.distance}' (only cosine)")
         self.device = int(ctx.get("device", os.environ.get("SUPER_RAG_AMD_DEVICE", 0)))
         self.snapshot_dir = ctx.get("snapshot_dir")
+        self.coalesce = bool(ctx.get("coalesce", True))
+        self.max_batch = int(ctx.get("max_batch", 256))
         self.compact_ratio = float(ctx.get("compact_ratio", 0.5))
         self.store = self
         if self.snapshot_dir and _get(self.collection_name) is None:
@@ -204,13 +207,33 @@ class MI355XVectorStoreConnector:
         c = _get(self.collection_name)
         if c is None or query.top_k is None or query.top_k <= 0:
             return QueryResult(query=query.query, results=[])
-        q = np.asarray(query.embedding, dtype=np.float32)[None]
-        with c.lock:
-            dist, rows = c.store.search(q, int(query.top_k))
-            results = [DocumentWithScore(text=c.texts[r], score=float(d),
-                                         metadata=copy.deepcopy(c.metadatas[r]))
-                       for d, r in zip(dist[0].tolist(), rows[0].tolist()) if r >= 0]
+        q = np.asarray(query.embedding, dtype=np.float32)
+        if self.coalesce:
+            # concurrent single-query searches share one device batch (coalesce.py)
+            if c.coalescer is None:
+                with c.lock:
+                    if c.coalescer is None:
+                        from .coalesce import Coalescer
+                        c.coalescer = Coalescer(lambda items, c=c: self._search_batch(c, items),
+                                                max_batch=self.max_batch)
+            results = c.coalescer((q, int(query.top_k)))
+        else:
+            results = self._search_batch(c, [(q, int(query.top_k))])[0]
         return QueryResult(query=query.query, results=results)
+
+    @staticmethod
+    def _search_batch(c: _Collection, items) -> List[List[DocumentWithScore]]:
+        """[(query vector, top_k)] -> per query [DocumentWithScore] (distance asc, no ids)."""
+        Q = np.stack([np.asarray(q, dtype=np.float32).reshape(-1) for q, _ in items])
+        kmax = max(k for _, k in items)
+        out = []
+        with c.lock:
+            dist, rows = c.store.search(Q, kmax)
+            for i, (_, k) in enumerate(items):
+                out.append([DocumentWithScore(text=c.texts[r], score=float(d),
+                                              metadata=copy.deepcopy(c.metadatas[r]))
+                            for d, r in zip(dist[i, :k].tolist(), rows[i, :k].tolist()) if r >= 0])
+        return out
 
     def get_vectors(self, ids: List[str]) -> np.ndarray:
         """Stored (normalised, fp16-rounded) vectors for uuids (with_vectors=True support)."""

@@ -80,6 +80,7 @@ class _Spec:
     def __init__(self, hidden=8, pair_style=0):
         self.hidden = hidden
         self.pair_style = pair_style
+        self.pad_id = 1
 
 
 class TextTokenizer:
