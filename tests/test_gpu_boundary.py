@@ -154,3 +154,31 @@ def test_concurrent_requests_coalesce_into_device_batches_with_identical_results
     assert enc._query_coalescer.batches < len(queries)
     assert V._collections["gpu_coal"].coalescer.items == len(queries)
     conn.delete_collection()
+
+
+def test_http_seam_on_the_hip_models():
+    # the OpenAI /embeddings + Jina /rerank server in front of real HIP encoders returns what the
+    # drop-in services return (the wire seam adds no numerics)
+    from fastapi.testclient import TestClient
+    from super_rag_amd.embed import EmbeddingService
+    from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
+    from super_rag_amd.rerank import RerankService
+    from super_rag_amd.server import create_app
+    from super_rag_amd.tokenizer import Tokenizer
+
+    es = ModelSpec("t-bert", "bert", 30522, 256, 2, 4, 512, 128, 2, 1e-12, 0)
+    rs = ModelSpec("t-xlmr", "xlmr", 30522, 256, 2, 4, 512, 130, 1, 1e-5, 1, classifier=1,
+                   bos_id=0, eos_id=2, pad_id=1, max_length=128, residual_fp16=True)
+    emb = EmbeddingService("openai", "e", "", "", 10, encoder=Encoder(es, weights=random_weights(es, 9, "test")),
+                           tokenizer=Tokenizer(es))
+    rer = RerankService("jina_ai", "r", "", "", encoder=Encoder(rs, weights=random_weights(rs, 10, "test")),
+                        tokenizer=Tokenizer(rs))
+    client = TestClient(create_app(lambda m: emb, lambda m: rer))
+    texts = _texts(20, 11)
+    body = client.post("/v1/embeddings", json={"model": "BAAI/bge-m3", "input": texts}).json()
+    np.testing.assert_allclose([d["embedding"] for d in body["data"]], emb.embed_documents(texts), atol=1e-6)
+    q = "w3 w9 w27"
+    res = client.post("/v1/rerank", json={"model": "BAAI/bge-reranker-v2-m3", "query": q,
+                                          "documents": texts}).json()["results"]
+    lg = rer.score(q, texts)
+    assert [r["index"] for r in res] == sorted(range(len(texts)), key=lambda i: (-lg[i], i))
