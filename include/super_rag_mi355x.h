@@ -90,6 +90,13 @@ int sr_store_get(sr_store* s, const int64_t* rows, int64_t n, float* out);
  * q: B x dim host fp32 (normalised internally).  out_dist / out_rows: B x k host buffers, each
  * query's results sorted by (dist asc, row asc).  Blocking. */
 int sr_store_search(sr_store* s, const float* q, int B, int k, float* out_dist, int64_t* out_rows);
+/* Filtered search (the score_threshold / filter kwargs the reference passes and SeekDB's
+ * connector ignores, context/context.py:37-47, :74-111): only rows with
+ * allow[row] != 0 (host, n_rows bytes) compete, so a query still gets its k best ELIGIBLE rows.
+ * The eligibility mask (allow & live) is kept on the device and reused while mask_key (non-zero)
+ * and the store contents are unchanged; mask_key 0 uploads it every call. */
+int sr_store_search_masked(sr_store* s, const float* q, int B, int k, const uint8_t* allow,
+                           int64_t mask_key, float* out_dist, int64_t* out_rows);
 /* Device variant: q is B x dim on the device (SR_DTYPE_F32 or SR_DTYPE_F16), out_sim/out_rows
  * device buffers of B x k (similarity = 1 - dist, rows int64; -1 / -inf when missing).
  * row_offset is added to every returned row (global row id of a shard).  Synchronises `stream`

@@ -215,6 +215,16 @@ int sr_store_search(sr_store* s, const float* q, int B, int k, float* out_dist, 
   SR_API_END
 }
 
+int sr_store_search_masked(sr_store* s, const float* q, int B, int k, const uint8_t* allow,
+                           int64_t mask_key, float* out_dist, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  SR_NONNULL(allow);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->search_host(q, B, k, out_dist, out_rows, allow, mask_key);
+  SR_API_END
+}
+
 int sr_store_search_dev(sr_store* s, const void* q, int q_dtype, int B, int k, float* out_sim,
                         int64_t* out_rows, int64_t row_offset, void* stream) {
   SR_API_BEGIN

@@ -66,9 +66,11 @@ class Store {
   int64_t add_dev(const void* vecs, int dtype, int64_t n, hipStream_t s);
   void remove(const int64_t* rows, int64_t n);
   void get(const int64_t* rows, int64_t n, float* out);
-  void search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows);
+  // allow: optional host eligibility mask (n_rows bytes), cached on the device per mask_key
+  void search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows,
+                   const uint8_t* allow = nullptr, int64_t mask_key = 0);
   void search_dev(const void* q, int q_dtype, int B, int k, float* out_sim, int64_t* out_rows,
-                  int64_t row_offset, hipStream_t s);
+                  int64_t row_offset, hipStream_t s, const uint8_t* elig = nullptr);
   void save(const char* path);
   static Store* load(const char* path, int device);
   void compact(int64_t* old_to_new);
@@ -86,7 +88,7 @@ class Store {
   void ensure_query_ws(int B);
   // Runs the chunked scan/select schedule for one block of <= 256 normalised queries.
   void search_block(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
-                    int64_t row_offset, hipStream_t s, bool safe);
+                    int64_t row_offset, hipStream_t s, bool safe, const uint8_t* live);
 
   int dim_, ld_, device_;
   int64_t n_rows_ = 0, n_live_ = 0, capacity_ = 0;
@@ -97,6 +99,9 @@ class Store {
   // search workspace
   DevBuf qbuf_, qstage_, cand_, cnt_, tau_, overflow_, osim_, orows_, scratch_;
   int ws_queries_ = 0;
+  // filtered search: device eligibility mask (live & allow) and what it was built from
+  DevBuf mask_;
+  int64_t version_ = 0, mask_key_ = 0, mask_version_ = -1, mask_rows_ = -1;
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -119,6 +119,7 @@ int64_t Store::add_dev(const void* vecs, int dtype, int64_t n, hipStream_t s) {
   std::fill(live_host_.begin() + first, live_host_.begin() + first + n, 1);
   n_rows_ += n;
   n_live_ += n;
+  ++version_;
   return first;
 }
 
@@ -143,6 +144,7 @@ void Store::remove(const int64_t* rows, int64_t n) {
       --n_live_;
     }
   }
+  ++version_;
 }
 
 void Store::get(const int64_t* rows, int64_t n, float* out) {
@@ -180,13 +182,12 @@ void Store::ensure_query_ws(int B) {
 }
 
 void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
-                         int64_t row_offset, hipStream_t s, bool safe) {
+                         int64_t row_offset, hipStream_t s, bool safe, const uint8_t* live) {
   const int cap = select_capacity();
   uint64_t* cand = cand_.as<uint64_t>();
   int* cnt = cnt_.as<int>();
   float* tau = tau_.as<float>();
   int* ovf = overflow_.as<int>();
-  const uint8_t* live = live_.as<uint8_t>();
   const half_t* C = corpus_.as<half_t>();
   const int64_t n = n_rows_;
   if (n == 0) {
@@ -210,7 +211,9 @@ void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t
 }
 
 void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
-                       int64_t* out_rows, int64_t row_offset, hipStream_t s) {
+                       int64_t* out_rows, int64_t row_offset, hipStream_t s, const uint8_t* elig) {
+  // elig: per-row eligibility (device, n_rows bytes; live & filter), or null for the live flags
+  const uint8_t* live = elig ? elig : live_.as<uint8_t>();
   SR_CHECK(B >= 0, "store.search: negative batch");
   SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "store.search: top_k must be in [1, 1024]");
   SR_CHECK(k <= select_capacity() / 4, "store.search: top_k too large");
@@ -225,7 +228,7 @@ void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
   for (int b0 = 0; b0 < B; b0 += kQueryBlock) {
     const int bb = std::min(kQueryBlock, B - b0);
     search_block(qn + (int64_t)b0 * ld_, bb, k, out_sim + (int64_t)b0 * k,
-                 out_rows + (int64_t)b0 * k, row_offset, s, false);
+                 out_rows + (int64_t)b0 * k, row_offset, s, false, live);
   }
   int ovf = 0;
   SR_HIP(hipMemcpyAsync(&ovf, overflow_.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -236,16 +239,34 @@ void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
     for (int b0 = 0; b0 < B; b0 += kQueryBlock) {
       const int bb = std::min(kQueryBlock, B - b0);
       search_block(qn + (int64_t)b0 * ld_, bb, k, out_sim + (int64_t)b0 * k,
-                   out_rows + (int64_t)b0 * k, row_offset, s, true);
+                   out_rows + (int64_t)b0 * k, row_offset, s, true, live);
     }
     end(s);
   }
 }
 
-void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows) {
+void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows,
+                        const uint8_t* allow, int64_t mask_key) {
   SR_CHECK(B >= 0 && (B == 0 || (q && out_dist && out_rows)), "store.search: null buffer");
   if (B == 0) return;
   DeviceGuard g(device_);
+  const uint8_t* elig = nullptr;
+  if (allow) {
+    // eligibility = live & allow, uploaded once per (mask_key, store version)
+    if (mask_key == 0 || mask_key != mask_key_ || mask_version_ != version_ || mask_rows_ != n_rows_) {
+      std::vector<uint8_t> m((size_t)std::max<int64_t>(n_rows_, 1));
+      for (int64_t r = 0; r < n_rows_; ++r) m[(size_t)r] = (live_host_[(size_t)r] && allow[r]) ? 1 : 0;
+      mask_.reserve(m.size());
+      begin(stream_);
+      SR_HIP(hipMemcpyAsync(mask_.p, m.data(), (size_t)n_rows_, hipMemcpyHostToDevice, stream_));
+      SR_HIP(hipStreamSynchronize(stream_));
+      end(stream_);
+      mask_key_ = mask_key;
+      mask_version_ = version_;
+      mask_rows_ = n_rows_;
+    }
+    elig = mask_.as<uint8_t>();
+  }
   const size_t qb = (size_t)B * dim_ * sizeof(float);
   const size_t ob = (size_t)B * k * (sizeof(float) + sizeof(int64_t));
   qstage_.reserve(qb + ob);
@@ -253,7 +274,7 @@ void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* 
   float* dsim = reinterpret_cast<float*>(qstage_.as<char>() + qb);
   int64_t* drows = reinterpret_cast<int64_t*>(dsim + (size_t)B * k);
   SR_HIP(hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, stream_));
-  search_dev(dq, SR_DTYPE_F32, B, k, dsim, drows, 0, stream_);
+  search_dev(dq, SR_DTYPE_F32, B, k, dsim, drows, 0, stream_, elig);
   SR_HIP(hipMemcpyAsync(out_dist, dsim, (size_t)B * k * sizeof(float), hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipMemcpyAsync(out_rows, drows, (size_t)B * k * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipStreamSynchronize(stream_));
@@ -362,6 +383,7 @@ void Store::compact(int64_t* old_to_new) {
   std::fill(live_host_.begin(), live_host_.begin() + m, 1);
   n_rows_ = m;
   n_live_ = m;
+  ++version_;
 }
 
 }  // namespace sr

@@ -70,6 +70,8 @@ SIGNATURES = {
     "sr_store_dim": (c_int, [c_void_p, P_I32]),
     "sr_store_get": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "sr_store_search": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sr_store_search_masked": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p,
+                                       c_void_p]),
     "sr_store_search_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                     c_int64, c_void_p]),
     "sr_store_save": (c_int, [c_void_p, c_char_p]),

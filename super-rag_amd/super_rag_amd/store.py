@@ -92,8 +92,10 @@ class NativeStore:
         N.call("sr_store_get", self._h, N.ptr(r), r.shape[0], N.ptr(out))
         return out
 
-    def search(self, queries, k: int):
-        """Host path: returns (dist [B,k] fp32, rows [B,k] int64); dist = 1 - cos, ascending."""
+    def search(self, queries, k: int, allow=None, mask_key: int = 0):
+        """Host path: returns (dist [B,k] fp32, rows [B,k] int64); dist = 1 - cos, ascending.
+        ``allow`` (bool/uint8 [n_rows]) restricts the candidates to the allowed rows (the mask is
+        cached on the device while ``mask_key`` != 0 and the store is unchanged)."""
         q = np.ascontiguousarray(np.asarray(queries, dtype=np.float32))
         if q.ndim == 1:
             q = q[None]
@@ -102,7 +104,17 @@ class NativeStore:
         B = q.shape[0]
         dist = np.empty((B, k), dtype=np.float32)
         rows = np.empty((B, k), dtype=np.int64)
-        N.call("sr_store_search", self._h, N.ptr(q), B, int(k), N.ptr(dist), N.ptr(rows))
+        if allow is None:
+            N.call("sr_store_search", self._h, N.ptr(q), B, int(k), N.ptr(dist), N.ptr(rows))
+        else:
+            n, _ = self.count()
+            a = np.ascontiguousarray(np.asarray(allow, dtype=np.uint8))
+            if a.shape != (n,):
+                raise ValueError(f"allow mask must have {n} entries, got {a.shape}")
+            if n == 0:
+                a = np.zeros(1, dtype=np.uint8)
+            N.call("sr_store_search_masked", self._h, N.ptr(q), B, int(k), N.ptr(a), int(mask_key),
+                   N.ptr(dist), N.ptr(rows))
         return dist, rows
 
     def search_dev(self, q, k: int, out_sim=None, out_rows=None, row_offset: int = 0, stream=None):

@@ -66,6 +66,8 @@ class _Collection:
         self.metadatas: List[Optional[dict]] = []
         self.lock = threading.RLock()
         self.coalescer = None   # created on first coalesced search (coalesce.py)
+        self.version = 0        # bumped on every add / delete / compaction
+        self.masks: Dict[str, tuple] = {}   # filter -> (version, mask_key, allow mask)
 
     def snapshot(self, directory: str) -> None:
         os.makedirs(directory, exist_ok=True)
@@ -93,6 +95,7 @@ class _Collection:
 
 _registry_lock = threading.Lock()
 _collections: Dict[str, _Collection] = {}
+_mask_serial = 0   # device-mask cache keys (sr_store_search_masked)
 
 
 def _get(name: str) -> Optional[_Collection]:
@@ -112,6 +115,10 @@ class MI355XVectorStoreConnector:
         self.snapshot_dir = ctx.get("snapshot_dir")
         self.coalesce = bool(ctx.get("coalesce", True))
         self.max_batch = int(ctx.get("max_batch", 256))
+        # opt-in: apply the score_threshold / filter kwargs the reference passes and SeekDB's
+        # connector ignores (seekdb_connector.py:99-100).  Off by default = reference behaviour.
+        self.honor_score_threshold = bool(ctx.get("honor_score_threshold", False))
+        self.honor_filter = bool(ctx.get("honor_filter", False))
         self.compact_ratio = float(ctx.get("compact_ratio", 0.5))
         self.store = self
         if self.snapshot_dir and _get(self.collection_name) is None:
@@ -170,6 +177,7 @@ class MI355XVectorStoreConnector:
                 c.row_of[u] = int(r)
                 c.texts.append(n.text)
                 c.metadatas.append(copy.deepcopy(n.metadata) if n.metadata is not None else None)
+            c.version += 1
             self._persist(c)
         logger.debug("Added %d documents to collection %s", len(ids), self.collection_name)
         return ids
@@ -192,6 +200,7 @@ class MI355XVectorStoreConnector:
                 n_rows, n_live = c.store.count()
                 if n_rows and n_live < (1.0 - self.compact_ratio) * n_rows:
                     self._compact(c)
+                c.version += 1
             self._persist(c)
 
     def _compact(self, c: _Collection) -> None:
@@ -208,6 +217,8 @@ class MI355XVectorStoreConnector:
         if c is None or query.top_k is None or query.top_k <= 0:
             return QueryResult(query=query.query, results=[])
         q = np.asarray(query.embedding, dtype=np.float32)
+        flt = kwargs.get("filter") if self.honor_filter else None
+        thr = kwargs.get("score_threshold") if self.honor_score_threshold else None
         if self.coalesce:
             # concurrent single-query searches share one device batch (coalesce.py)
             if c.coalescer is None:
@@ -216,23 +227,54 @@ class MI355XVectorStoreConnector:
                         from .coalesce import Coalescer
                         c.coalescer = Coalescer(lambda items, c=c: self._search_batch(c, items),
                                                 max_batch=self.max_batch)
-            results = c.coalescer((q, int(query.top_k)))
+            results = c.coalescer((q, int(query.top_k), flt))
         else:
-            results = self._search_batch(c, [(q, int(query.top_k))])[0]
+            results = self._search_batch(c, [(q, int(query.top_k), flt)])[0]
+        if thr is not None:
+            # similarity = 1 - distance >= threshold (results are distance-ascending: a prefix)
+            results = [d for d in results if 1.0 - d.score >= float(thr)]
         return QueryResult(query=query.query, results=results)
 
     @staticmethod
+    def _allow_mask(c: _Collection, flt):
+        """(mask_key, allow[n_rows]) for a filter, cached per collection version."""
+        from .filters import canonical, matches
+        key = canonical(flt)
+        hit = c.masks.get(key)
+        if hit is not None and hit[0] == c.version:
+            return hit[1], hit[2]
+        allow = np.fromiter((u is not None and matches(flt, md)
+                             for u, md in zip(c.ids, c.metadatas)), dtype=np.uint8, count=len(c.ids))
+        global _mask_serial
+        with _registry_lock:
+            _mask_serial += 1
+            mkey = _mask_serial
+        c.masks[key] = (c.version, mkey, allow)
+        return mkey, allow
+
+    @staticmethod
     def _search_batch(c: _Collection, items) -> List[List[DocumentWithScore]]:
-        """[(query vector, top_k)] -> per query [DocumentWithScore] (distance asc, no ids)."""
-        Q = np.stack([np.asarray(q, dtype=np.float32).reshape(-1) for q, _ in items])
-        kmax = max(k for _, k in items)
-        out = []
+        """[(query vector, top_k, filter)] -> per query [DocumentWithScore] (distance asc, no
+        ids).  Queries with the same filter share one device search."""
+        out: List[List[DocumentWithScore]] = [[] for _ in items]
+        groups: Dict[str, list] = {}
+        for i, (_, _, flt) in enumerate(items):
+            groups.setdefault("" if flt is None else json.dumps(flt, sort_keys=True, default=str),
+                              []).append(i)
         with c.lock:
-            dist, rows = c.store.search(Q, kmax)
-            for i, (_, k) in enumerate(items):
-                out.append([DocumentWithScore(text=c.texts[r], score=float(d),
-                                              metadata=copy.deepcopy(c.metadatas[r]))
-                            for d, r in zip(dist[i, :k].tolist(), rows[i, :k].tolist()) if r >= 0])
+            for key, idx in groups.items():
+                Q = np.stack([np.asarray(items[i][0], dtype=np.float32).reshape(-1) for i in idx])
+                kmax = max(items[i][1] for i in idx)
+                if key == "":
+                    dist, rows = c.store.search(Q, kmax)
+                else:
+                    mkey, allow = MI355XVectorStoreConnector._allow_mask(c, items[idx[0]][2])
+                    dist, rows = c.store.search(Q, kmax, allow=allow, mask_key=mkey)
+                for j, i in enumerate(idx):
+                    k = items[i][1]
+                    out[i] = [DocumentWithScore(text=c.texts[r], score=float(d),
+                                                metadata=copy.deepcopy(c.metadatas[r]))
+                              for d, r in zip(dist[j, :k].tolist(), rows[j, :k].tolist()) if r >= 0]
         return out
 
     def get_vectors(self, ids: List[str]) -> np.ndarray:

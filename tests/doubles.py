@@ -62,7 +62,8 @@ class NumpyStore:
             s.rows, s.live = z["rows"], z["live"]
         return s
 
-    def search(self, q, k):
+    def search(self, q, k, allow=None, mask_key=0):
+        live = self.live if allow is None else (self.live & np.asarray(allow, dtype=bool))
         q = np.asarray(q, np.float64)
         qn = q / np.linalg.norm(q, axis=1, keepdims=True)
         rn = self.rows / np.maximum(np.linalg.norm(self.rows, axis=1, keepdims=True), 1e-300)
@@ -70,7 +71,7 @@ class NumpyStore:
         out = np.full((len(q), k), -1, dtype=np.int64)
         for b in range(len(q)):
             d = 1.0 - rn @ qn[b]
-            order = [i for i in np.lexsort((np.arange(len(d)), d)) if self.live[i]][:k]
+            order = [i for i in np.lexsort((np.arange(len(d)), d)) if live[i]][:k]
             dist[b, : len(order)] = d[order]
             out[b, : len(order)] = order
         return dist, out

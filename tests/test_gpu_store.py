@@ -177,3 +177,48 @@ def test_device_path_shards_and_merge():
     torch.cuda.synchronize()
     assert np.array_equal(mr.cpu().numpy(), r_full)
     np.testing.assert_allclose(1.0 - ms.cpu().numpy(), d_full, atol=1e-6)
+
+
+def test_masked_search_k_best_eligible_rows():
+    # sr_store_search_masked: only allow & live rows compete (filters / chat_id of the
+    # reference's ContextManager, honoured behind ctx["honor_filter"]); 60k rows exercise the
+    # dense chunk + threshold chunks; the device mask is reused per key and rebuilt when the
+    # store changes (deletes) or the key changes.
+    dim, n = 128, 60_000
+    x = _clustered(n, dim, seed=21)
+    s = _store(dim)
+    s.add(x)
+    q = _queries(x, 17, seed=22)
+    rng = np.random.default_rng(23)
+    allow = rng.random(n) < 0.3
+    stored = s.get(np.arange(n)).astype(np.float64)
+    qq = quantize_like_store(q).astype(np.float64)
+
+    def check(live, key, k=25):
+        d_ref, r_ref = cosine_topk(stored, qq, k, live=live, normalize=False)
+        d, r = s.search(q, k, allow=allow, mask_key=key)
+        s_ref = np.where(r_ref >= 0, 1.0 - d_ref, -np.inf)
+        s_gpu = np.where(r >= 0, 1.0 - d.astype(np.float64), -np.inf)
+        assert same_topk_modulo_ties(r, s_gpu, r_ref, s_ref, EPS)
+        ok = r >= 0
+        assert np.array_equal(ok, r_ref >= 0)
+        assert allow[r[ok]].all()
+        return r
+
+    live = allow.copy()
+    check(live, 7)
+    check(live, 7)                        # cached device mask
+    r = check(live, 0)                    # uncached
+    dead = np.unique(r[:, :3].reshape(-1))
+    s.remove(dead)                        # store version changes -> mask rebuilt
+    live[dead] = False
+    r2 = check(live, 7)
+    assert not np.isin(r2, dead).any()
+    allow[:] = False
+    allow[:5] = True                      # fewer eligible rows than k
+    elig = [i for i in range(5) if i not in set(dead.tolist())]
+    d3, r3 = s.search(q, 10, allow=allow, mask_key=8)
+    for row in r3:
+        assert sorted(row[: len(elig)].tolist()) == elig and (row[len(elig):] == -1).all()
+    with pytest.raises(Exception):
+        s.search(q, 10, allow=allow[:-1])
