@@ -182,3 +182,49 @@ def test_http_seam_on_the_hip_models():
                                           "documents": texts}).json()["results"]
     lg = rer.score(q, texts)
     assert [r["index"] for r in res] == sorted(range(len(texts)), key=lambda i: (-lg[i], i))
+
+
+def test_ingest_write_path_long_chunks():
+    # VectorIndexer.create/update/delete_index (index/vector_and_full_text_index.py:29-225) with
+    # chunk-sized inputs (~400-600 tokens, truncated at the model's 512): GPU embeddings == oracle,
+    # the chunks are searchable, updates replace ids, deletes remove them.
+    from types import SimpleNamespace
+    from super_rag_amd.embed import EmbeddingService
+    from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
+    from super_rag_amd.index import VectorIndexer, chunk_text
+    from super_rag_amd.models import QueryWithEmbedding
+    from super_rag_amd.tokenizer import Tokenizer
+    from super_rag_amd import vectorstore as V
+
+    es = ModelSpec("t-small", "bert", 30522, 384, 2, 6, 1536, 512, 2, 1e-12, 0)
+    w = random_weights(es, seed=12, style="test")
+    tok = Tokenizer(es)
+    svc = EmbeddingService("openai", "BAAI/bge-small-en", "", "", 10, encoder=Encoder(es, weights=w),
+                           tokenizer=tok, device_batch=16)
+    rng = np.random.default_rng(13)
+    words = [f"t{i}" for i in range(3000)]
+    parts = [SimpleNamespace(content=" ".join(rng.choice(words, int(rng.integers(380, 620)))),
+                             metadata={"name": f"doc{i}.md", "titles": ["Doc", f"S{i}"]})
+             for i in range(40)]
+    V._collections.clear()
+    conn = V.MI355XVectorStoreConnector({"collection": "gpu_ingest", "device": 0})
+    ix = VectorIndexer(conn, svc)
+    ids = ix.create_index(parts)["context_ids"]
+    assert len(ids) == len(parts)
+    texts = [chunk_text(p).replace("\n", " ") for p in parts]
+    lens = [len(tok.encode_batch([t])[0][0]) for t in texts]
+    assert max(lens) == 512                                  # truncated at max_length
+    for i in (int(np.argmax(lens)), int(np.argmin(lens))):
+        ref = R.embed(_cfg(es), w, *tok.encode_batch([texts[i]]))[0]
+        got = conn.get_vectors([ids[i]])[0]
+        assert np.linalg.norm(got - ref) < 4e-3              # fp16-stored row vs fp32 oracle
+    qv = svc.embed_query(texts[5])
+    hits = conn.search(QueryWithEmbedding(query="q", top_k=3, embedding=qv)).results
+    assert hits[0].metadata["source"] == "doc5.md" and hits[0].score < 1e-3
+    new_ids = ix.update_index(ids[:10], parts[:10])["context_ids"]
+    assert not set(new_ids) & set(ids) and conn.store is conn
+    n_rows, n_live = V._collections["gpu_ingest"].store.count()
+    assert n_live == len(parts)
+    ix.delete_index(new_ids + ids[10:])
+    assert V._collections["gpu_ingest"].store.count()[1] == 0
+    conn.delete_collection()
