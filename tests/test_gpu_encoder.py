@@ -198,3 +198,25 @@ def test_ln_folded_embedder(pool):
     got = enc.embed(ids, mask, pool=pool)
     ref = R.embed(_ref_cfg(spec), w, ids, mask, pool=pool)
     assert _rel(got, ref).max() <= 4e-3
+
+
+@pytest.mark.parametrize("S", [700, 2048])
+def test_bge_m3_widths_long_sequences(S):
+    # bge-m3 / bge-reranker-v2-m3 widths (XLM-R large: d 1024, 16 heads, FFN 4096; 2 of the 24
+    # layers) at sequence lengths past 512 (max_position 8194): the 64-key-tile attention path,
+    # the 256x256 GEMM tiles at d = 1024; CLS embedding and classification logit vs the oracle.
+    from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
+    emb = ModelSpec("m3-2l", "xlmr", 250002, 1024, 2, 16, 4096, 8194, 1, 1e-5, 1, bos_id=0,
+                    eos_id=2, pad_id=1, max_length=8192)
+    w = random_weights(emb, seed=51, style="test")
+    enc = Encoder(emb, weights=w)
+    ids, mask = _batch(emb, 3, S, seed=S)
+    got = enc.embed(ids, mask, pool="cls")
+    ref = R.embed(_ref_cfg(emb), w, ids, mask, pool="cls")
+    assert _rel(got, ref).max() <= 2e-3
+    rr = ModelSpec("m3r-2l", "xlmr", 250002, 1024, 2, 16, 4096, 8194, 1, 1e-5, 1, classifier=1,
+                   bos_id=0, eos_id=2, pad_id=1, max_length=8192, residual_fp16=True)
+    wr = random_weights(rr, seed=52, style="test")
+    lg = Encoder(rr, weights=wr).cross_score(ids, mask)
+    lg_ref = R.cross_logits(_ref_cfg(rr), wr, ids, mask)
+    assert np.abs(lg - lg_ref).max() <= 1e-2 * (1.0 + np.abs(lg_ref).max())
