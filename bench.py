@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-queries", type=int, default=2)
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
+    ap.add_argument("--dist-backend", default=os.environ.get("SR_BENCH_BACKEND", "nccl"),
+                    help="nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     return ap.parse_args()
 
 
@@ -76,11 +78,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dist_backend == "gloo":  # rehearsal mode: ranks may share the visible GPUs
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from super_rag_amd import _native as N
     from super_rag_amd.encoder import MODELS, Encoder, random_weights
@@ -155,7 +162,7 @@ def main():
     N.profile_enable(False)
     prof = N.profile_read()
     if world > 1:
-        t = torch.tensor([dt], device=dev)
+        t = torch.tensor([dt], device=dev if a.dist_backend != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     queries = world * a.batch * a.steps

@@ -57,13 +57,23 @@ class SearchPipeline:
         if self.world == 1:
             return self.store.search_dev(q_emb, self.K, row_offset=self.offset)
         import torch.distributed as dist
-        allq = torch.empty((self.world * B, q_emb.shape[1]), dtype=q_emb.dtype, device=q_emb.device)
-        dist.all_gather_into_tensor(allq, q_emb.contiguous(), group=self.group)
-        sims, rows = self.store.search_dev(allq, self.K, row_offset=self.offset)
+        # RCCL moves device tensors; the gloo backend (CPU tests, rehearsals of several ranks on
+        # one GPU) stages the same exchange through host memory
+        host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda
+        dev = q_emb.device
+        qx = q_emb.contiguous().cpu() if host else q_emb.contiguous()
+        allq = torch.empty((self.world * B, q_emb.shape[1]), dtype=q_emb.dtype, device=qx.device)
+        dist.all_gather_into_tensor(allq, qx, group=self.group)
+        sims, rows = self.store.search_dev(allq.to(dev) if host else allq, self.K,
+                                           row_offset=self.offset)
+        if host:
+            sims, rows = sims.cpu(), rows.cpu()
         rs = torch.empty_like(sims)
         rr = torch.empty_like(rows)
         dist.all_to_all_single(rs, sims, group=self.group)
         dist.all_to_all_single(rr, rows, group=self.group)
+        if host:
+            rs, rr = rs.to(dev), rr.to(dev)
         return self.merge_fn(rs.view(self.world, B, self.K), rr.view(self.world, B, self.K),
                              self.K, device=q_emb.device.index or 0)
 

@@ -67,3 +67,85 @@ def test_pipeline_stages_match_oracle(res16):
                                      lg_ref[b, order][None], 2 * tol)
         got = dict(zip(cand[b].tolist(), range(K)))
         np.testing.assert_allclose(flog[b], lg_ref[b, [got[r] for r in final[b]]], atol=tol)
+
+
+def _sharded_worker(rank, world, port, out_q):
+    # one rank of a world-size-2 SearchPipeline sharing the box's GPU (gloo exchange staged through
+    # host memory; the same code runs over RCCL, one rank per GPU, in bench.py)
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "super-rag_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        res = _run_pipeline(rank, world)
+        out_q.put((rank, res))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_pipeline(rank, world, sharded=True):
+    # rank's B queries; sharded: over rows [r0, r1) of the corpus (shard_offset r0) inside a
+    # world-size process group, else over the whole corpus in a single process
+    import torch
+    from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
+    from super_rag_amd.pipeline import SearchPipeline
+    from super_rag_amd.store import NativeStore
+    es = ModelSpec("e", "bert", 2000, 128, 2, 2, 256, 64, 2, 1e-12, 0)
+    rs = ModelSpec("r", "xlmr", 2000, 128, 2, 2, 256, 80, 1, 1e-5, 1, classifier=1, bos_id=0,
+                   eos_id=2, pad_id=1, residual_fp16=True)
+    emb = Encoder(es, weights=random_weights(es, 1, "test"))
+    rer = Encoder(rs, weights=random_weights(rs, 2, "test"))
+    rng = np.random.default_rng(0)
+    N, B, K, k, S = 30001, 8, 20, 5, 48
+    corpus = rng.standard_normal((N, 128)).astype(np.float32)
+    p_tok = rng.integers(5, 2000, (N, 40)).astype(np.int32)
+    p_len = rng.integers(1, 41, N).astype(np.int32)
+    q_ids = rng.integers(5, 2000, (world * B, 16)).astype(np.int32)
+    q_ids[:, 0] = 101
+    q_tok = rng.integers(5, 2000, (world * B, 10)).astype(np.int32)
+    q_len = rng.integers(1, 11, world * B).astype(np.int32)
+    per = (N + world - 1) // world
+    r0, r1 = (rank * per, min(N, (rank + 1) * per)) if sharded else (0, N)
+    store = NativeStore(128)
+    store.add(corpus[r0:r1])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    pipe = SearchPipeline(emb, rer, store, t(p_tok), t(p_len), k_candidates=K, k_final=k,
+                          pair_len=S, shard_offset=r0)
+    mine = slice(rank * B, (rank + 1) * B)
+    res = pipe.run(t(q_ids[mine]), t(np.ones_like(q_ids[mine])), t(q_tok[mine]), t(q_len[mine]))
+    torch.cuda.synchronize()
+    return {f: getattr(res, f).cpu().numpy() for f in ("rows", "logits", "cand_rows", "cand_sims")}
+
+
+def test_two_rank_sharded_pipeline_equals_single_process():
+    # world-size-2 rehearsal of the multi-GPU path on one GPU: C1 all-gather of the query
+    # embeddings, per-shard top-K with global row offsets, C2 all-to-all, K2 merge, rerank of the
+    # rank's own queries == the single-process pipeline over the whole corpus.
+    import os
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 200
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process: every rank's queries over the full corpus
+    import torch.distributed as dist
+    assert not dist.is_initialized()
+    full = {r: _run_pipeline(r, world, sharded=False) for r in range(world)}
+    for r in range(world):
+        np.testing.assert_array_equal(got[r]["cand_rows"], full[r]["cand_rows"])
+        np.testing.assert_allclose(got[r]["cand_sims"], full[r]["cand_sims"], atol=1e-6)
+        np.testing.assert_array_equal(got[r]["rows"], full[r]["rows"])
+        np.testing.assert_allclose(got[r]["logits"], full[r]["logits"], atol=1e-5)
