@@ -438,27 +438,55 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   const int nk = K / GBK;
   const int arow = wn * 128 + (lane & 15), brow = wm * 64 + (lane & 15), c0 = lane >> 4;
 
-  uint32_t vw[4], vx[4];
-  stage_offsets<4>(vw, K, wave, lane);
-  stage_offsets<4>(vx, lda, wave, lane);
+  // LDS-DMA staging is split by K-step parity: the 4 waves of group (s & 1) issue all 64 pieces
+  // (8 rows x 128 B each, 16 per wave) of K-step s, the other group none.  A piece costs its wave
+  // ~60-180 issue cycles; with both halves loading in lockstep the two waves of every SIMD stalled
+  // together, now one wave per SIMD loads while its partner keeps the matrix pipe busy.
+  // Piece p's lane offset depends on p only through p * 8 rows (uniform, in soffset) and the
+  // swizzle parity p & 1, so a lane keeps 2 offsets per operand.
+  const int grp = wave >> 2, w4 = wave & 3;
+  uint32_t vbw[2], vbx[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int ch = (lane & 7) ^ ((lane >> 4) + 4 * par);
+    vbw[par] = (uint32_t)(((int64_t)(lane >> 3) * K + ch * 8) * 2);
+    vbx[par] = (uint32_t)(((int64_t)(lane >> 3) * lda + ch * 8) * 2);
+  }
   // tile panels: W rows [nn, nn+256) and X rows [mm, min(M, mm+256)) (a lambda may not carry the
   // buffer-resource type through its signature: hipcc then drops the host stubs of this template)
   auto stage = [&](int kt, half_t* s, int mm, int nn) {
-    stage_buf<4>(panel_rsrc(W + (int64_t)nn * K, (int64_t)BN * K * 2), vw, kt * GBK * 2, s, wave);
-    stage_buf<4>(panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2),
-                 vx, kt * GBK * 2, s + BN * GBK, wave);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto rw = panel_rsrc(W + (int64_t)nn * K, (int64_t)BN * K * 2);
+    const auto rx = panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2);
+    // row-group offsets advanced in place (an opaque running value: precomputed per piece and
+    // hoisted, the 32 soffsets would exhaust the SGPRs)
+    int sw = w4 * 8 * 16 * K + kt * GBK * 2, sx = w4 * 8 * 16 * (int)lda + kt * GBK * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      asm volatile("" : "+s"(sw));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, SR_LDS(s + (w4 * 8 + i) * 8 * GBK), 16,
+                                               vbw[i & 1], sw, 0, 0);
+      sw += 16 * K;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      asm volatile("" : "+s"(sx));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, SR_LDS(s + BN * GBK + (w4 * 8 + i) * 8 * GBK), 16,
+                                               vbx[i & 1], sx, 0, 0);
+      sx += 16 * (int)lda;
+    }
+#endif
   };
 
   float4v acc[8][4];
   half8 aX[4], aY[4], bX[4], bY[4];
 
-  // prologue of the first tile
-  stage(0, lds, m0, n0);
-  if (nk > 1) {
-    stage(1, lds + STAGE, m0, n0);
-    SR_WAITCNT(8, 15);
-  } else {
+  // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
+  if (grp == 0) {
+    stage(0, lds, m0, n0);
     SR_WAITCNT(0, 15);
+  } else if (nk > 1) {
+    stage(1, lds + STAGE, m0, n0);
   }
   __builtin_amdgcn_s_barrier();
   bool stores_pending = false;  // 32 unchecked epilogue stores of the previous tile in flight
@@ -512,11 +540,15 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (SN == 1 && DIAG != 1) stage(kt + 2, cur, m0, n0);
+    // (group (kt & 1) stages K-step kt + 2 in one burst while the partner wave of every SIMD,
+    // from the other group, runs its MFMAs)
+    if (SN == 1 && DIAG != 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
     if (SN == 2) {
       if (more_) {
-        stage(0, lds, mn, nn);
-        stage(1, lds + STAGE, mn, nn);
+        if (grp == 0)
+          stage(0, lds, mn, nn);
+        else
+          stage(1, lds + STAGE, mn, nn);
       }
     }
     // p3: A[4..7] x B' (k 32..63); reads K-step kt+1's p0 operands
@@ -531,15 +563,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bY[j], acc[4 + i][j], 0, 0, 0);
-    if (SN == 1) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    } else if (RN) {
+    if (RN) {
       SR_INTERLEAVE(8);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -627,13 +651,21 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
                                        Y, ldy, lf);
     }
     if (!more) break;
-    // next tile: K-step 0 landed (younger: K-step 1's 8 glds + 32 stores when unchecked)
+    // next tile: K-step 0 (group 0's 16 glds) landed; younger: the epilogue's NSTORE stores
+    // (group 1: its K-step 1 glds too, awaited in K-step 0).  Unchecked tiles: wait for all.
     if (!full)
-      SR_WAITCNT(8, 15);
-    else if constexpr (PipeEpi<EPI>::NSTORE == 16)
-      SR_WAITCNT(24, 15);
-    else
-      SR_WAITCNT(40, 15);
+      SR_WAITCNT(0, 15);
+    else if constexpr (PipeEpi<EPI>::NSTORE == 16) {
+      if (grp == 0)
+        SR_WAITCNT(16, 15);
+      else
+        SR_WAITCNT(32, 15);
+    } else {
+      if (grp == 0)
+        SR_WAITCNT(32, 15);
+      else
+        SR_WAITCNT(48, 15);
+    }
     __builtin_amdgcn_s_barrier();
     stores_pending = full;
     t = t_next;
