@@ -203,6 +203,13 @@ def main():
                                 else f"{dom['bytes'] / dom['launches']:.4g} B"),
                  "algorithmic_B_per_launch": round(dom["bytes"] / dom["launches"])})
     roof["traffic"], roof["traffic_source"] = pmc_traffic(dom_name)
+    pmc = pmc_record(dom_name)
+    if pmc and pmc.get("clock_ghz") and roof["bound"] == "mfma":
+        # the clock the chip holds under this MFMA load (DVFS) and the matrix-pipe utilisation
+        # measured by the PMC pass: frac of the spec peak vs of the peak at the held clock
+        roof["pmc_clock_ghz"] = pmc["clock_ghz"]
+        roof["pmc_mfma_util"] = pmc.get("mfma_util")
+        roof["peak_at_held_clock"] = round(PEAK_F16_TFLOPS * pmc["clock_ghz"] / 2.4, 1)
     step_ms = dt / a.steps * 1e3
     kern = {k: {"ms_per_step": round(v["total_ms"] / a.steps, 3), "launches": v["launches"],
                 ("tflops" if v["flops"] > 0 else "gbs"):
@@ -246,6 +253,16 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_record(kernel):
+    """The kernel's record in the newest committed PMC summary (tools/pmc_traffic.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f)["kernels"].get(kernel)
 
 
 def pmc_traffic(kernel):

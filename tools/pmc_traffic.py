@@ -10,7 +10,13 @@ per logical kernel (the names `sr_profile_*` / bench.py use) the mean bytes per 
                                            coalesced streaming read — 128-B requests tallied as 64 B)
   write_B = WRITE_SIZE (KiB) x 1024        (exact for 16-B-per-lane stores)
 Both counters come from the L2 memory-side request counters, so Infinity-Cache hits are included.
+
+With a third pass (mfma/pmc_1: SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE) it also reports per kernel
+the clock the chip held (GRBM_GUI_ACTIVE is summed over the 8 XCDs: / 8 / duration) and the matrix
+pipe utilisation = MFMA busy cycles (16 per v_mfma_f32_16x16x32_f16, summed over SIMDs) / (1024
+SIMDs x duration x held clock).
 """
+import os
 import csv
 import json
 import re
@@ -66,12 +72,36 @@ def main():
         wb = w_tot.get(k, 0.0) / max(w_n.get(k, 1), 1) * 1024
         out["kernels"][k] = {"launches": f_n.get(k, 0), "fetch_B": round(fb),
                              "write_B": round(wb), "traffic_B": round(fb + wb)}
+    mf = f"{src}/mfma/pmc_1/run_counter_collection.csv"
+    if os.path.exists(mf):
+        busy, gui, dur, seen = defaultdict(float), defaultdict(float), defaultdict(float), set()
+        with open(mf) as f:
+            for row in csv.DictReader(f):
+                k = logical(row["Kernel_Name"])
+                if k is None:
+                    continue
+                if row["Counter_Name"] == "SQ_VALU_MFMA_BUSY_CYCLES":
+                    busy[k] += float(row["Counter_Value"])
+                elif row["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                    gui[k] += float(row["Counter_Value"])
+                if row["Dispatch_Id"] not in seen:
+                    seen.add(row["Dispatch_Id"])
+                    dur[k] += (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
+        out["method"] += ("; mfma pass: clock = GRBM_GUI_ACTIVE / 8 / duration, mfma_util = "
+                          "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x duration x clock)")
+        for k in dur:
+            if dur[k] <= 0 or k not in out["kernels"]:
+                continue
+            clk = gui[k] / 8.0 / dur[k]
+            out["kernels"][k]["clock_ghz"] = round(clk / 1e9, 3)
+            out["kernels"][k]["mfma_util"] = round(busy[k] / (1024.0 * dur[k] * clk), 4) if clk else None
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     for k, v in sorted(out["kernels"].items(),
                        key=lambda kv: -kv[1]["traffic_B"] * kv[1]["launches"]):
         print(f"{k:32s} launches {v['launches']:5d}  fetch {v['fetch_B'] / 1e6:10.2f} MB  "
-              f"write {v['write_B'] / 1e6:10.2f} MB  per launch")
+              f"write {v['write_B'] / 1e6:10.2f} MB  per launch  clock {v.get('clock_ghz')} GHz  "
+              f"mfma_util {v.get('mfma_util')}")
 
 
 if __name__ == "__main__":

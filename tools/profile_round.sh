@@ -3,6 +3,8 @@
 #   1. kernel-trace + stats of the default bench command
 #   2. FETCH_SIZE and WRITE_SIZE in separate PMC passes (MI355X_MICROARCH.md: one TCC counter
 #      group per pass) over a 1-step bench
+#   3. MFMA busy cycles + GRBM_GUI_ACTIVE (matrix-pipe utilisation and the clock actually held)
+# Summaries: python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles/<tag>_pmc_traffic.json
 # Outputs under gpurun_out/prof_<tag>/.
 set -e
 TAG=${1:-r01}
@@ -15,3 +17,5 @@ timeout -k 10 600 rocprofv3 -i tools/pmc_fetch.txt -d $OUT/fetch -o run --output
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_fetch.log 2>&1
 timeout -k 10 600 rocprofv3 -i tools/pmc_write.txt -d $OUT/write -o run --output-format csv -- \
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_write.log 2>&1
+timeout -k 10 600 rocprofv3 -i tools/pmc_mfma.txt -d $OUT/mfma -o run --output-format csv -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_mfma.log 2>&1
