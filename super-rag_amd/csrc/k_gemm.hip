@@ -357,6 +357,40 @@ struct PipeEpi {
   }
 };
 
+// EPI_SCAN epilogue (K1 threshold mode on the GEMM main loop): lane owns
+// sim(row n = nw0 + 16i + 4(lane>>4) + r, query q = mw0 + 16j + (lane&15)) of the chunk; keys of
+// live rows with sim >= tau[q] are appended to q's candidate list (cap entries, overflow counted).
+__device__ __forceinline__ void scan_epilogue(float4v (&acc)[8][4], int nw0, int mw0, int lane, int B,
+                                              int nrows, const float* __restrict__ tau,
+                                              const uint8_t* __restrict__ live,
+                                              uint64_t* __restrict__ cand, int cap, const LnFold& lf) {
+  float t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = mw0 + 16 * j + (lane & 15);
+    t[j] = q < B ? tau[q] : INFINITY;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int nb = nw0 + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + r;
+      if (n >= nrows) continue;
+      if (live != nullptr && live[n] == 0) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float sim = acc[i][j][r];
+        if (sim >= t[j]) {  // false for padded queries (t = inf)
+          const int q = mw0 + 16 * j + (lane & 15);
+          const int pos = atomicAdd(reinterpret_cast<int*>(lf.stat_out) + q, 1);
+          if (pos < cap) cand[(int64_t)q * cap + pos] = make_key(sim, (uint32_t)(lf.stat_ld + n));
+        }
+      }
+    }
+  }
+}
+
 // Buffer-resource LDS-DMA staging (buffer_load_dwordx4 ... lds): the tile's panel base lives in
 // the SGPR descriptor, the K offset in soffset, so a lane keeps ONE 32-bit VGPR offset per
 // instruction for the whole kernel; rows past num_records read as zero (no clamp needed).
@@ -413,7 +447,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr int STAGE = (BN + BM) * GBK;  // halfs per buffer (64 KiB)
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
 
-  const int tiles_n = N / BN;
+  const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
   int t, t_end, t_step;
   {
@@ -456,7 +490,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // buffer-resource type through its signature: hipcc then drops the host stubs of this template)
   auto stage = [&](int kt, half_t* s, int mm, int nn) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const auto rw = panel_rsrc(W + (int64_t)nn * K, (int64_t)BN * K * 2);
+    const auto rw = panel_rsrc(W + (int64_t)nn * K, (int64_t)(N - nn < BN ? N - nn : BN) * K * 2);
     const auto rx = panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2);
     // row-group offsets advanced in place (an opaque running value: precomputed per piece and
     // hoisted, the 32 soffsets would exhaust the SGPRs)
@@ -597,7 +631,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     else
       kstep(kt, 0, false, lenient, 0, 0, false);
 
-    const bool full = m0 + BM <= M;
+    // (EPI_SCAN issues a data-dependent number of atomics / stores: never counted as pending)
+    const bool full = EPI != EPI_SCAN && m0 + BM <= M;
     if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
       const int g = lane >> 4, odd = g & 1;
       const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
@@ -643,6 +678,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
       if (sacc == 12345.678f) reinterpret_cast<float*>(Y)[tid] = sacc;
+    } else if constexpr (EPI == EPI_SCAN) {
+      scan_epilogue(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                    reinterpret_cast<const uint8_t*>(R), reinterpret_cast<uint64_t*>(Y), (int)ldy, lf);
     } else if (full) {
       PipeEpi<EPI>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr,
                                         Y, ldy, lf);
@@ -968,6 +1006,27 @@ static const char* epi_name(int epi) {
 }
 
 // Tile override for parity tests: SR_GEMM_TILE=small|big (read per launch), or gemm_force_tile().
+void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* live, int64_t r0,
+                             int64_t r1, const half_t* Q, int B, const float* tau, uint64_t* cand,
+                             int* cnt, int cap, hipStream_t s) {
+  SR_CHECK(B > 0 && B <= 256, "cosine_scan_gemm: 1..256 queries");
+  SR_CHECK(ldc % GBK == 0 && ldc >= 2 * GBK, "cosine_scan_gemm: padded dim must be a multiple of 64, >= 128");
+  if (r1 <= r0) return;
+  const int64_t n = r1 - r0;
+  SR_CHECK(n < (1ll << 31), "cosine_scan_gemm: chunk too large");
+  const double rows = (double)n;
+  ProfScope prof("cosine_scan", s, 2.0 * rows * ldc * B, rows * ldc * 2.0 + (double)B * ldc * 2.0);
+  LnFold lf;
+  lf.stat_out = reinterpret_cast<float*>(cnt);  // (EPI_SCAN field re-use, see LnFold)
+  lf.stat_ld = r0;
+  const int64_t tiles = ceil_div(n, 256);
+  const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+  hipLaunchKernelGGL((gemm_pipe_kernel<EPI_SCAN, true>), grid, block, 0, s, Q, ldc,
+                     corpus + r0 * ldc, tau, (const void*)(live ? live + r0 : nullptr), (int64_t)0,
+                     (void*)cand, (int64_t)cap, B, (int)n, (int)ldc, lf);
+  SR_LAUNCH_CHECK();
+}
+
 static int g_force_tile = -1;
 void gemm_force_tile(int t) { g_force_tile = t; }
 static int forced_tile() {

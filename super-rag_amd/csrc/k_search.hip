@@ -14,6 +14,8 @@
 // key by an MSB radix select (8-bit digits, per-wave LDS histograms, wave-parallel suffix scan)
 // and bitonic-sorts the k winners.  Keys are unique (row in the low word), so the k-th key is
 // exact and ties in similarity resolve by ascending row id, as the oracle does.
+#include <cstdlib>
+
 #include "sr_common.h"
 #include "sr_kernels.h"
 
@@ -420,6 +422,8 @@ int scan_query_tiles(int B) {
   return 16;
 }
 
+static bool g_scan_legacy = std::getenv("SR_SCAN_LEGACY") != nullptr;
+
 void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uint8_t* live,
                         int64_t r0, int64_t r1, const half_t* Q, int B, const float* tau,
                         uint64_t* cand, int* cnt, int cap, hipStream_t s) {
@@ -428,6 +432,11 @@ void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uin
   if (r1 <= r0) return;
   SR_CHECK(!dense || r1 - r0 <= cap, "cosine_scan: dense chunk larger than the candidate list");
   const int qt = scan_query_tiles(B);
+  if (!dense && qt == 16 && ldc >= 2 * SBK && r1 - r0 >= 8 * SROWS && !g_scan_legacy) {
+    // large query blocks: the pipelined 256 x 256 GEMM main loop with the threshold epilogue
+    launch_cosine_scan_gemm(corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap, s);
+    return;
+  }
   const dim3 grid((unsigned)ceil_div(r1 - r0, SROWS));
   const double rows = (double)(r1 - r0);
   ProfScope prof(dense ? "cosine_scan_dense" : "cosine_scan", s, 2.0 * rows * ldc * B,

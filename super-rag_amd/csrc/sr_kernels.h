@@ -18,7 +18,10 @@ enum Epilogue {
   EPI_LNF_F16 = 5,        // y = rstd * (acc - mu * c[n]) + b'[n], W' = W . diag(gamma) -> fp16
   EPI_LNF_GELU_F16 = 6,   // y = 2 gelu(same) (the FFN2 weight carries the 0.5)          -> fp16
   EPI_RES16_STATS = 7,    // y = acc + b + R (fp16, already normalised) -> fp16 + row statistics
-  EPI_LNR16_STATS = 8     // y = acc + b + LN(R) (R un-normalised)      -> fp16 + row statistics
+  EPI_LNR16_STATS = 8,    // y = acc + b + LN(R) (R un-normalised)      -> fp16 + row statistics
+  // K1 on the GEMM main loop (internal: launch_cosine_scan_gemm): W = corpus rows, X = queries,
+  // epilogue = threshold filter appending (sim, row) keys to per-query candidate lists
+  EPI_SCAN = 9
 };
 
 // Per-row statistics hand-over between GEMMs (Chan-combinable partials over 128-column spans):
@@ -31,6 +34,9 @@ struct LnFold {
   const float* gamma = nullptr;    // LNR: LayerNorm weight of the residual rows (its beta is
                                    //      pre-added to the GEMM bias)
   float* stat_out = nullptr;       // *_STATS: [M][N / 128] partials of the output rows
+  // EPI_SCAN re-uses the fields (kernel-argument SGPRs are scarce in the persistent kernels):
+  // stat_out = per-query candidate counts (int*), stat_ld = global row id of the chunk's first
+  // row; bias = tau[B], R = live flags of the chunk, Y = candidate keys [B][cap] (ldy = cap).
 };
 
 // k_gemm.hip — Y = epi(X . W^T + bias (+ R)); K % 64 == 0, N % 128 == 0.
@@ -44,6 +50,11 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
                          const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy,
                          int M, int N, int K, hipStream_t stream, const LnFold* lf = nullptr);
 void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
+// K1 for large query blocks (B in (128, 256]) on the pipelined GEMM: rows [r0, r1) of the corpus
+// against B queries; non-dense threshold mode only (same contract as launch_cosine_scan).
+void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* live, int64_t r0,
+                             int64_t r1, const half_t* Q, int B, const float* tau, uint64_t* cand,
+                             int* cnt, int cap, hipStream_t s);
 
 // k_attention.hip — ctx = MHA(qkv, key padding mask) for the first Sq query rows of each
 // sequence; ctx rows are laid out [B][Sq][d].

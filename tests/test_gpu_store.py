@@ -87,6 +87,23 @@ def test_multi_chunk_threshold_path():
     assert recall_at_k(r[:, :10], r_true) >= 0.99
 
 
+@pytest.mark.parametrize("dim,B", [(768, 256), (384, 200), (128, 160)])
+def test_large_query_block_gemm_scan(dim, B):
+    # query blocks of 129..256 scan the threshold chunks on the pipelined GEMM main loop
+    # (EPI_SCAN epilogue); 120k rows with tombstones: dense chunk, then 64k / 48k chunks whose
+    # last 256-row tile is partial
+    x = _clustered(120_000, dim, seed=dim + 1, centers=256)
+    s = _store(dim)
+    s.add(x)
+    dead = np.arange(5, 120_000, 7)
+    s.remove(dead)
+    live = np.ones(120_000, bool)
+    live[dead] = False
+    q = _queries(x, B, seed=B)
+    d, r = _check(s, q, 20, live=live)
+    assert not np.isin(r, dead).any()
+
+
 def test_tombstones_and_short_results():
     dim = 64
     x = _clustered(3000, dim, seed=5)
