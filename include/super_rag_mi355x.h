@@ -117,6 +117,53 @@ int sr_topk_merge_dev(const float* sims, const int64_t* rows, int P, int B, int 
                       float* out_sim, int64_t* out_rows, int device, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Lexical (BM25) index and hybrid dense + lexical retrieval  (BASELINE config 5)
+ * The reference declares a `fulltext_search` node type (schema/view_models.py:276-283,
+ * FulltextSearchParams{topk, keywords} at :1043-1047) and a merge slot for its output
+ * (nodeflow/runners/merge.py:18-20) but ships no backend for them; these entry points are that
+ * backend.  Rows are the same row ids as the companion sr_store (the connector adds both in step).
+ * Scoring is Okapi BM25 with Lucene's idf ln(1 + (N - df + 0.5) / (df + 0.5)) over LIVE rows,
+ * accumulated in 2^-16 fixed point (exact, order-independent); see DESIGN.md "Hybrid retrieval".
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct sr_lex sr_lex;
+
+int sr_lex_create(int device, float k1, float b, sr_lex** out);
+/* Append n documents: document i has the DISTINCT term ids terms[off[i] .. off[i+1]) with
+ * frequencies tf[...] (>= 1) and length dl[i] (tokens); off[0] == 0.  first_row receives the row
+ * id of document 0 (rows are consecutive). */
+int sr_lex_add(sr_lex* x, const int64_t* off, const int32_t* terms, const int32_t* tf,
+               const int32_t* dl, int64_t n, int64_t* first_row);
+int sr_lex_remove(sr_lex* x, const int64_t* rows, int64_t n);
+int sr_lex_stats(sr_lex* x, int64_t* n_rows, int64_t* n_live, int64_t* n_postings,
+                 int64_t* vocab, double* avgdl);
+/* BM25 top-k: query b is the term ids qterms[qoff[b] .. qoff[b+1]) (a repeated term counts once
+ * per occurrence; unknown ids are ignored).  out_score / out_rows: B x k host buffers sorted by
+ * (score desc, row asc); -inf / -1 past the matching rows.  allow (optional, n_rows bytes) as in
+ * sr_store_search_masked. */
+int sr_lex_search(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                  const uint8_t* allow, int64_t mask_key, float* out_score, int64_t* out_rows);
+int sr_lex_save(sr_lex* x, const char* path);
+int sr_lex_load(const char* path, int device, sr_lex** out);
+int sr_lex_compact(sr_lex* x, int64_t* old_to_new);
+void sr_lex_destroy(sr_lex* x);
+
+/* Reciprocal-rank fusion of two ranked row lists per query (B x ka and B x kb, -1 padded), as
+ * graphiti rrf (graphiti_core/search/search_utils.py:1762-1778): score = sum 1 / (rank +
+ * rank_const) in fp64, order (score desc, first appearance), rows with score < min_score
+ * dropped.  Host buffers; computed on `device`. */
+int sr_rrf_fuse(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
+                int rank_const, double min_score, int k_out, double* out_score,
+                int64_t* out_rows, int device);
+/* Hybrid retrieval on one device: dense top-k_each (sr_store_search semantics) and BM25
+ * top-k_each of the same queries, fused on the device by rrf into B x k (out_score = rrf score).
+ * q: B x dim host fp32; the lexical query as in sr_lex_search; allow optional (mask_key as in
+ * sr_store_search_masked). */
+int sr_hybrid_search(sr_store* s, sr_lex* x, const float* q, const int64_t* qoff,
+                     const int32_t* qterms, int B, int k, int k_each, int rank_const,
+                     double min_score, const uint8_t* allow, int64_t mask_key,
+                     double* out_score, int64_t* out_rows);
+
+/* ------------------------------------------------------------------------------------------------
  * Transformer encoder (BERT / XLM-R family: bge-small/base-en, bge-m3, bge-reranker-*)
  * Weights are set by Hugging Face tensor name without the model prefix, e.g.
  * "embeddings.word_embeddings.weight", "encoder.layer.3.attention.self.query.weight",

@@ -14,6 +14,9 @@ struct sr_store {
 struct sr_encoder {
   sr::Encoder* impl;
 };
+struct sr_lex {
+  sr::LexIndex* impl;
+};
 
 namespace sr {
 
@@ -291,6 +294,175 @@ int sr_topk_merge_dev(const float* sims, const int64_t* rows, int P, int B, int 
 }
 
 // ---- encoder ---------------------------------------------------------------------------------
+// ---- lexical index / hybrid ------------------------------------------------------------------
+int sr_lex_create(int device, float k1, float b, sr_lex** out) {
+  SR_API_BEGIN
+  SR_NONNULL(out);
+  *out = nullptr;
+  *out = new sr_lex{new sr::LexIndex(device, k1, b)};
+  SR_API_END
+}
+
+int sr_lex_add(sr_lex* x, const int64_t* off, const int32_t* terms, const int32_t* tf,
+               const int32_t* dl, int64_t n, int64_t* first_row) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->add(off, terms, tf, dl, n, first_row);
+  SR_API_END
+}
+
+int sr_lex_remove(sr_lex* x, const int64_t* rows, int64_t n) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  if (n > 0) SR_NONNULL(rows);
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->remove(rows, n);
+  SR_API_END
+}
+
+int sr_lex_stats(sr_lex* x, int64_t* n_rows, int64_t* n_live, int64_t* n_postings, int64_t* vocab,
+                 double* avgdl) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->stats(n_rows, n_live, n_postings, vocab, avgdl);
+  SR_API_END
+}
+
+int sr_lex_search(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                  const uint8_t* allow, int64_t mask_key, float* out_score, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  if (B > 0) {
+    SR_NONNULL(qoff);
+    SR_NONNULL(out_score);
+    SR_NONNULL(out_rows);
+    if (qoff[B] > 0) SR_NONNULL(qterms);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->search_host(qoff, qterms, B, k, allow, mask_key, out_score, out_rows);
+  SR_API_END
+}
+
+int sr_lex_save(sr_lex* x, const char* path) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  SR_NONNULL(path);
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->save(path);
+  SR_API_END
+}
+
+int sr_lex_load(const char* path, int device, sr_lex** out) {
+  SR_API_BEGIN
+  SR_NONNULL(path);
+  SR_NONNULL(out);
+  *out = nullptr;
+  sr::LexIndex* li = sr::LexIndex::load(path, device);
+  *out = new sr_lex{li};
+  SR_API_END
+}
+
+int sr_lex_compact(sr_lex* x, int64_t* old_to_new) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->compact(old_to_new);
+  SR_API_END
+}
+
+void sr_lex_destroy(sr_lex* x) {
+  if (!x) return;
+  delete x->impl;
+  delete x;
+}
+
+int sr_rrf_fuse(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
+                int rank_const, double min_score, int k_out, double* out_score,
+                int64_t* out_rows, int device) {
+  SR_API_BEGIN
+  SR_CHECK(B >= 0, "rrf: negative batch");
+  if (B == 0) return SR_OK;
+  SR_NONNULL(out_score);
+  SR_NONNULL(out_rows);
+  if (ka > 0) SR_NONNULL(rows_a);
+  if (kb > 0) SR_NONNULL(rows_b);
+  sr::DeviceGuard g(device);
+  const size_t ba = (size_t)B * ka * 8, bb = (size_t)B * kb * 8, bo = (size_t)B * k_out * 8;
+  sr::DevBuf ws;
+  ws.reserve(ba + bb + 2 * bo + 8);
+  char* w = ws.as<char>();
+  int64_t* da = reinterpret_cast<int64_t*>(w);
+  int64_t* db = reinterpret_cast<int64_t*>(w + ba);
+  double* ds = reinterpret_cast<double*>(w + ba + bb);
+  int64_t* dr = reinterpret_cast<int64_t*>(w + ba + bb + bo);
+  hipStream_t st = nullptr;
+  SR_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  try {
+    if (ba) SR_HIP(hipMemcpyAsync(da, rows_a, ba, hipMemcpyHostToDevice, st));
+    if (bb) SR_HIP(hipMemcpyAsync(db, rows_b, bb, hipMemcpyHostToDevice, st));
+    sr::launch_rrf_fuse(da, ka, db, kb, B, rank_const, min_score, k_out, ds, dr, st);
+    SR_HIP(hipMemcpyAsync(out_score, ds, bo, hipMemcpyDeviceToHost, st));
+    SR_HIP(hipMemcpyAsync(out_rows, dr, bo, hipMemcpyDeviceToHost, st));
+    SR_HIP(hipStreamSynchronize(st));
+  } catch (...) {
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    throw;
+  }
+  SR_HIP(hipStreamDestroy(st));
+  SR_API_END
+}
+
+int sr_hybrid_search(sr_store* s, sr_lex* x, const float* q, const int64_t* qoff,
+                     const int32_t* qterms, int B, int k, int k_each, int rank_const,
+                     double min_score, const uint8_t* allow, int64_t mask_key,
+                     double* out_score, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  SR_NONNULL(x);
+  SR_CHECK(B >= 0, "hybrid: negative batch");
+  if (B == 0) return SR_OK;
+  SR_NONNULL(q);
+  SR_NONNULL(qoff);
+  SR_NONNULL(out_score);
+  SR_NONNULL(out_rows);
+  SR_CHECK(k_each >= 1 && k_each <= SR_MAX_TOPK, "hybrid: k_each must be in [1, 1024]");
+  SR_CHECK(k >= 1 && k <= 2 * k_each, "hybrid: k must be in [1, 2 * k_each]");
+  std::scoped_lock lk(s->impl->mu, x->impl->mu);
+  sr::Store& st = *s->impl;
+  sr::LexIndex& lx = *x->impl;
+  SR_CHECK(st.device() == lx.device(), "hybrid: store and lexical index on different devices");
+  int64_t lrows = 0;
+  lx.stats(&lrows, nullptr, nullptr, nullptr, nullptr);
+  SR_CHECK(lrows == st.rows(), "hybrid: store and lexical index hold different row counts");
+  sr::DeviceGuard g(st.device());
+  hipStream_t sm = lx.stream();
+  const size_t bq = (size_t)B * st.dim() * 4, be = (size_t)B * k_each * 8, bo = (size_t)B * k * 8;
+  sr::DevBuf ws;
+  ws.reserve(bq + 4 * be + 2 * bo + 64);
+  char* w = ws.as<char>();
+  float* dq = reinterpret_cast<float*>(w);
+  float* dsim = reinterpret_cast<float*>(w + bq);
+  int64_t* drow = reinterpret_cast<int64_t*>(w + bq + be);
+  float* lsc = reinterpret_cast<float*>(w + bq + 2 * be);
+  int64_t* lrow = reinterpret_cast<int64_t*>(w + bq + 3 * be);
+  double* os = reinterpret_cast<double*>(w + bq + 4 * be);
+  int64_t* orow = reinterpret_cast<int64_t*>(w + bq + 4 * be + bo);
+  const uint8_t* elig = st.eligibility(allow, mask_key);
+  lx.begin(sm);
+  SR_HIP(hipMemcpyAsync(dq, q, bq, hipMemcpyHostToDevice, sm));
+  st.search_dev(dq, SR_DTYPE_F32, B, k_each, dsim, drow, 0, sm, elig);
+  lx.search_dev(qoff, qterms, B, k_each, allow, mask_key, lsc, lrow, sm);
+  sr::launch_rrf_fuse(drow, k_each, lrow, k_each, B, rank_const, min_score, k, os, orow, sm);
+  SR_HIP(hipMemcpyAsync(out_score, os, bo, hipMemcpyDeviceToHost, sm));
+  SR_HIP(hipMemcpyAsync(out_rows, orow, bo, hipMemcpyDeviceToHost, sm));
+  lx.end(sm);
+  SR_HIP(hipStreamSynchronize(sm));
+  SR_API_END
+}
+
 int sr_encoder_create(const sr_encoder_config* cfg, int device, sr_encoder** out) {
   SR_API_BEGIN
   SR_NONNULL(cfg);

@@ -1,0 +1,651 @@
+// BM25 lexical index over the store's rows and the reciprocal-rank fusion of a dense and a lexical
+// ranking ("dense + BM25 fusion"; the reference's fulltext index is a no-op and its
+// node slot `fulltext_search_docs` (nodeflow/runners/merge.py:18-20) is empty, so the scoring
+// below is this library's own definition, documented in DESIGN.md, and the fusion follows the
+// reference's only precedent, graphiti rrf, super_rag/graphiti/graphiti_core/search/search_utils.py:1762-1778).
+//
+// Layout in HBM
+//   forward index (append-only, row order): fterm[P] int32, fval[P] u64 = row << 32 | tf;
+//   dlen[rows] int32 (document length in tokens), live[rows] u8;
+//   inverted index (CSR by term over LIVE documents, rebuilt on the device when dirty):
+//   off[T + 1] int64, post[nnz] u64 = row << 32 | tf, rows ascending inside a term (stable radix
+//   sort of the row-ordered forward index by term id).
+//
+// Scoring (one query block of QB queries):
+//   L1 lex_score: one workgroup per (query, term, 4096-posting chunk).  Each posting's Okapi weight
+//      w = idf * (tf * (k1 + 1)) / (tf + k1 * ((1 - b) + b * (dl / avgdl)))   (fp32, no FMA
+//      contraction, so a numpy float32 restatement reproduces it bit for bit) is quantised to
+//      q = max(1, rint(w * 2^16)) x (query multiplicity) and added with a 32-bit atomic into the
+//      query's dense accumulator acc[qb][row].  The first touch of a row (old == 0; q >= 1 so a
+//      touched row is never 0) appends the row to the query's touched list.  Integer sums make the
+//      result independent of the atomic order: bit-exact against the oracle.
+//   L2 lex_select: one workgroup per query: exact top-k of keys (acc << 32 | ~row) over the touched
+//      list with the block radix select (sr_topk.h, keys gathered from HBM each pass), then the
+//      touched accumulator entries are reset to 0 (the accumulator stays all-zero between calls).
+// Fusion:
+//   F1 rrf_fuse: one workgroup per query: rrf score of a row = sum over the lists of
+//      1 / (rank + rank_const) in fp64 (list a first, as graphiti accumulates), ordered by score
+//      descending with ties by first appearance (a's ranks, then b's new rows in b order), as
+//      Python's stable sort over the insertion-ordered dict does; rows below min_score dropped.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "sr_kernels.h"
+#include "sr_runtime.h"
+#include "sr_topk.h"
+
+namespace sr {
+
+constexpr int LEX_CHUNK = 4096;      // postings per scoring workgroup
+constexpr int LEX_THREADS = 256;
+constexpr float LEX_SCALE = 65536.f;  // fixed-point unit of the accumulated score
+
+struct LexChunk {
+  int64_t start;  // first posting
+  int32_t len;    // postings in this chunk
+  int32_t qb;     // query index inside the block
+  float idf;
+  int32_t mult;   // multiplicity of the term in the query
+};
+
+// ---- rebuild ------------------------------------------------------------------------------------
+__global__ void lex_keys_kernel(const int32_t* __restrict__ fterm, const uint64_t* __restrict__ fval,
+                                const uint8_t* __restrict__ live, int64_t P, uint32_t dead_key,
+                                uint32_t* __restrict__ keys, int* __restrict__ df) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  const uint32_t row = (uint32_t)(fval[i] >> 32);
+  const int32_t t = fterm[i];
+  if (live[row]) {
+    keys[i] = (uint32_t)t;
+    atomicAdd(&df[t], 1);
+  } else {
+    keys[i] = dead_key;
+  }
+}
+
+// ---- L1 -----------------------------------------------------------------------------------------
+// (no FMA contraction anywhere below: the BM25 weight and the fp64 rrf sums are restated in numpy
+// / Python, which round every operation)
+#pragma clang fp contract(off)
+__device__ __forceinline__ uint32_t bm25_fixed(float idf, float tf, float dl, float avgdl, float k1,
+                                               float b, float one_minus_b, float k1p1) {
+  const float t1 = __fdiv_rn(dl, avgdl);
+  const float norm = k1 * (one_minus_b + b * t1);
+  const float w = idf * __fdiv_rn(tf * k1p1, tf + norm);
+  const float q = rintf(w * LEX_SCALE);
+  return q < 1.f ? 1u : (uint32_t)q;
+}
+
+__global__ __launch_bounds__(LEX_THREADS) void lex_score_kernel(
+    const LexChunk* __restrict__ chunks, const uint64_t* __restrict__ post,
+    const int32_t* __restrict__ dlen, const uint8_t* __restrict__ elig, int64_t rows,
+    float avgdl, float k1, float b, uint32_t* __restrict__ acc, int* __restrict__ tcnt,
+    const int64_t* __restrict__ toff, int32_t* __restrict__ touched) {
+  const LexChunk c = chunks[blockIdx.x];
+  const float one_minus_b = 1.f - b, k1p1 = k1 + 1.f;
+  uint32_t* a = acc + (int64_t)c.qb * rows;
+  int32_t* tl = touched + toff[c.qb];
+  for (int i = threadIdx.x; i < c.len; i += LEX_THREADS) {
+    const uint64_t v = post[c.start + i];
+    const uint32_t row = (uint32_t)(v >> 32);
+    if (elig && !elig[row]) continue;
+    const float tf = (float)(uint32_t)v;
+    const float dl = (float)dlen[row];
+    const uint32_t q = bm25_fixed(c.idf, tf, dl, avgdl, k1, b, one_minus_b, k1p1) * (uint32_t)c.mult;
+    const uint32_t old = atomicAdd(&a[row], q);
+    if (old == 0u) tl[atomicAdd(&tcnt[c.qb], 1)] = (int32_t)row;
+  }
+}
+
+// ---- L2 -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(SEL_THREADS, 1) void lex_select_kernel(
+    uint32_t* __restrict__ acc, int64_t rows, const int* __restrict__ tcnt,
+    const int64_t* __restrict__ toff, const int32_t* __restrict__ touched, int k,
+    float* __restrict__ out_score, int64_t* __restrict__ out_rows) {
+  __shared__ SelShared sh;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  uint32_t* a = acc + (int64_t)q * rows;
+  const int32_t* tl = touched + toff[q];
+  const int n = tcnt[q];
+  auto key = [&](int i) {
+    const uint32_t r = (uint32_t)tl[i];
+    return ((uint64_t)a[r] << 32) | (uint64_t)(0xffffffffu - r);
+  };
+  const int m = block_topk(key, n, k, sh);
+  for (int i = tid; i < k; i += blockDim.x) {
+    const bool ok = i < m;
+    const uint64_t kk = ok ? sh.sel[i] : 0ull;
+    out_score[(int64_t)q * k + i] = ok ? (float)(uint32_t)(kk >> 32) / LEX_SCALE : -INFINITY;
+    out_rows[(int64_t)q * k + i] = ok ? (int64_t)(0xffffffffu - (uint32_t)kk) : -1;
+  }
+  __syncthreads();  // every key read before the reset
+  for (int i = tid; i < n; i += blockDim.x) a[tl[i]] = 0u;
+}
+
+// ---- F1 -----------------------------------------------------------------------------------------
+constexpr int RRF_THREADS = 256;
+constexpr int RRF_MAX = 2 * SR_MAX_TOPK;
+
+__global__ __launch_bounds__(RRF_THREADS) void rrf_fuse_kernel(
+    const int64_t* __restrict__ rows_a, int ka, const int64_t* __restrict__ rows_b, int kb,
+    int rank_const, double min_score, int k_out, double* __restrict__ out_score,
+    int64_t* __restrict__ out_rows) {
+  __shared__ int64_t row[RRF_MAX];
+  __shared__ double score[RRF_MAX];
+  __shared__ int match[SR_MAX_TOPK];   // b item j: index in a, or -1
+  __shared__ int newpos[SR_MAX_TOPK];  // b item j (unmatched): its item index
+  __shared__ int na_s, nb_s, n_s;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int64_t* ra = rows_a + (int64_t)q * ka;
+  const int64_t* rb = rows_b + (int64_t)q * kb;
+  if (tid == 0) {
+    int na = 0, nb = 0;
+    while (na < ka && ra[na] >= 0) ++na;  // lists are -1 padded after their valid prefix
+    while (nb < kb && rb[nb] >= 0) ++nb;
+    na_s = na;
+    nb_s = nb;
+  }
+  __syncthreads();
+  const int na = na_s, nb = nb_s;
+  for (int i = tid; i < na; i += RRF_THREADS) {
+    row[i] = ra[i];
+    score[i] = 0.0 + 1.0 / (double)(i + rank_const);
+  }
+  for (int j = tid; j < nb; j += RRF_THREADS) {
+    const int64_t r = rb[j];
+    int m = -1;
+    for (int i = 0; i < na; ++i)
+      if (ra[i] == r) {
+        m = i;
+        break;
+      }
+    match[j] = m;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // new rows of list b keep b's order after a's rows (dict insertion order)
+    int n = na;
+    for (int j = 0; j < nb; ++j) newpos[j] = match[j] < 0 ? n++ : -1;
+    n_s = n;
+  }
+  __syncthreads();
+  for (int j = tid; j < nb; j += RRF_THREADS) {
+    const double add = 1.0 / (double)(j + rank_const);
+    if (match[j] >= 0) {
+      score[match[j]] = score[match[j]] + add;  // a row appears at most once per list
+    } else {
+      row[newpos[j]] = rb[j];
+      score[newpos[j]] = 0.0 + add;
+    }
+  }
+  __syncthreads();
+  const int n = n_s;
+  // rank = items strictly before this one in (score desc, insertion asc) order
+  for (int i = tid; i < n; i += RRF_THREADS) {
+    const double s = score[i];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += (score[j] > s || (score[j] == s && j < i)) ? 1 : 0;
+    if (rank < k_out) {
+      const bool keep = s >= min_score;
+      out_score[(int64_t)q * k_out + rank] = keep ? s : -INFINITY;
+      out_rows[(int64_t)q * k_out + rank] = keep ? row[i] : -1;
+    }
+  }
+  for (int i = n + tid; i < k_out; i += RRF_THREADS) {
+    out_score[(int64_t)q * k_out + i] = -INFINITY;
+    out_rows[(int64_t)q * k_out + i] = -1;
+  }
+}
+
+void launch_rrf_fuse(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
+                     int rank_const, double min_score, int k_out, double* out_score,
+                     int64_t* out_rows, hipStream_t s) {
+  SR_CHECK(ka >= 0 && ka <= SR_MAX_TOPK && kb >= 0 && kb <= SR_MAX_TOPK, "rrf: list length > 1024");
+  SR_CHECK(k_out >= 1 && k_out <= RRF_MAX, "rrf: k_out must be in [1, 2048]");
+  SR_CHECK(rank_const >= 1, "rrf: rank_const must be >= 1");
+  if (B <= 0) return;
+  ProfScope prof("rrf_fuse", s, 0.0, (double)B * (ka + kb) * 8.0);
+  hipLaunchKernelGGL(rrf_fuse_kernel, dim3(B), dim3(RRF_THREADS), 0, s, rows_a, ka, rows_b, kb,
+                     rank_const, min_score, k_out, out_score, out_rows);
+  SR_LAUNCH_CHECK();
+}
+
+// ================================================================================================
+// LexIndex
+LexIndex::LexIndex(int device, float k1, float b) : device_(device), k1_(k1), b_(b) {
+  SR_CHECK(k1 >= 0.f && b >= 0.f && b <= 1.f, "lex: need k1 >= 0 and 0 <= b <= 1");
+  DeviceGuard g(device_);
+  SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  SR_HIP(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  SR_HIP(hipEventRecord(done_, stream_));
+}
+
+LexIndex::~LexIndex() {
+  DeviceGuard g(device_);
+  if (stream_) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
+  if (done_) (void)hipEventDestroy(done_);
+}
+
+static void grow_copy(DevBuf& buf, size_t used_bytes, size_t need_bytes, hipStream_t s) {
+  if (need_bytes <= buf.bytes) return;
+  size_t cap = std::max<size_t>(need_bytes, std::max<size_t>(buf.bytes * 2, 1 << 16));
+  DevBuf nb;
+  nb.reserve(cap);
+  if (used_bytes) SR_HIP(hipMemcpyAsync(nb.p, buf.p, used_bytes, hipMemcpyDeviceToDevice, s));
+  SR_HIP(hipStreamSynchronize(s));
+  std::swap(buf.p, nb.p);
+  std::swap(buf.bytes, nb.bytes);
+}
+
+void LexIndex::add(const int64_t* off, const int32_t* terms, const int32_t* tf, const int32_t* dl,
+                   int64_t n, int64_t* first_row) {
+  SR_CHECK(n >= 0, "lex.add: negative count");
+  if (first_row) *first_row = rows_;
+  if (n == 0) return;
+  SR_CHECK(off && dl && off[0] == 0, "lex.add: off[0] must be 0");
+  const int64_t P = off[n];
+  SR_CHECK(P >= 0 && (P == 0 || (terms && tf)), "lex.add: null term arrays");
+  SR_CHECK(rows_ + n <= (int64_t)0x7fffffff, "lex.add: more than 2^31 rows");
+  std::vector<uint64_t> val((size_t)P);
+  for (int64_t i = 0; i < n; ++i) {
+    SR_CHECK(off[i + 1] >= off[i], "lex.add: off must be non-decreasing");
+    SR_CHECK(dl[i] >= 0, "lex.add: negative document length");
+    for (int64_t p = off[i]; p < off[i + 1]; ++p) {
+      SR_CHECK(terms[p] >= 0, "lex.add: negative term id");
+      SR_CHECK(tf[p] >= 1, "lex.add: term frequency must be >= 1");
+      val[(size_t)p] = ((uint64_t)(rows_ + i) << 32) | (uint32_t)tf[p];
+      vocab_ = std::max<int64_t>(vocab_, (int64_t)terms[p] + 1);
+    }
+  }
+  DeviceGuard g(device_);
+  begin(stream_);
+  grow_copy(fterm_, (size_t)P_ * 4, (size_t)(P_ + P) * 4, stream_);
+  grow_copy(fval_, (size_t)P_ * 8, (size_t)(P_ + P) * 8, stream_);
+  grow_copy(dlen_, (size_t)rows_ * 4, (size_t)(rows_ + n) * 4, stream_);
+  grow_copy(live_, (size_t)rows_, (size_t)(rows_ + n), stream_);
+  if (P) {
+    SR_HIP(hipMemcpyAsync(fterm_.as<int32_t>() + P_, terms, (size_t)P * 4, hipMemcpyHostToDevice, stream_));
+    SR_HIP(hipMemcpyAsync(fval_.as<uint64_t>() + P_, val.data(), (size_t)P * 8, hipMemcpyHostToDevice, stream_));
+  }
+  SR_HIP(hipMemcpyAsync(dlen_.as<int32_t>() + rows_, dl, (size_t)n * 4, hipMemcpyHostToDevice, stream_));
+  SR_HIP(hipMemsetAsync(live_.as<uint8_t>() + rows_, 1, (size_t)n, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+  end(stream_);
+  for (int64_t i = 0; i < n; ++i) {
+    dl_host_.push_back(dl[i]);
+    live_host_.push_back(1);
+    sum_dl_ += dl[i];
+  }
+  rows_ += n;
+  live_n_ += n;
+  P_ += P;
+  dirty_ = true;
+  ++version_;
+}
+
+void LexIndex::remove(const int64_t* rows, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    SR_CHECK(rows[i] >= 0 && rows[i] < rows_, "lex.remove: row out of range");
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = rows[i];
+    if (!live_host_[(size_t)r]) continue;
+    live_host_[(size_t)r] = 0;
+    --live_n_;
+    sum_dl_ -= dl_host_[(size_t)r];
+  }
+  DeviceGuard g(device_);
+  begin(stream_);
+  if (rows_) SR_HIP(hipMemcpyAsync(live_.p, live_host_.data(), (size_t)rows_, hipMemcpyHostToDevice, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+  end(stream_);
+  dirty_ = true;
+  ++version_;
+}
+
+void LexIndex::rebuild(hipStream_t s) {
+  if (!dirty_) return;
+  const int64_t T = vocab_;
+  df_host_.assign((size_t)T, 0);
+  nnz_ = 0;
+  off_.reserve((size_t)(T + 1) * 8);
+  if (P_ == 0 || T == 0) {
+    SR_HIP(hipMemsetAsync(off_.p, 0, (size_t)(T + 1) * 8, s));
+    SR_HIP(hipStreamSynchronize(s));
+    dirty_ = false;
+    return;
+  }
+  SR_CHECK(P_ <= (int64_t)0x7fffffff, "lex: more than 2^31 postings per index");
+  const int P = (int)P_;
+  int end_bit = 1;
+  while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)T) ++end_bit;  // keys 0..T
+  DevBuf keys_in, keys_out, df, tmp;
+  keys_in.reserve((size_t)P * 4);
+  keys_out.reserve((size_t)P * 4);
+  post_.reserve((size_t)P * 8);
+  df.reserve((size_t)(T + 1) * 4);
+  SR_HIP(hipMemsetAsync(df.p, 0, (size_t)(T + 1) * 4, s));
+  {
+    ProfScope prof("lex_rebuild_keys", s, 0.0, (double)P * 16.0);
+    hipLaunchKernelGGL(lex_keys_kernel, dim3((unsigned)ceil_div(P, 256)), dim3(256), 0, s,
+                       fterm_.as<int32_t>(), fval_.as<uint64_t>(), live_.as<uint8_t>(), (int64_t)P,
+                       (uint32_t)T, keys_in.as<uint32_t>(), df.as<int>());
+    SR_LAUNCH_CHECK();
+  }
+  size_t tb_sort = 0, tb_scan = 0;
+  SR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, keys_in.as<uint32_t>(),
+                                            keys_out.as<uint32_t>(), fval_.as<uint64_t>(),
+                                            post_.as<uint64_t>(), P, 0, end_bit, s));
+  SR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, df.as<int>(), off_.as<int64_t>(),
+                                          (int)(T + 1), s));
+  tmp.reserve(std::max(tb_sort, tb_scan));
+  {
+    ProfScope prof("lex_rebuild_sort", s, 0.0, (double)P * 24.0);
+    SR_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb_sort, keys_in.as<uint32_t>(),
+                                              keys_out.as<uint32_t>(), fval_.as<uint64_t>(),
+                                              post_.as<uint64_t>(), P, 0, end_bit, s));
+  }
+  SR_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb_scan, df.as<int>(), off_.as<int64_t>(),
+                                          (int)(T + 1), s));
+  SR_HIP(hipMemcpyAsync(df_host_.data(), df.p, (size_t)T * 4, hipMemcpyDeviceToHost, s));
+  SR_HIP(hipMemcpyAsync(&nnz_, off_.as<int64_t>() + T, 8, hipMemcpyDeviceToHost, s));
+  SR_HIP(hipStreamSynchronize(s));
+  off_host_.resize((size_t)T + 1);
+  int64_t acc = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    off_host_[(size_t)t] = acc;
+    acc += df_host_[(size_t)t];
+  }
+  off_host_[(size_t)T] = acc;
+  SR_CHECK(acc == nnz_, "lex: rebuild count mismatch");
+  dirty_ = false;
+}
+
+const uint8_t* LexIndex::eligibility(const uint8_t* allow, int64_t mask_key, hipStream_t s) {
+  if (!allow) return nullptr;  // postings of dead rows are gone after the rebuild
+  if (mask_key == 0 || mask_key != mask_key_ || mask_version_ != version_) {
+    std::vector<uint8_t> m((size_t)std::max<int64_t>(rows_, 1));
+    for (int64_t r = 0; r < rows_; ++r) m[(size_t)r] = (live_host_[(size_t)r] && allow[r]) ? 1 : 0;
+    mask_.reserve(m.size());
+    SR_HIP(hipMemcpyAsync(mask_.p, m.data(), (size_t)rows_, hipMemcpyHostToDevice, s));
+    SR_HIP(hipStreamSynchronize(s));
+    mask_key_ = mask_key;
+    mask_version_ = version_;
+  }
+  return mask_.as<uint8_t>();
+}
+
+float LexIndex::idf(int64_t df) const {
+  // Lucene's BM25 idf (always positive), in double then rounded to fp32 once.
+  const double N = (double)live_n_, d = (double)df;
+  return (float)std::log(1.0 + (N - d + 0.5) / (d + 0.5));
+}
+
+float LexIndex::avgdl() const {
+  return live_n_ > 0 ? (float)((double)sum_dl_ / (double)live_n_) : 1.f;
+}
+
+void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k,
+                          const uint8_t* allow, int64_t mask_key, float* out_score,
+                          int64_t* out_rows, hipStream_t s) {
+  SR_CHECK(B >= 0, "lex.search: negative batch");
+  SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "lex.search: top_k must be in [1, 1024]");
+  if (B == 0) return;
+  SR_CHECK(qoff && qoff[0] == 0, "lex.search: qoff[0] must be 0");
+  DeviceGuard g(device_);
+  begin(s);
+  rebuild(s);
+  const uint8_t* elig = eligibility(allow, mask_key, s);
+  // per query: distinct known terms with multiplicity, and the touched-list capacity
+  struct QT {
+    int32_t term, mult;
+  };
+  std::vector<std::vector<QT>> qt((size_t)B);
+  std::vector<int64_t> cap((size_t)B, 0);
+  for (int b = 0; b < B; ++b) {
+    SR_CHECK(qoff[b + 1] >= qoff[b], "lex.search: qoff must be non-decreasing");
+    std::vector<QT>& v = qt[(size_t)b];
+    for (int64_t p = qoff[b]; p < qoff[b + 1]; ++p) {
+      const int32_t t = qterms[p];
+      if (t < 0 || t >= vocab_ || df_host_[(size_t)t] == 0) continue;
+      bool seen = false;
+      for (auto& e : v)
+        if (e.term == t) {
+          ++e.mult;
+          seen = true;
+        }
+      if (!seen) {
+        v.push_back({t, 1});
+        cap[(size_t)b] += df_host_[(size_t)t];
+      }
+    }
+    cap[(size_t)b] = std::min<int64_t>(cap[(size_t)b], rows_);
+  }
+  // query blocks: the dense accumulator (QB x rows u32) within ~2 GiB
+  const int64_t rows = std::max<int64_t>(rows_, 1);
+  const int QB = (int)std::max<int64_t>(1, std::min<int64_t>(B, ((int64_t)2 << 30) / (rows * 4)));
+  const float adl = avgdl();
+  if (acc_rows_ < rows || acc_q_ < QB) {
+    SR_HIP(hipStreamSynchronize(s));
+    acc_.release();
+    acc_.reserve((size_t)QB * rows * 4);
+    SR_HIP(hipMemsetAsync(acc_.p, 0, (size_t)QB * rows * 4, s));
+    acc_rows_ = rows;
+    acc_q_ = QB;
+  }
+  for (int b0 = 0; b0 < B; b0 += QB) {
+    const int qb = std::min(QB, B - b0);
+    std::vector<int64_t> toff((size_t)qb + 1, 0);
+    for (int i = 0; i < qb; ++i) toff[(size_t)i + 1] = toff[(size_t)i] + cap[(size_t)(b0 + i)];
+    std::vector<LexChunk> ch;
+    for (int i = 0; i < qb; ++i) {
+      for (const QT& e : qt[(size_t)(b0 + i)]) {
+        const int64_t st = off_host_[(size_t)e.term], len = df_host_[(size_t)e.term];
+        const float w = idf(len);
+        for (int64_t c = 0; c < len; c += LEX_CHUNK)
+          ch.push_back({st + c, (int32_t)std::min<int64_t>(LEX_CHUNK, len - c), i, w, e.mult});
+      }
+    }
+    const size_t b_ch = ch.size() * sizeof(LexChunk), b_off = (size_t)(qb + 1) * 8;
+    const size_t b_cnt = (size_t)qb * 4, b_tl = (size_t)std::max<int64_t>(toff[(size_t)qb], 1) * 4;
+    ws_.reserve(b_ch + b_off + b_cnt + b_tl + 64);
+    char* w = ws_.as<char>();
+    LexChunk* d_ch = reinterpret_cast<LexChunk*>(w);
+    int64_t* d_toff = reinterpret_cast<int64_t*>(w + round_up(b_ch, 16));
+    int* d_cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(d_toff) + round_up(b_off, 16));
+    int32_t* d_tl = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d_cnt) + round_up(b_cnt, 16));
+    if (b_ch) SR_HIP(hipMemcpyAsync(d_ch, ch.data(), b_ch, hipMemcpyHostToDevice, s));
+    SR_HIP(hipMemcpyAsync(d_toff, toff.data(), b_off, hipMemcpyHostToDevice, s));
+    SR_HIP(hipMemsetAsync(d_cnt, 0, b_cnt, s));
+    if (!ch.empty()) {
+      ProfScope prof("lex_score", s, 0.0, (double)(toff[(size_t)qb]) * 16.0);
+      hipLaunchKernelGGL(lex_score_kernel, dim3((unsigned)ch.size()), dim3(LEX_THREADS), 0, s, d_ch,
+                         post_.as<uint64_t>(), dlen_.as<int32_t>(), elig, rows, adl, k1_, b_,
+                         acc_.as<uint32_t>(), d_cnt, d_toff, d_tl);
+      SR_LAUNCH_CHECK();
+    }
+    {
+      ProfScope prof("lex_select", s, 0.0, (double)(toff[(size_t)qb]) * 8.0);
+      hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), 0, s, acc_.as<uint32_t>(),
+                         rows, d_cnt, d_toff, d_tl, k, out_score + (int64_t)b0 * k,
+                         out_rows + (int64_t)b0 * k);
+      SR_LAUNCH_CHECK();
+    }
+    // the host vectors above back async copies: finish the block before they go away
+    SR_HIP(hipStreamSynchronize(s));
+  }
+  end(s);
+}
+
+void LexIndex::search_host(const int64_t* qoff, const int32_t* qterms, int B, int k,
+                           const uint8_t* allow, int64_t mask_key, float* out_score,
+                           int64_t* out_rows) {
+  if (B == 0) return;
+  SR_CHECK(out_score && out_rows, "lex.search: null output");
+  DeviceGuard g(device_);
+  const size_t ob = (size_t)B * k;
+  out_.reserve((size_t)round_up((int64_t)ob * 4, 16) + ob * 8);
+  float* ds = out_.as<float>();
+  int64_t* dr = reinterpret_cast<int64_t*>(out_.as<char>() + round_up((int64_t)ob * 4, 16));
+  search_dev(qoff, qterms, B, k, allow, mask_key, ds, dr, stream_);
+  SR_HIP(hipMemcpyAsync(out_score, ds, ob * 4, hipMemcpyDeviceToHost, stream_));
+  SR_HIP(hipMemcpyAsync(out_rows, dr, ob * 8, hipMemcpyDeviceToHost, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+}
+
+void LexIndex::stats(int64_t* rows, int64_t* live, int64_t* postings, int64_t* vocab,
+                     double* avgdl_out) {
+  if (rows) *rows = rows_;
+  if (live) *live = live_n_;
+  if (postings) *postings = P_;
+  if (vocab) *vocab = vocab_;
+  if (avgdl_out) *avgdl_out = live_n_ > 0 ? (double)sum_dl_ / (double)live_n_ : 0.0;
+}
+
+// Download the forward index (row order) to the host.
+void LexIndex::forward(std::vector<int32_t>& fterm, std::vector<uint64_t>& fval) {
+  fterm.resize((size_t)P_);
+  fval.resize((size_t)P_);
+  if (P_) {
+    SR_HIP(hipMemcpyAsync(fterm.data(), fterm_.p, (size_t)P_ * 4, hipMemcpyDeviceToHost, stream_));
+    SR_HIP(hipMemcpyAsync(fval.data(), fval_.p, (size_t)P_ * 8, hipMemcpyDeviceToHost, stream_));
+  }
+  SR_HIP(hipStreamSynchronize(stream_));
+}
+
+// Snapshot (little endian): "SRMILEX1", float k1, float b, int64 rows, int64 P,
+// rows x int32 dl, rows x u8 live, P x int32 term, P x u64 (row << 32 | tf).
+void LexIndex::save(const char* path) {
+  DeviceGuard g(device_);
+  begin(stream_);
+  std::vector<int32_t> ft;
+  std::vector<uint64_t> fv;
+  forward(ft, fv);
+  end(stream_);
+  std::string tmp = std::string(path) + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) throw Error(SR_ERR_IO, std::string("lex.save: cannot open ") + path);
+  bool ok = std::fwrite("SRMILEX1", 1, 8, f) == 8;
+  ok = ok && std::fwrite(&k1_, 4, 1, f) == 1 && std::fwrite(&b_, 4, 1, f) == 1;
+  ok = ok && std::fwrite(&rows_, 8, 1, f) == 1 && std::fwrite(&P_, 8, 1, f) == 1;
+  ok = ok && (rows_ == 0 || std::fwrite(dl_host_.data(), 4, (size_t)rows_, f) == (size_t)rows_);
+  ok = ok && (rows_ == 0 || std::fwrite(live_host_.data(), 1, (size_t)rows_, f) == (size_t)rows_);
+  ok = ok && (P_ == 0 || std::fwrite(ft.data(), 4, (size_t)P_, f) == (size_t)P_);
+  ok = ok && (P_ == 0 || std::fwrite(fv.data(), 8, (size_t)P_, f) == (size_t)P_);
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok || std::rename(tmp.c_str(), path) != 0)
+    throw Error(SR_ERR_IO, std::string("lex.save: write failed for ") + path);
+}
+
+LexIndex* LexIndex::load(const char* path, int device) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) throw Error(SR_ERR_IO, std::string("lex.load: cannot open ") + path);
+  char magic[8];
+  float k1 = 0.f, b = 0.f;
+  int64_t rows = -1, P = -1;
+  bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "SRMILEX1", 8) == 0;
+  ok = ok && std::fread(&k1, 4, 1, f) == 1 && std::fread(&b, 4, 1, f) == 1;
+  ok = ok && std::fread(&rows, 8, 1, f) == 1 && std::fread(&P, 8, 1, f) == 1 && rows >= 0 && P >= 0;
+  std::vector<int32_t> dl, ft;
+  std::vector<uint8_t> live;
+  std::vector<uint64_t> fv;
+  if (ok) {
+    dl.resize((size_t)rows);
+    live.resize((size_t)rows);
+    ft.resize((size_t)P);
+    fv.resize((size_t)P);
+    ok = (rows == 0 || std::fread(dl.data(), 4, (size_t)rows, f) == (size_t)rows) &&
+         (rows == 0 || std::fread(live.data(), 1, (size_t)rows, f) == (size_t)rows) &&
+         (P == 0 || std::fread(ft.data(), 4, (size_t)P, f) == (size_t)P) &&
+         (P == 0 || std::fread(fv.data(), 8, (size_t)P, f) == (size_t)P);
+  }
+  std::fclose(f);
+  if (!ok) throw Error(SR_ERR_IO, std::string("lex.load: not a valid lexical snapshot: ") + path);
+  LexIndex* x = new LexIndex(device, k1, b);
+  try {
+    x->load_rows(dl, live, ft, fv);
+  } catch (...) {
+    delete x;
+    throw;
+  }
+  return x;
+}
+
+// Replace the contents with a row-ordered forward index (load / compact).
+void LexIndex::load_rows(const std::vector<int32_t>& dl, const std::vector<uint8_t>& live,
+                         const std::vector<int32_t>& ft, const std::vector<uint64_t>& fv) {
+  const int64_t rows = (int64_t)dl.size(), P = (int64_t)ft.size();
+  DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
+  fterm_.release();
+  fval_.release();
+  dlen_.release();
+  live_.release();
+  fterm_.reserve((size_t)std::max<int64_t>(P, 1) * 4);
+  fval_.reserve((size_t)std::max<int64_t>(P, 1) * 8);
+  dlen_.reserve((size_t)std::max<int64_t>(rows, 1) * 4);
+  live_.reserve((size_t)std::max<int64_t>(rows, 1));
+  if (P) {
+    SR_HIP(hipMemcpyAsync(fterm_.p, ft.data(), (size_t)P * 4, hipMemcpyHostToDevice, stream_));
+    SR_HIP(hipMemcpyAsync(fval_.p, fv.data(), (size_t)P * 8, hipMemcpyHostToDevice, stream_));
+  }
+  if (rows) {
+    SR_HIP(hipMemcpyAsync(dlen_.p, dl.data(), (size_t)rows * 4, hipMemcpyHostToDevice, stream_));
+    SR_HIP(hipMemcpyAsync(live_.p, live.data(), (size_t)rows, hipMemcpyHostToDevice, stream_));
+  }
+  SR_HIP(hipStreamSynchronize(stream_));
+  end(stream_);
+  rows_ = rows;
+  P_ = P;
+  dl_host_ = dl;
+  live_host_ = live;
+  live_n_ = 0;
+  sum_dl_ = 0;
+  vocab_ = 0;
+  for (int64_t r = 0; r < rows; ++r)
+    if (live[(size_t)r]) {
+      ++live_n_;
+      sum_dl_ += dl[(size_t)r];
+    }
+  for (int32_t t : ft) vocab_ = std::max<int64_t>(vocab_, (int64_t)t + 1);
+  acc_rows_ = 0;  // the accumulator is re-sized (and zeroed) at the next search
+  dirty_ = true;
+  ++version_;
+}
+
+void LexIndex::compact(int64_t* old_to_new) {
+  DeviceGuard g(device_);
+  begin(stream_);
+  std::vector<int32_t> ft;
+  std::vector<uint64_t> fv;
+  forward(ft, fv);
+  end(stream_);
+  std::vector<int64_t> remap((size_t)rows_, -1);
+  int64_t n = 0;
+  for (int64_t r = 0; r < rows_; ++r)
+    if (live_host_[(size_t)r]) remap[(size_t)r] = n++;
+  if (old_to_new)
+    for (int64_t r = 0; r < rows_; ++r) old_to_new[r] = remap[(size_t)r];
+  std::vector<int32_t> dl((size_t)n), ft2;
+  std::vector<uint8_t> live((size_t)n, 1);
+  std::vector<uint64_t> fv2;
+  for (int64_t r = 0; r < rows_; ++r)
+    if (remap[(size_t)r] >= 0) dl[(size_t)remap[(size_t)r]] = dl_host_[(size_t)r];
+  for (int64_t p = 0; p < P_; ++p) {
+    const int64_t r = (int64_t)(fv[(size_t)p] >> 32), nr = remap[(size_t)r];
+    if (nr < 0) continue;
+    ft2.push_back(ft[(size_t)p]);
+    fv2.push_back(((uint64_t)nr << 32) | (fv[(size_t)p] & 0xffffffffull));
+  }
+  load_rows(dl, live, ft2, fv2);
+}
+
+}  // namespace sr

@@ -114,4 +114,9 @@ void launch_build_pairs(const int32_t* q_tok, const int32_t* q_len, int lq_max,
 void launch_rerank_select(const float* logits, int B, int K, int k_out, int32_t* out_index,
                           hipStream_t s);
 
+// k_lex.hip — reciprocal-rank fusion of two ranked row lists per query (-1 padded), fp64 scores.
+void launch_rrf_fuse(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
+                     int rank_const, double min_score, int k_out, double* out_score,
+                     int64_t* out_rows, hipStream_t s);
+
 }  // namespace sr

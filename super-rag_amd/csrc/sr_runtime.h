@@ -71,6 +71,8 @@ class Store {
                    const uint8_t* allow = nullptr, int64_t mask_key = 0);
   void search_dev(const void* q, int q_dtype, int B, int k, float* out_sim, int64_t* out_rows,
                   int64_t row_offset, hipStream_t s, const uint8_t* elig = nullptr);
+  // device eligibility mask live & allow (cached per mask_key and store version); null for null
+  const uint8_t* eligibility(const uint8_t* allow, int64_t mask_key);
   void save(const char* path);
   static Store* load(const char* path, int device);
   void compact(int64_t* old_to_new);
@@ -157,6 +159,59 @@ class Encoder {
   DevBuf statA_, statB_, mrA_, mrB_;  // per-row LayerNorm partials / (mu, rstd) (folded path)
   bool fold_ready_ = false;  // folded weights match the current weights
   int64_t ws_tokens_ = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
+// BM25 lexical index over the rows of a store (k_lex.hip).
+class LexIndex {
+ public:
+  LexIndex(int device, float k1, float b);
+  ~LexIndex();
+
+  // n documents: terms[off[i] .. off[i+1]) distinct term ids with frequencies tf, length dl[i]
+  void add(const int64_t* off, const int32_t* terms, const int32_t* tf, const int32_t* dl,
+           int64_t n, int64_t* first_row);
+  void remove(const int64_t* rows, int64_t n);
+  void compact(int64_t* old_to_new);
+  // query b: terms qterms[qoff[b] .. qoff[b+1]) (repeats count); outputs on the device (search_dev,
+  // on stream s) or the host
+  void search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
+                  int64_t mask_key, float* out_score, int64_t* out_rows, hipStream_t s);
+  void search_host(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
+                   int64_t mask_key, float* out_score, int64_t* out_rows);
+  void stats(int64_t* rows, int64_t* live, int64_t* postings, int64_t* vocab, double* avgdl);
+  void save(const char* path);
+  static LexIndex* load(const char* path, int device);
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }
+  void begin(hipStream_t s) { SR_HIP(hipStreamWaitEvent(s, done_, 0)); }
+  void end(hipStream_t s) { SR_HIP(hipEventRecord(done_, s)); }
+
+  std::mutex mu;
+
+ private:
+  void rebuild(hipStream_t s);
+  const uint8_t* eligibility(const uint8_t* allow, int64_t mask_key, hipStream_t s);
+  float idf(int64_t df) const;
+  float avgdl() const;
+  void forward(std::vector<int32_t>& fterm, std::vector<uint64_t>& fval);
+  void load_rows(const std::vector<int32_t>& dl, const std::vector<uint8_t>& live,
+                 const std::vector<int32_t>& ft, const std::vector<uint64_t>& fv);
+
+  int device_;
+  float k1_, b_;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t done_ = nullptr;
+  int64_t rows_ = 0, live_n_ = 0, P_ = 0, vocab_ = 0, nnz_ = 0, sum_dl_ = 0;
+  bool dirty_ = true;
+  // device: forward index, per-row data, inverted index, workspaces
+  DevBuf fterm_, fval_, dlen_, live_, off_, post_, acc_, ws_, out_, mask_;
+  int64_t acc_rows_ = 0, acc_q_ = 0;
+  // host mirrors
+  std::vector<int32_t> dl_host_, df_host_;
+  std::vector<uint8_t> live_host_;
+  std::vector<int64_t> off_host_;
+  int64_t version_ = 0, mask_key_ = 0, mask_version_ = -1;
 };
 
 }  // namespace sr

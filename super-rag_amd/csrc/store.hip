@@ -245,28 +245,30 @@ void Store::search_dev(const void* q, int q_dtype, int B, int k, float* out_sim,
   }
 }
 
+const uint8_t* Store::eligibility(const uint8_t* allow, int64_t mask_key) {
+  if (!allow) return nullptr;
+  // eligibility = live & allow, uploaded once per (mask_key, store version)
+  if (mask_key == 0 || mask_key != mask_key_ || mask_version_ != version_ || mask_rows_ != n_rows_) {
+    std::vector<uint8_t> m((size_t)std::max<int64_t>(n_rows_, 1));
+    for (int64_t r = 0; r < n_rows_; ++r) m[(size_t)r] = (live_host_[(size_t)r] && allow[r]) ? 1 : 0;
+    mask_.reserve(m.size());
+    begin(stream_);
+    SR_HIP(hipMemcpyAsync(mask_.p, m.data(), (size_t)n_rows_, hipMemcpyHostToDevice, stream_));
+    SR_HIP(hipStreamSynchronize(stream_));
+    end(stream_);
+    mask_key_ = mask_key;
+    mask_version_ = version_;
+    mask_rows_ = n_rows_;
+  }
+  return mask_.as<uint8_t>();
+}
+
 void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows,
                         const uint8_t* allow, int64_t mask_key) {
   SR_CHECK(B >= 0 && (B == 0 || (q && out_dist && out_rows)), "store.search: null buffer");
   if (B == 0) return;
   DeviceGuard g(device_);
-  const uint8_t* elig = nullptr;
-  if (allow) {
-    // eligibility = live & allow, uploaded once per (mask_key, store version)
-    if (mask_key == 0 || mask_key != mask_key_ || mask_version_ != version_ || mask_rows_ != n_rows_) {
-      std::vector<uint8_t> m((size_t)std::max<int64_t>(n_rows_, 1));
-      for (int64_t r = 0; r < n_rows_; ++r) m[(size_t)r] = (live_host_[(size_t)r] && allow[r]) ? 1 : 0;
-      mask_.reserve(m.size());
-      begin(stream_);
-      SR_HIP(hipMemcpyAsync(mask_.p, m.data(), (size_t)n_rows_, hipMemcpyHostToDevice, stream_));
-      SR_HIP(hipStreamSynchronize(stream_));
-      end(stream_);
-      mask_key_ = mask_key;
-      mask_version_ = version_;
-      mask_rows_ = n_rows_;
-    }
-    elig = mask_.as<uint8_t>();
-  }
+  const uint8_t* elig = eligibility(allow, mask_key);
   const size_t qb = (size_t)B * dim_ * sizeof(float);
   const size_t ob = (size_t)B * k * (sizeof(float) + sizeof(int64_t));
   qstage_.reserve(qb + ob);

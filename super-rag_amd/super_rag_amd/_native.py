@@ -78,6 +78,20 @@ SIGNATURES = {
     "sr_store_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
     "sr_store_compact": (c_int, [c_void_p, c_void_p]),
     "sr_store_destroy": (None, [c_void_p]),
+    "sr_lex_create": (c_int, [c_int, c_float, c_float, POINTER(c_void_p)]),
+    "sr_lex_add": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, P_I64]),
+    "sr_lex_remove": (c_int, [c_void_p, c_void_p, c_int64]),
+    "sr_lex_stats": (c_int, [c_void_p, P_I64, P_I64, P_I64, P_I64, POINTER(c_double)]),
+    "sr_lex_search": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64,
+                              c_void_p, c_void_p]),
+    "sr_lex_save": (c_int, [c_void_p, c_char_p]),
+    "sr_lex_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
+    "sr_lex_compact": (c_int, [c_void_p, c_void_p]),
+    "sr_lex_destroy": (None, [c_void_p]),
+    "sr_rrf_fuse": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_double, c_int,
+                            c_void_p, c_void_p, c_int]),
+    "sr_hybrid_search": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                 c_int, c_int, c_double, c_void_p, c_int64, c_void_p, c_void_p]),
     "sr_topk_merge_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                   c_void_p, c_int, c_void_p]),
     "sr_encoder_create": (c_int, [POINTER(EncoderConfigC), c_int, POINTER(c_void_p)]),
@@ -119,6 +133,14 @@ def load() -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
+        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7.  If this
+        # library is loaded first, the dynamic loader binds /opt/rocm's copy and a later
+        # torch.cuda init fails with "No HIP GPUs are available" (measured on the MI355X box);
+        # importing torch first makes both bind the same, already-loaded runtime.
+        try:
+            import torch  # noqa: F401
+        except Exception:  # noqa: BLE001 - torch is optional for the host-buffer entry points
+            pass
         path = library_path()
         if not os.path.exists(path):
             raise NativeUnavailableError(

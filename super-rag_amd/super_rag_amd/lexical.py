@@ -1,0 +1,220 @@
+"""Lexical (BM25) retrieval and dense + lexical hybrid fusion: host side of sr_lex_* /
+sr_rrf_fuse / sr_hybrid_search (include/super_rag_mi355x.h).
+
+The reference declares the pieces but ships no backend: a ``fulltext_search`` node type and
+``FulltextSearchParams{topk, keywords}`` (schema/view_models.py:276-283, :1043-1047), a
+``fulltext_search_docs`` merge slot (nodeflow/runners/merge.py:18-20) and a
+``enable_vector_and_fulltext`` collection flag.  Here:
+
+  * ``analyze(text)``: lower-case, Unicode ``\\w+`` tokens (no stemming, no stop words);
+  * ``Vocab``: term -> int32 id per collection (persisted with the collection snapshot);
+  * ``NativeLexIndex``: the device BM25 index (k_lex.hip): Okapi BM25, k1 = 1.2, b = 0.75, Lucene's
+    idf ln(1 + (N - df + 0.5) / (df + 0.5)) over live rows, scores in 2^-16 fixed point;
+  * ``rrf_fuse`` / ``hybrid_search``: reciprocal-rank fusion as graphiti's ``rrf``
+    (graphiti_core/search/search_utils.py:1762-1778), on the device.
+There is no CPU fallback: every entry point needs the HIP library and a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+from collections import Counter
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+_TOKEN = re.compile(r"\w+", re.UNICODE)
+K1 = 1.2
+B = 0.75
+
+
+def analyze(text: Optional[str]) -> List[str]:
+    """Text -> lexical tokens (lower-cased Unicode word characters)."""
+    return _TOKEN.findall(text.lower()) if text else []
+
+
+class Vocab:
+    """Term string <-> dense int32 id."""
+
+    def __init__(self, terms: Iterable[str] = ()):
+        self.terms: List[str] = []
+        self.ids: Dict[str, int] = {}
+        for t in terms:
+            self.ids.setdefault(t, len(self.terms))
+            if len(self.ids) > len(self.terms):
+                self.terms.append(t)
+
+    def __len__(self) -> int:
+        return len(self.terms)
+
+    def doc_ids(self, tokens: Sequence[str]) -> List[int]:
+        """Ids of a document's tokens, adding new terms."""
+        out = []
+        for t in tokens:
+            i = self.ids.get(t)
+            if i is None:
+                i = self.ids[t] = len(self.terms)
+                self.terms.append(t)
+            out.append(i)
+        return out
+
+    def query_ids(self, tokens: Sequence[str]) -> List[int]:
+        """Ids of a query's tokens; unknown terms are dropped (they match no row)."""
+        return [self.ids[t] for t in tokens if t in self.ids]
+
+
+def doc_arrays(docs: Sequence[Sequence[int]]):
+    """Token-id lists -> (off int64[n+1], terms int32, tf int32, dl int32): each document's distinct
+    terms in first-occurrence order with their counts; dl = token count."""
+    off = np.zeros(len(docs) + 1, dtype=np.int64)
+    terms: List[int] = []
+    tfs: List[int] = []
+    dl = np.empty(len(docs), dtype=np.int32)
+    for i, d in enumerate(docs):
+        c = Counter(d)
+        terms.extend(c.keys())
+        tfs.extend(c.values())
+        off[i + 1] = len(terms)
+        dl[i] = len(d)
+    return off, np.asarray(terms, dtype=np.int32), np.asarray(tfs, dtype=np.int32), dl
+
+
+def query_arrays(queries: Sequence[Sequence[int]]):
+    qoff = np.zeros(len(queries) + 1, dtype=np.int64)
+    flat: List[int] = []
+    for i, q in enumerate(queries):
+        flat.extend(int(t) for t in q)
+        qoff[i + 1] = len(flat)
+    qterms = np.asarray(flat if flat else [0], dtype=np.int32)
+    return qoff, qterms
+
+
+def _mask(allow, n_rows: int):
+    a = np.ascontiguousarray(np.asarray(allow, dtype=np.uint8))
+    if a.shape != (n_rows,):
+        raise ValueError(f"allow mask must have {n_rows} entries, got {a.shape}")
+    return a if n_rows else np.zeros(1, dtype=np.uint8)
+
+
+class NativeLexIndex:
+    """BM25 index over the rows of a store, resident in HBM of one device."""
+
+    def __init__(self, device: int = 0, k1: float = K1, b: float = B, _handle=None):
+        self._h = None
+        if _handle is None:
+            N.require_gpu()
+            h = ctypes.c_void_p()
+            N.call("sr_lex_create", int(device), float(k1), float(b), ctypes.byref(h))
+            _handle = h
+        self._h = _handle
+        self.device = int(device)
+
+    @classmethod
+    def load(cls, path: str, device: int = 0) -> "NativeLexIndex":
+        N.require_gpu()
+        h = ctypes.c_void_p()
+        N.call("sr_lex_load", path.encode(), int(device), ctypes.byref(h))
+        return cls(device, _handle=h)
+
+    def close(self) -> None:
+        if self._h:
+            N.load().sr_lex_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, docs: Sequence[Sequence[int]]) -> int:
+        """Append documents (token-id lists); returns the first row id."""
+        if not len(docs):
+            return self.stats()["rows"]
+        off, terms, tf, dl = doc_arrays(docs)
+        if terms.size == 0:
+            terms = np.zeros(1, dtype=np.int32)
+            tf = np.ones(1, dtype=np.int32)
+        first = ctypes.c_int64(0)
+        N.call("sr_lex_add", self._h, N.ptr(off), N.ptr(terms), N.ptr(tf), N.ptr(dl), len(docs),
+               ctypes.byref(first))
+        return int(first.value)
+
+    def remove(self, rows) -> None:
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int64))
+        N.call("sr_lex_remove", self._h, N.ptr(r), r.shape[0])
+
+    def compact(self) -> np.ndarray:
+        n = self.stats()["rows"]
+        m = np.empty(max(n, 1), dtype=np.int64)
+        N.call("sr_lex_compact", self._h, N.ptr(m))
+        return m[:n]
+
+    def save(self, path: str) -> None:
+        N.call("sr_lex_save", self._h, path.encode())
+
+    def stats(self) -> dict:
+        v = [ctypes.c_int64(0) for _ in range(4)]
+        a = ctypes.c_double(0.0)
+        N.call("sr_lex_stats", self._h, *[ctypes.byref(x) for x in v], ctypes.byref(a))
+        return {"rows": v[0].value, "live": v[1].value, "postings": v[2].value,
+                "vocab": v[3].value, "avgdl": a.value}
+
+    def search(self, queries: Sequence[Sequence[int]], k: int, allow=None, mask_key: int = 0):
+        """BM25 top-k per query (token-id lists) -> (score [B,k] fp32 desc, rows [B,k] int64)."""
+        Bq = len(queries)
+        scores = np.empty((Bq, k), dtype=np.float32)
+        rows = np.empty((Bq, k), dtype=np.int64)
+        if Bq == 0:
+            return scores, rows
+        qoff, qterms = query_arrays(queries)
+        a = None if allow is None else _mask(allow, self.stats()["rows"])
+        N.call("sr_lex_search", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+               None if a is None else N.ptr(a), int(mask_key), N.ptr(scores), N.ptr(rows))
+        return scores, rows
+
+    def hybrid(self, store, queries, query_terms, k: int, k_each: Optional[int] = None,
+               rank_const: int = 1, min_score: float = float("-inf"), allow=None, mask_key: int = 0):
+        """hybrid_search over (store, this index)."""
+        return hybrid_search(store, self, queries, query_terms, k, k_each, rank_const, min_score,
+                             allow, mask_key)
+
+
+def rrf_fuse(rows_a, rows_b, k: int, rank_const: int = 1, min_score: float = 0.0,
+             device: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """Device rrf of two ranked row lists per query ([B, ka], [B, kb], -1 padded)."""
+    N.require_gpu()
+    a = np.ascontiguousarray(np.asarray(rows_a, dtype=np.int64))
+    b = np.ascontiguousarray(np.asarray(rows_b, dtype=np.int64))
+    Bq = a.shape[0]
+    assert b.shape[0] == Bq
+    scores = np.empty((Bq, k), dtype=np.float64)
+    rows = np.empty((Bq, k), dtype=np.int64)
+    N.call("sr_rrf_fuse", N.ptr(a), a.shape[1], N.ptr(b), b.shape[1], Bq, int(rank_const),
+           float(min_score), int(k), N.ptr(scores), N.ptr(rows), int(device))
+    return scores, rows
+
+
+def hybrid_search(store, lex: NativeLexIndex, queries, query_terms: Sequence[Sequence[int]], k: int,
+                  k_each: Optional[int] = None, rank_const: int = 1,
+                  min_score: float = float("-inf"), allow=None, mask_key: int = 0):
+    """Dense top-k_each (cosine, store) and BM25 top-k_each (lex) fused by rrf on the device ->
+    (rrf score [B,k] fp64 desc, rows [B,k] int64)."""
+    q = np.ascontiguousarray(np.asarray(queries, dtype=np.float32))
+    if q.ndim == 1:
+        q = q[None]
+    Bq = q.shape[0]
+    assert len(query_terms) == Bq
+    k_each = int(k_each or k)
+    scores = np.empty((Bq, k), dtype=np.float64)
+    rows = np.empty((Bq, k), dtype=np.int64)
+    if Bq == 0:
+        return scores, rows
+    qoff, qterms = query_arrays(query_terms)
+    a = None if allow is None else _mask(allow, store.count()[0])
+    N.call("sr_hybrid_search", store._h, lex._h, N.ptr(q), N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+           k_each, int(rank_const), float(min_score), None if a is None else N.ptr(a),
+           int(mask_key), N.ptr(scores), N.ptr(rows))
+    return scores, rows

@@ -13,6 +13,11 @@ Runner behaviour mirrors the reference:
   * rerank (nodeflow/runners/rerank.py:21-202): service rerank when configured, else / on any
     error the fallback order (graph results first, then score descending).
   * merge (nodeflow/runners/merge.py:12-65): union of the five lists, dedupe by exact text.
+  * fulltext_search: the reference declares the node type (schema/view_models.py:276-283,
+    FulltextSearchParams{topk, keywords} at :1043-1047) and the merge slot fulltext_search_docs
+    (merge.py:18-20) but registers no runner; this one answers it with the device BM25 index
+    (lexical.py; collections indexed with VECTOR_DB_CONTEXT {"fulltext": true}), tagging
+    metadata.recall_type = "fulltext_search" and degrading every error to [] like vector_search.
 Outside a super_rag deployment a minimal local registry with the same decorator and SystemInput
 is used, so the pack can be exercised standalone (tests/test_boundary.py).
 """
@@ -74,6 +79,17 @@ class VectorSearchInput(BaseModel):
 
 
 class VectorSearchOutput(BaseModel):
+    docs: List[DocumentWithScore]
+
+
+class FulltextSearchInput(BaseModel):
+    top_k: int = Field(5, description="Number of top results to return")
+    keywords: Optional[List[str]] = Field(None, description="Custom keywords to use for fulltext search")
+    collection_ids: Optional[List[str]] = Field(default_factory=list, description="Collection IDs")
+    chat_id: Optional[str] = Field(None, description="Chat ID to filter chat documents")
+
+
+class FulltextSearchOutput(BaseModel):
     docs: List[DocumentWithScore]
 
 
@@ -226,6 +242,38 @@ class VectorSearchNodeRunner(BaseNodeRunner):
         return VectorSearchOutput(docs=docs), {}
 
 
+class FulltextSearchNodeRunner(BaseNodeRunner):
+    def __init__(self):
+        self.repository = VectorSearchRepository()
+
+    async def run(self, ui: FulltextSearchInput, si) -> Tuple[FulltextSearchOutput, dict]:
+        from .vectorstore import MI355XVectorStoreConnector
+        collection_ids = ui.collection_ids or getattr(si, "collection_ids", [])
+        chat_id = ui.chat_id or getattr(si, "chat_id", None)
+        collection = None
+        if collection_ids:
+            collection = await self.repository.get_collection(si.user, collection_ids[0])
+        if not collection:
+            return FulltextSearchOutput(docs=[]), {}
+        try:
+            ctx = vector_db_context()
+            ctx["collection"] = collection_name_for(collection.id)
+            conn = MI355XVectorStoreConnector(ctx)
+            # the chat filter of the vector path (context/context.py:74-111; applied with
+            # ctx["honor_filter"]); the rows are the vector rows, so no indexer clause
+            flt = {"chat_id": chat_id} if chat_id else None
+            docs = await asyncio.to_thread(conn.fulltext_search, si.query, ui.top_k, ui.keywords,
+                                           filter=flt)
+            for item in docs:
+                if item.metadata is None:
+                    item.metadata = {}
+                item.metadata["recall_type"] = "fulltext_search"
+            return FulltextSearchOutput(docs=docs), {}
+        except Exception as e:  # noqa: BLE001 - degrade to [] like vector_search
+            logger.error("Fulltext search failed for collection %s: %s", collection.id, e)
+            return FulltextSearchOutput(docs=[]), {}
+
+
 class RerankNodeRunner(BaseNodeRunner):
     async def run(self, ui: RerankInput, si) -> Tuple[RerankOutput, dict]:
         docs = ui.docs
@@ -285,5 +333,7 @@ def register(include_merge: bool = False) -> None:
     register_node_runner("vector_search", input_model=VectorSearchInput,
                          output_model=VectorSearchOutput)(VectorSearchNodeRunner)
     register_node_runner("rerank", input_model=RerankInput, output_model=RerankOutput)(RerankNodeRunner)
+    register_node_runner("fulltext_search", input_model=FulltextSearchInput,
+                         output_model=FulltextSearchOutput)(FulltextSearchNodeRunner)
     if include_merge or not HOST_NODEFLOW:
         register_node_runner("merge", input_model=MergeInput, output_model=MergeOutput)(MergeNodeRunner)

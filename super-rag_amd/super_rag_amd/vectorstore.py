@@ -9,6 +9,10 @@ Mirrors SeekDBVectorStoreConnector (super_rag/vectorstore/seekdb_connector.py:31
   * ``search(QueryWithEmbedding, **kw) -> QueryResult`` with ``score = cosine distance``
     ascending and no ids in the documents (:98-155); the extra kwargs the reference passes
     (limit, score_threshold, filter, search_params, ...) are accepted and ignored, as there.
+Opt-in lexical retrieval (ctx ``fulltext``): every added node's text is also indexed for BM25 on
+the device (lexical.py, k_lex.hip); ``fulltext_search(text, top_k, keywords)`` backs the
+reference's ``fulltext_search`` node type, and ctx ``hybrid`` makes ``search`` fuse the dense and
+the BM25 rankings by reciprocal rank on the device (score = rrf score, descending).
 Collections are process-wide (like a server): every connector object for the same collection
 name sees the same rows.  Row ids <-> uuid strings, texts and metadata live on the host; vectors
 live in HBM.  With ``ctx["snapshot_dir"]`` a collection is reloaded at construction and
@@ -43,8 +47,20 @@ def _native_load(path: str, device: int):
     return NativeStore.load(path, device=device)
 
 
+def _native_lex(device: int):
+    from .lexical import NativeLexIndex
+    return NativeLexIndex(device)
+
+
+def _native_lex_load(path: str, device: int):
+    from .lexical import NativeLexIndex
+    return NativeLexIndex.load(path, device)
+
+
 _store_factory: Callable = _native_store
 _store_loader: Callable = _native_load
+_lex_factory: Callable = _native_lex
+_lex_loader: Callable = _native_lex_load
 
 
 def set_store_backend(factory: Callable, loader: Callable | None = None) -> None:
@@ -52,6 +68,13 @@ def set_store_backend(factory: Callable, loader: Callable | None = None) -> None
     global _store_factory, _store_loader
     _store_factory = factory
     _store_loader = loader or _native_load
+
+
+def set_lex_backend(factory: Callable, loader: Callable | None = None) -> None:
+    """Test seam: replace how per-collection lexical indexes are created / loaded."""
+    global _lex_factory, _lex_loader
+    _lex_factory = factory
+    _lex_loader = loader or _native_lex_load
 
 
 class _Collection:
@@ -68,14 +91,34 @@ class _Collection:
         self.coalescer = None   # created on first coalesced search (coalesce.py)
         self.version = 0        # bumped on every add / delete / compaction
         self.masks: Dict[str, tuple] = {}   # filter -> (version, mask_key, allow mask)
+        self.lex = None         # BM25 index over the same rows (ctx "fulltext"), lexical.py
+        self.vocab = None
+
+    def ensure_lex(self) -> None:
+        """Create the lexical index, back-filling the rows added before it existed."""
+        if self.lex is not None:
+            return
+        from .lexical import Vocab, analyze
+        vocab = Vocab()
+        lex = _lex_factory(self.device)
+        if self.ids:
+            lex.add([vocab.doc_ids(analyze(t)) if t is not None else [] for t in self.texts])
+            dead = [r for r, u in enumerate(self.ids) if u is None]
+            if dead:
+                lex.remove(np.asarray(dead, dtype=np.int64))
+        self.lex, self.vocab = lex, vocab
 
     def snapshot(self, directory: str) -> None:
         os.makedirs(directory, exist_ok=True)
         base = os.path.join(directory, self.name)
         self.store.save(base + ".srmi")
+        meta = {"dim": self.dim, "ids": self.ids, "texts": self.texts,
+                "metadatas": self.metadatas}
+        if self.lex is not None:
+            self.lex.save(base + ".srlex")
+            meta["lex_vocab"] = self.vocab.terms
         with open(base + ".json.tmp", "w", encoding="utf-8") as f:
-            json.dump({"dim": self.dim, "ids": self.ids, "texts": self.texts,
-                       "metadatas": self.metadatas}, f)
+            json.dump(meta, f)
         os.replace(base + ".json.tmp", base + ".json")
 
     @classmethod
@@ -90,6 +133,10 @@ class _Collection:
         c.texts = meta["texts"]
         c.metadatas = meta["metadatas"]
         c.row_of = {u: i for i, u in enumerate(c.ids) if u is not None}
+        if "lex_vocab" in meta and os.path.exists(base + ".srlex"):
+            from .lexical import Vocab
+            c.lex = _lex_loader(base + ".srlex", device)
+            c.vocab = Vocab(meta["lex_vocab"])
         return c
 
 
@@ -120,6 +167,11 @@ class MI355XVectorStoreConnector:
         self.honor_score_threshold = bool(ctx.get("honor_score_threshold", False))
         self.honor_filter = bool(ctx.get("honor_filter", False))
         self.compact_ratio = float(ctx.get("compact_ratio", 0.5))
+        # opt-in lexical retrieval: BM25 index of the node texts; hybrid = rrf-fused search
+        self.hybrid = bool(ctx.get("hybrid", False))
+        self.fulltext = bool(ctx.get("fulltext", False)) or self.hybrid
+        self.hybrid_k_each = ctx.get("hybrid_k_each")
+        self.rrf_rank_const = int(ctx.get("rrf_rank_const", 1))
         self.store = self
         if self.snapshot_dir and _get(self.collection_name) is None:
             c = _Collection.restore(self.collection_name, self.snapshot_dir, self.device)
@@ -149,7 +201,7 @@ class MI355XVectorStoreConnector:
         if c is not None and hasattr(c.store, "close"):
             c.store.close()
         if self.snapshot_dir:
-            for ext in (".srmi", ".json"):
+            for ext in (".srmi", ".json", ".srlex"):
                 p = os.path.join(self.snapshot_dir, self.collection_name + ext)
                 if os.path.exists(p):
                     os.remove(p)
@@ -170,7 +222,13 @@ class MI355XVectorStoreConnector:
             raise ValueError(f"embedding dimension {vecs.shape[1]} != collection dimension {c.dim}")
         ids = [str(uuid.uuid4()) for _ in nodes]
         with c.lock:
+            if self.fulltext:
+                c.ensure_lex()
             rows = c.store.add(vecs)
+            if c.lex is not None:
+                from .lexical import analyze
+                first = c.lex.add([c.vocab.doc_ids(analyze(n.text)) for n in nodes])
+                assert first == int(rows[0]), "lexical index out of step with the store"
             for u, r, n in zip(ids, rows, nodes):
                 assert int(r) == len(c.ids)
                 c.ids.append(u)
@@ -193,6 +251,8 @@ class MI355XVectorStoreConnector:
             rows = [c.row_of.pop(u) for u in ids if u in c.row_of]
             if rows:
                 c.store.remove(np.asarray(rows, dtype=np.int64))
+                if c.lex is not None:
+                    c.lex.remove(np.asarray(rows, dtype=np.int64))
                 for r in rows:
                     c.ids[r] = None
                     c.texts[r] = None
@@ -205,6 +265,9 @@ class MI355XVectorStoreConnector:
 
     def _compact(self, c: _Collection) -> None:
         remap = c.store.compact()
+        if c.lex is not None:
+            lremap = c.lex.compact()
+            assert np.array_equal(np.asarray(lremap), np.asarray(remap)), "lexical remap differs"
         keep = [i for i, r in enumerate(remap) if r >= 0]
         c.ids = [c.ids[i] for i in keep]
         c.texts = [c.texts[i] for i in keep]
@@ -219,6 +282,10 @@ class MI355XVectorStoreConnector:
         q = np.asarray(query.embedding, dtype=np.float32)
         flt = kwargs.get("filter") if self.honor_filter else None
         thr = kwargs.get("score_threshold") if self.honor_score_threshold else None
+        if self.hybrid:
+            # rrf of the dense and the BM25 rankings on the device; score = rrf score (desc)
+            return QueryResult(query=query.query,
+                               results=self._hybrid(c, q, query.query or "", int(query.top_k), flt))
         if self.coalesce:
             # concurrent single-query searches share one device batch (coalesce.py)
             if c.coalescer is None:
@@ -276,6 +343,48 @@ class MI355XVectorStoreConnector:
                                                 metadata=copy.deepcopy(c.metadatas[r]))
                               for d, r in zip(dist[j, :k].tolist(), rows[j, :k].tolist()) if r >= 0]
         return out
+
+    def _hybrid(self, c: _Collection, q, text: str, k: int, flt) -> List[DocumentWithScore]:
+        from .lexical import analyze
+        with c.lock:
+            c.ensure_lex()
+            terms = c.vocab.query_ids(analyze(text))
+            k_each = int(self.hybrid_k_each or max(k, 4 * k))
+            k_each = min(k_each, 1024)
+            k = min(k, 2 * k_each)
+            allow, mkey = None, 0
+            if flt is not None:
+                mkey, allow = self._allow_mask(c, flt)
+            scores, rows = c.lex.hybrid(c.store, q.reshape(1, -1), [terms], k, k_each,
+                                        self.rrf_rank_const, allow=allow, mask_key=mkey)
+            return [DocumentWithScore(text=c.texts[r], score=float(s),
+                                      metadata=copy.deepcopy(c.metadatas[r]))
+                    for s, r in zip(scores[0].tolist(), rows[0].tolist()) if r >= 0]
+
+    def fulltext_search(self, query_text: str, top_k: int, keywords: Optional[List[str]] = None,
+                        **kwargs: Any) -> List[DocumentWithScore]:
+        """BM25 top-k over the collection's texts (the reference's ``fulltext_search`` node,
+        FulltextSearchParams{topk, keywords}); score = BM25 score, descending.  ``keywords``, when
+        given, replace the query text's terms.  kwargs ``filter`` is honoured with
+        ctx["honor_filter"], as in search()."""
+        c = _get(self.collection_name)
+        if c is None or top_k is None or top_k <= 0:
+            return []
+        from .lexical import analyze
+        text = " ".join(keywords) if keywords else (query_text or "")
+        flt = kwargs.get("filter") if self.honor_filter else None
+        with c.lock:
+            c.ensure_lex()
+            terms = c.vocab.query_ids(analyze(text))
+            if not terms:
+                return []
+            allow, mkey = None, 0
+            if flt is not None:
+                mkey, allow = self._allow_mask(c, flt)
+            scores, rows = c.lex.search([terms], min(int(top_k), 1024), allow=allow, mask_key=mkey)
+            return [DocumentWithScore(text=c.texts[r], score=float(s),
+                                      metadata=copy.deepcopy(c.metadatas[r]))
+                    for s, r in zip(scores[0].tolist(), rows[0].tolist()) if r >= 0]
 
     def get_vectors(self, ids: List[str]) -> np.ndarray:
         """Stored (normalised, fp16-rounded) vectors for uuids (with_vectors=True support)."""

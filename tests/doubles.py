@@ -77,6 +77,68 @@ class NumpyStore:
         return dist, out
 
 
+class NumpyLex:
+    """BM25 index double with the NativeLexIndex method surface (scores from the oracle)."""
+
+    def __init__(self, device: int = 0):
+        self.docs = []          # token-id lists
+        self.live = np.zeros(0, bool)
+
+    def _corpus(self):
+        from oracle.bm25 import LexCorpus
+        from super_rag_amd.lexical import doc_arrays
+        off, t, tf, dl = doc_arrays(self.docs)
+        return LexCorpus(off, t, tf, dl, self.live)
+
+    def add(self, docs):
+        first = len(self.docs)
+        self.docs.extend(list(d) for d in docs)
+        self.live = np.concatenate([self.live, np.ones(len(docs), bool)])
+        return first
+
+    def remove(self, rows):
+        self.live[np.asarray(rows, dtype=np.int64)] = False
+
+    def compact(self):
+        m = np.full(len(self.docs), -1, dtype=np.int64)
+        keep = np.nonzero(self.live)[0]
+        m[keep] = np.arange(len(keep))
+        self.docs = [self.docs[i] for i in keep]
+        self.live = np.ones(len(keep), bool)
+        return m
+
+    def stats(self):
+        return {"rows": len(self.docs), "live": int(self.live.sum())}
+
+    def save(self, path):
+        import json
+        import os
+        with open(path + ".tmp", "w") as f:
+            json.dump({"docs": self.docs, "live": self.live.tolist()}, f)
+        os.replace(path + ".tmp", path)
+
+    @classmethod
+    def load(cls, path, device=0):
+        import json
+        with open(path) as f:
+            d = json.load(f)
+        x = cls()
+        x.docs, x.live = d["docs"], np.asarray(d["live"], bool)
+        return x
+
+    def search(self, queries, k, allow=None, mask_key=0):
+        from oracle.bm25 import bm25_topk
+        return bm25_topk(self._corpus(), queries, k, allow=allow)
+
+    def hybrid(self, store, queries, query_terms, k, k_each=None, rank_const=1,
+               min_score=float("-inf"), allow=None, mask_key=0):
+        from oracle.bm25 import rrf_rows
+        k_each = k_each or k
+        _, dense = store.search(queries, k_each, allow=allow, mask_key=mask_key)
+        _, lexical = self.search(query_terms, k_each, allow=allow)
+        return rrf_rows(dense, lexical, k, rank_const, min_score)
+
+
 class _Spec:
     def __init__(self, hidden=8, pair_style=0):
         self.hidden = hidden

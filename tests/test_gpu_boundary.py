@@ -6,6 +6,7 @@ weights (oracle/encoder_ref.py, oracle/cosine_topk.py).  The connector's referen
 (score = cosine distance ascending, no ids in the documents, deletes by uuid, reorder-only rerank)
 are asserted on real kernels, not on the CPU doubles of test_boundary.py."""
 import asyncio
+import os
 
 import numpy as np
 import pytest
@@ -228,3 +229,20 @@ def test_ingest_write_path_long_chunks():
     ix.delete_index(new_ids + ids[10:])
     assert V._collections["gpu_ingest"].store.count()[1] == 0
     conn.delete_collection()
+
+
+def test_native_library_first_then_torch_in_one_process():
+    # PyTorch bundles its own HIP runtime: the binding must not let the native library bind a
+    # second one that torch then cannot initialise (_native.load imports torch first).
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "from super_rag_amd import _native as N\n"
+            "from super_rag_amd.lexical import rrf_fuse\n"
+            "import numpy as np\n"
+            "N.require_gpu(); rrf_fuse(np.array([[1, 2]]), np.array([[2, 3]]), 3)\n"
+            "import torch; torch.cuda.init(); assert torch.cuda.device_count() >= 1\n"
+            "print('ok')\n") % (root, os.path.join(root, "super-rag_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-2000:]

@@ -1,0 +1,190 @@
+"""GPU parity of the lexical (BM25) index and the hybrid rrf fusion (k_lex.hip) through the C-ABI:
+bit-exact against the oracle (oracle/bm25.py) — BM25 scores are 2^-16 fixed-point integers summed
+order-independently, rrf scores are fp64 sums of the same reciprocals in the same order."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rrf_fixtures.json")
+
+
+def _docs(rng, n, vocab, zipf=1.25, max_len=48):
+    lens = rng.integers(0, max_len, n)
+    flat = (rng.zipf(zipf, int(lens.sum())) - 1) % vocab
+    out, p = [], 0
+    for L in lens:
+        out.append(flat[p:p + L].tolist())
+        p += L
+    return out
+
+
+def _queries(rng, B, vocab, zipf=1.25):
+    qs = [((rng.zipf(zipf, rng.integers(1, 8)) - 1) % vocab).tolist() for _ in range(B)]
+    qs[0] = qs[0] + qs[0][:1]        # a repeated term counts twice
+    qs[1] = [vocab + 5]              # unknown term
+    qs[2] = []                       # empty query
+    qs[3] = [int(np.argmax(np.bincount(np.concatenate([np.asarray(q, int) for q in qs[4:]]))))]
+    return qs
+
+
+def _oracle(docs, live):
+    from oracle.bm25 import LexCorpus
+    from super_rag_amd.lexical import doc_arrays
+    return LexCorpus(*doc_arrays(docs), live)
+
+
+@pytest.mark.parametrize("n,vocab,k", [(3000, 400, 10), (20000, 3000, 100), (5000, 50, 1024)])
+def test_bm25_topk_bit_exact(n, vocab, k):
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(n)
+    docs = _docs(rng, n, vocab)
+    lex = NativeLexIndex()
+    assert lex.add(docs[: n // 2]) == 0
+    assert lex.add(docs[n // 2:]) == n // 2
+    dead = rng.choice(n, n // 20, replace=False)
+    lex.remove(dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    qs = _queries(rng, 37, vocab)
+    s, r = lex.search(qs, k)
+    so, ro = bm25_topk(_oracle(docs, live), qs, k)
+    np.testing.assert_array_equal(r, ro)
+    np.testing.assert_array_equal(s, so)
+    assert (r[1] == -1).all() and (r[2] == -1).all()
+    # the accumulator is left all-zero: a second call returns the same
+    s2, r2 = lex.search(qs, k)
+    np.testing.assert_array_equal(r2, r)
+    np.testing.assert_array_equal(s2, s)
+    st = lex.stats()
+    assert st["rows"] == n and st["live"] == n - len(dead)
+
+
+def test_bm25_allow_mask_mutations_and_snapshot(tmp_path):
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(7)
+    n, vocab, k = 4000, 300, 25
+    docs = _docs(rng, n, vocab)
+    lex = NativeLexIndex()
+    lex.add(docs)
+    live = np.ones(n, bool)
+    qs = _queries(rng, 20, vocab)
+    allow = rng.random(n) < 0.3
+    for mkey in (11, 11, 0):
+        s, r = lex.search(qs, k, allow=allow, mask_key=mkey)
+        so, ro = bm25_topk(_oracle(docs, live), qs, k, allow=allow)
+        np.testing.assert_array_equal(r, ro)
+        np.testing.assert_array_equal(s, so)
+    # a removal after the mask was cached must invalidate it (same mask_key)
+    gone = ro[4][ro[4] >= 0][:3]
+    lex.remove(gone)
+    live[gone] = False
+    s, r = lex.search(qs, k, allow=allow, mask_key=11)
+    so, ro = bm25_topk(_oracle(docs, live), qs, k, allow=allow)
+    np.testing.assert_array_equal(r, ro)
+    np.testing.assert_array_equal(s, so)
+    # append more rows: statistics (N, df, avgdl) change for every query
+    more = _docs(rng, 500, vocab)
+    lex.add(more)
+    docs = docs + more
+    live = np.concatenate([live, np.ones(500, bool)])
+    s, r = lex.search(qs, k)
+    so, ro = bm25_topk(_oracle(docs, live), qs, k)
+    np.testing.assert_array_equal(r, ro)
+    np.testing.assert_array_equal(s, so)
+    # snapshot round trip
+    p = str(tmp_path / "x.srlex")
+    lex.save(p)
+    lex2 = NativeLexIndex.load(p)
+    s2, r2 = lex2.search(qs, k)
+    np.testing.assert_array_equal(r2, r)
+    np.testing.assert_array_equal(s2, s)
+    # compaction: dead rows dropped, ids remapped like the store's
+    remap = lex.compact()
+    keep = np.nonzero(live)[0]
+    assert (remap[keep] == np.arange(len(keep))).all() and (remap[~live] == -1).all()
+    s3, r3 = lex.search(qs, k)
+    so, ro = bm25_topk(_oracle([docs[i] for i in keep], np.ones(len(keep), bool)), qs, k)
+    np.testing.assert_array_equal(r3, ro)
+    np.testing.assert_array_equal(s3, so)
+
+
+def test_rrf_device_matches_reference_fixtures():
+    from super_rag_amd.lexical import rrf_fuse
+    cases = json.load(open(GOLD))["cases"]
+    for c in cases:
+        names = {}
+        for lst in c["lists"]:
+            for u in lst:
+                names.setdefault(u, len(names))
+        a, b = c["lists"]
+        ka, kb = max(len(a), 1), max(len(b), 1)
+        ra = np.full((1, ka), -1, np.int64)
+        rb = np.full((1, kb), -1, np.int64)
+        ra[0, :len(a)] = [names[u] for u in a]
+        rb[0, :len(b)] = [names[u] for u in b]
+        k_out = max(len(names), 1) + 2
+        s, r = rrf_fuse(ra, rb, k_out, c["rank_const"], c["min_score"])
+        inv = {v: u for u, v in names.items()}
+        m = len(c["ids"])
+        assert [inv[int(x)] for x in r[0, :m]] == c["ids"]
+        assert [float(x).hex() for x in s[0, :m]] == c["scores"]
+        assert (r[0, m:] == -1).all()
+
+
+def test_hybrid_search_is_rrf_of_dense_and_bm25():
+    from oracle.bm25 import rrf_rows
+    from super_rag_amd.lexical import NativeLexIndex, hybrid_search
+    from super_rag_amd.store import NativeStore
+    rng = np.random.default_rng(9)
+    n, vocab, dim = 30000, 2000, 96
+    docs = _docs(rng, n, vocab)
+    vecs = rng.standard_normal((n, dim)).astype(np.float32)
+    store = NativeStore(dim)
+    store.add(vecs)
+    lex = NativeLexIndex()
+    lex.add(docs)
+    dead = rng.choice(n, 300, replace=False)
+    store.remove(dead)
+    lex.remove(dead)
+    B, k, k_each = 24, 10, 40
+    qv = rng.standard_normal((B, dim)).astype(np.float32)
+    qs = _queries(rng, B, vocab)
+    for allow, mkey in ((None, 0), (rng.random(n) < 0.5, 5)):
+        s, r = hybrid_search(store, lex, qv, qs, k, k_each, rank_const=1, allow=allow, mask_key=mkey)
+        _, dr = store.search(qv, k_each, allow=allow, mask_key=mkey)
+        _, lr = lex.search(qs, k_each, allow=allow, mask_key=mkey)
+        so, ro = rrf_rows(dr, lr, k, 1)
+        np.testing.assert_array_equal(r, ro)
+        np.testing.assert_array_equal(s, so)
+        if allow is not None:
+            assert allow[r[r >= 0]].all()
+    # rank_const 60 and a min_score cut
+    s, r = hybrid_search(store, lex, qv, qs, k, k_each, rank_const=60, min_score=0.02)
+    _, dr = store.search(qv, k_each)
+    _, lr = lex.search(qs, k_each)
+    so, ro = rrf_rows(dr, lr, k, 60, 0.02)
+    np.testing.assert_array_equal(r, ro)
+    np.testing.assert_array_equal(s[ro >= 0], so[ro >= 0])
+
+
+def test_bm25_large_corpus_exact():
+    # 400k rows x ~24 postings (Zipf): heavy-head terms with ~10^5-row posting lists
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(1)
+    n, vocab, k = 400_000, 50_000, 100
+    docs = _docs(rng, n, vocab, max_len=48)
+    lex = NativeLexIndex()
+    for i in range(0, n, 100_000):
+        lex.add(docs[i:i + 100_000])
+    qs = _queries(rng, 64, vocab)
+    s, r = lex.search(qs, k)
+    so, ro = bm25_topk(_oracle(docs, np.ones(n, bool)), qs, k)
+    np.testing.assert_array_equal(r, ro)
+    np.testing.assert_array_equal(s, so)
