@@ -479,6 +479,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // Piece p's lane offset depends on p only through p * 8 rows (uniform, in soffset) and the
   // swizzle parity p & 1, so a lane keeps 2 offsets per operand.
   const int grp = wave >> 2, w4 = wave & 3;
+  (void)w4;
   uint32_t vbw[2], vbx[2];
 #pragma unroll
   for (int par = 0; par < 2; ++par) {
@@ -756,7 +757,6 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(
     void* __restrict__ Y, int64_t ldy, int M, int N, int K, const LnFold lf) {
   constexpr int BN = 256, BM = 128, KS = 32, NSLOT = 3;
   constexpr int SLOT = (BN + BM) * KS;  // halfs (24 KiB)
-  constexpr int GW = 6;                 // glds per wave per K-step (4 W + 2 X)
   __shared__ __attribute__((aligned(16))) half_t lds[NSLOT * SLOT];
 
   const int tiles_n = N / BN;

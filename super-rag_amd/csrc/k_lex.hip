@@ -9,19 +9,23 @@
 //   dlen[rows] int32 (document length in tokens), live[rows] u8;
 //   inverted index (CSR by term over LIVE documents, rebuilt on the device when dirty):
 //   off[T + 1] int64, post[nnz] u64 = row << 32 | tf, rows ascending inside a term (stable radix
-//   sort of the row-ordered forward index by term id).
+//   sort of the row-ordered forward index by term id, dead rows keyed past the vocabulary; off by a
+//   binary search per term over the sorted keys).
 //
-// Scoring (one query block of QB queries):
-//   L1 lex_score: one workgroup per (query, term, 4096-posting chunk).  Each posting's Okapi weight
+// Scoring (one block of queries):
+//   L0 lex_bounds: for every (query term, 8192-row block) the first posting of that block
+//      (binary search: postings are row-sorted inside a term).
+//   L1 lex_score: one workgroup per (row block, query).  The query's postings of the block are
+//      contiguous in each term's list (streaming 8-byte loads); each posting's Okapi weight
 //      w = idf * (tf * (k1 + 1)) / (tf + k1 * ((1 - b) + b * (dl / avgdl)))   (fp32, no FMA
 //      contraction, so a numpy float32 restatement reproduces it bit for bit) is quantised to
-//      q = max(1, rint(w * 2^16)) x (query multiplicity) and added with a 32-bit atomic into the
-//      query's dense accumulator acc[qb][row].  The first touch of a row (old == 0; q >= 1 so a
-//      touched row is never 0) appends the row to the query's touched list.  Integer sums make the
-//      result independent of the atomic order: bit-exact against the oracle.
-//   L2 lex_select: one workgroup per query: exact top-k of keys (acc << 32 | ~row) over the touched
-//      list with the block radix select (sr_topk.h, keys gathered from HBM each pass), then the
-//      touched accumulator entries are reset to 0 (the accumulator stays all-zero between calls).
+//      q = max(1, rint(w * 2^16)) x (query multiplicity) and added with an LDS atomic into the
+//      block.s 32 KiB accumulator.  Non-zero entries are then appended to the query's candidate
+//      keys (score << 32 | ~row; one counter atomic per wave).  Integer sums make the result
+//      independent of the atomic order: bit-exact against the oracle.
+//   L2 lex_select: one workgroup per query: exact top-k of the candidate keys: a score histogram
+//      pass, then a pass collecting the keys of the top bins into LDS for the block radix select
+//      (sr_topk.h).
 // Fusion:
 //   F1 rrf_fuse: one workgroup per query: rrf score of a row = sum over the lists of
 //      1 / (rank + rank_const) in fp64 (list a first, as graphiti accumulates), ordered by score
@@ -40,32 +44,47 @@
 
 namespace sr {
 
-constexpr int LEX_CHUNK = 4096;      // postings per scoring workgroup
-constexpr int LEX_THREADS = 256;
-constexpr float LEX_SCALE = 65536.f;  // fixed-point unit of the accumulated score
+#ifndef SR_LEX_RB
+#define SR_LEX_RB 8192
+#endif
+constexpr int LEX_RB = SR_LEX_RB;      // rows per accumulation block (32 KiB of LDS; 16384: -20 %)
+constexpr int LEX_THREADS = 512;
+constexpr float LEX_SCALE = 65536.f;   // fixed-point unit of the accumulated score
+constexpr int64_t LEX_KEY_BUDGET = (int64_t)1 << 28;  // candidate keys per query block (2 GiB)
 
-struct LexChunk {
-  int64_t start;  // first posting
-  int32_t len;    // postings in this chunk
-  int32_t qb;     // query index inside the block
+struct LexTerm {  // one distinct term of one query
+  int64_t start;  // first posting of the term
+  int32_t len;    // its document frequency (postings)
   float idf;
   int32_t mult;   // multiplicity of the term in the query
+  int32_t pad;
 };
 
 // ---- rebuild ------------------------------------------------------------------------------------
+// sort key of every forward posting: its term, or dead_key (= vocabulary size, sorts last) for a
+// tombstoned row
 __global__ void lex_keys_kernel(const int32_t* __restrict__ fterm, const uint64_t* __restrict__ fval,
                                 const uint8_t* __restrict__ live, int64_t P, uint32_t dead_key,
-                                uint32_t* __restrict__ keys, int* __restrict__ df) {
+                                uint32_t* __restrict__ keys) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
   const uint32_t row = (uint32_t)(fval[i] >> 32);
-  const int32_t t = fterm[i];
-  if (live[row]) {
-    keys[i] = (uint32_t)t;
-    atomicAdd(&df[t], 1);
-  } else {
-    keys[i] = dead_key;
+  keys[i] = live[row] ? (uint32_t)fterm[i] : dead_key;
+}
+
+// off[t] = first sorted posting with key >= t, t in [0, T] (so off[T] = live postings); a binary
+// search per term instead of a histogram (whose atomics serialise on the Zipf head terms)
+__global__ void lex_offsets_kernel(const uint32_t* __restrict__ keys, int64_t P, int64_t T,
+                                   int64_t* __restrict__ off) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > T) return;
+  int64_t lo = 0, hi = P;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)keys[mid] < t) lo = mid + 1;
+    else hi = mid;
   }
+  off[t] = lo;
 }
 
 // ---- L1 -----------------------------------------------------------------------------------------
@@ -81,50 +100,181 @@ __device__ __forceinline__ uint32_t bm25_fixed(float idf, float tf, float dl, fl
   return q < 1.f ? 1u : (uint32_t)q;
 }
 
+// bnd[t][blk] = first posting of term slot t whose row is >= blk * LEX_RB (postings are sorted by
+// row inside a term, and a posting's u64 orders by row first), blk in [0, NB]
+__global__ void lex_bounds_kernel(const LexTerm* __restrict__ terms, int nslots, int NB,
+                                  const uint64_t* __restrict__ post, int32_t* __restrict__ bnd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)nslots * (NB + 1)) return;
+  const int t = (int)(i / (NB + 1)), blk = (int)(i % (NB + 1));
+  const LexTerm e = terms[t];
+  const uint64_t target = ((uint64_t)blk * LEX_RB) << 32;
+  int lo = 0, hi = e.len;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (post[e.start + mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  bnd[i] = lo;
+}
+
+// One workgroup per (query, row block): the query's postings whose rows fall in the block are
+// accumulated with LDS atomics into a 8192-row fixed-point accumulator, then every non-zero
+// entry is appended to the query's candidate keys (score << 32 | ~row), one counter atomic per
+// wave.  Postings of a block are contiguous in each term's list: streaming 8-byte loads.
 __global__ __launch_bounds__(LEX_THREADS) void lex_score_kernel(
-    const LexChunk* __restrict__ chunks, const uint64_t* __restrict__ post,
-    const int32_t* __restrict__ dlen, const uint8_t* __restrict__ elig, int64_t rows,
-    float avgdl, float k1, float b, uint32_t* __restrict__ acc, int* __restrict__ tcnt,
-    const int64_t* __restrict__ toff, int32_t* __restrict__ touched) {
-  const LexChunk c = chunks[blockIdx.x];
+    const LexTerm* __restrict__ terms, const int* __restrict__ slot_off, const int32_t* __restrict__ bnd,
+    int NB, const uint64_t* __restrict__ post, const int32_t* __restrict__ dlen,
+    const uint8_t* __restrict__ elig, int64_t rows, float avgdl, float k1, float b,
+    int* __restrict__ kcnt, const int64_t* __restrict__ koff, uint64_t* __restrict__ keys) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t acc[];
+  const int q = blockIdx.x, blk = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int s0 = slot_off[q], s1 = slot_off[q + 1];
+  int total = 0;
+  for (int t = s0; t < s1; ++t)
+    total += bnd[(int64_t)t * (NB + 1) + blk + 1] - bnd[(int64_t)t * (NB + 1) + blk];
+  if (total == 0) return;  // uniform: no posting of this query in this row block
+  for (int i = tid; i < LEX_RB; i += LEX_THREADS) acc[i] = 0u;
+  __syncthreads();
   const float one_minus_b = 1.f - b, k1p1 = k1 + 1.f;
-  uint32_t* a = acc + (int64_t)c.qb * rows;
-  int32_t* tl = touched + toff[c.qb];
-  for (int i = threadIdx.x; i < c.len; i += LEX_THREADS) {
-    const uint64_t v = post[c.start + i];
-    const uint32_t row = (uint32_t)(v >> 32);
-    if (elig && !elig[row]) continue;
-    const float tf = (float)(uint32_t)v;
-    const float dl = (float)dlen[row];
-    const uint32_t q = bm25_fixed(c.idf, tf, dl, avgdl, k1, b, one_minus_b, k1p1) * (uint32_t)c.mult;
-    const uint32_t old = atomicAdd(&a[row], q);
-    if (old == 0u) tl[atomicAdd(&tcnt[c.qb], 1)] = (int32_t)row;
+  const int64_t r0 = (int64_t)blk * LEX_RB;
+  for (int t = s0; t < s1; ++t) {
+    const LexTerm e = terms[t];
+    const int lo = bnd[(int64_t)t * (NB + 1) + blk], hi = bnd[(int64_t)t * (NB + 1) + blk + 1];
+    for (int p = lo + tid; p < hi; p += LEX_THREADS) {
+      const uint64_t v = post[e.start + p];
+      const uint32_t row = (uint32_t)(v >> 32);
+      if (elig && !elig[row]) continue;
+      const float tf = (float)(uint32_t)v;
+      const float dl = (float)dlen[row];
+      const uint32_t sc = bm25_fixed(e.idf, tf, dl, avgdl, k1, b, one_minus_b, k1p1) * (uint32_t)e.mult;
+      atomicAdd(&acc[row - r0], sc);
+    }
+  }
+  __syncthreads();
+  // wave w owns the contiguous entries [w * SPAN, (w + 1) * SPAN): count, one global atomic per
+  // workgroup (the per-query counter is shared by all NB workgroups of the query), then write
+  constexpr int SPAN = LEX_RB / (LEX_THREADS / 64);
+  __shared__ int wave_cnt[LEX_THREADS / 64];
+  __shared__ int wg_base;
+  const int wave = tid >> 6;
+  const uint32_t* mine = acc + wave * SPAN;
+  int cnt = 0;
+  for (int i = lane; i < SPAN; i += 64) cnt += __popcll(__ballot(mine[i] != 0u));
+  if (lane == 0) wave_cnt[wave] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < LEX_THREADS / 64; ++w) {
+      const int c = wave_cnt[w];
+      wave_cnt[w] = tot;
+      tot += c;
+    }
+    wg_base = atomicAdd(&kcnt[q], tot);
+  }
+  __syncthreads();
+  uint64_t* kl = keys + koff[q] + wg_base + wave_cnt[wave];
+  for (int i = lane; i < SPAN; i += 64) {
+    const uint32_t sc = mine[i];
+    const bool hit = sc != 0u;
+    const uint64_t bal = __ballot(hit);
+    if (hit) {
+      const uint32_t row = (uint32_t)(r0 + wave * SPAN + i);
+      kl[__popcll(bal & ((1ull << lane) - 1ull))] = ((uint64_t)sc << 32) | (uint64_t)(0xffffffffu - row);
+    }
+    kl += __popcll(bal);
   }
 }
 
 // ---- L2 -----------------------------------------------------------------------------------------
+// Two passes over the query's candidate keys instead of up to eight radix passes over HBM:
+//   pass 1: LDS histogram of a monotone 12-bit log-linear bin of every touched score;
+//   wave 0: the highest bin T with count(bin >= T) >= k (suffix scan over the 4096 bins);
+//   pass 2: keys with bin >= T are collected into LDS, then the exact block top-k runs on them.
+// If more than LSEL_CAP keys share the top bins (ties), the exact radix select runs over the
+// keys in HBM instead.
+constexpr int LSEL_BINS = 4096;
+constexpr int LSEL_CAP = 8192;
+
+__device__ __forceinline__ int score_bin(uint32_t s) {
+  const int e = 31 - __clz(s);  // s >= 1
+  if (e < 7) return (int)s;     // 1 .. 127 exact
+  return ((e - 6) << 7) | (int)((s >> (e - 7)) & 127u);  // <= 25 << 7 | 127 < 4096
+}
+
+struct LexSelSmem {
+  int hist[LSEL_BINS];
+  uint64_t keys[LSEL_CAP];
+  SelShared sh;
+  int thr, n_ge, nkeys;
+};
+
 __global__ __launch_bounds__(SEL_THREADS, 1) void lex_select_kernel(
-    uint32_t* __restrict__ acc, int64_t rows, const int* __restrict__ tcnt,
-    const int64_t* __restrict__ toff, const int32_t* __restrict__ touched, int k,
-    float* __restrict__ out_score, int64_t* __restrict__ out_rows) {
-  __shared__ SelShared sh;
-  const int q = blockIdx.x, tid = threadIdx.x;
-  uint32_t* a = acc + (int64_t)q * rows;
-  const int32_t* tl = touched + toff[q];
-  const int n = tcnt[q];
-  auto key = [&](int i) {
-    const uint32_t r = (uint32_t)tl[i];
-    return ((uint64_t)a[r] << 32) | (uint64_t)(0xffffffffu - r);
-  };
-  const int m = block_topk(key, n, k, sh);
+    const uint64_t* __restrict__ keys, const int* __restrict__ kcnt,
+    const int64_t* __restrict__ koff, int k, float* __restrict__ out_score,
+    int64_t* __restrict__ out_rows) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  LexSelSmem& S = *reinterpret_cast<LexSelSmem*>(smem_raw);
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const uint64_t* kl = keys + koff[q];
+  const int n = kcnt[q];
+  for (int i = tid; i < LSEL_BINS; i += blockDim.x) S.hist[i] = 0;
+  if (tid == 0) S.nkeys = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += blockDim.x) atomicAdd(&S.hist[score_bin((uint32_t)(kl[i] >> 32))], 1);
+  __syncthreads();
+  if (tid < 64) {
+    // lane l owns bins [64 l, 64 l + 64); suffix counts from the top bin down
+    int c = 0;
+    for (int j = 0; j < 64; ++j) c += S.hist[64 * lane + j];
+    int suf = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_down(suf, o, 64);
+      if (lane + o < 64) suf += v;
+    }
+    const int kk = n < k ? n : k;
+    const uint64_t bal = __ballot(suf >= kk && kk > 0);
+    if (tid == 0) {
+      S.thr = 0;
+      S.n_ge = n;
+    }
+    if (bal) {
+      const int L = 63 - __clzll(bal);
+      if (lane == L) {
+        int above = suf - c;  // keys in bins of higher lanes
+        int t = 64 * lane;
+        for (int j = 63; j >= 0; --j) {
+          above += S.hist[64 * lane + j];
+          if (above >= kk) {
+            t = 64 * lane + j;
+            break;
+          }
+        }
+        S.thr = t;
+        S.n_ge = above;
+      }
+    }
+  }
+  __syncthreads();
+  const int thr = S.thr;
+  int m;
+  if (S.n_ge <= LSEL_CAP) {
+    for (int i = tid; i < n; i += blockDim.x) {
+      const uint64_t key = kl[i];
+      if (score_bin((uint32_t)(key >> 32)) >= thr) S.keys[atomicAdd(&S.nkeys, 1)] = key;
+    }
+    __syncthreads();
+    m = block_topk([&](int i) { return S.keys[i]; }, S.nkeys, k, S.sh);
+  } else {
+    m = block_topk([&](int i) { return kl[i]; }, n, k, S.sh);
+  }
   for (int i = tid; i < k; i += blockDim.x) {
     const bool ok = i < m;
-    const uint64_t kk = ok ? sh.sel[i] : 0ull;
+    const uint64_t kk = ok ? S.sh.sel[i] : 0ull;
     out_score[(int64_t)q * k + i] = ok ? (float)(uint32_t)(kk >> 32) / LEX_SCALE : -INFINITY;
     out_rows[(int64_t)q * k + i] = ok ? (int64_t)(0xffffffffu - (uint32_t)kk) : -1;
   }
-  __syncthreads();  // every key read before the reset
-  for (int i = tid; i < n; i += blockDim.x) a[tl[i]] = 0u;
 }
 
 // ---- F1 -----------------------------------------------------------------------------------------
@@ -317,6 +467,7 @@ void LexIndex::rebuild(hipStream_t s) {
   nnz_ = 0;
   off_.reserve((size_t)(T + 1) * 8);
   if (P_ == 0 || T == 0) {
+    off_host_.assign((size_t)T + 1, 0);
     SR_HIP(hipMemsetAsync(off_.p, 0, (size_t)(T + 1) * 8, s));
     SR_HIP(hipStreamSynchronize(s));
     dirty_ = false;
@@ -326,45 +477,36 @@ void LexIndex::rebuild(hipStream_t s) {
   const int P = (int)P_;
   int end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)T) ++end_bit;  // keys 0..T
-  DevBuf keys_in, keys_out, df, tmp;
+  DevBuf keys_in, keys_out, tmp;
   keys_in.reserve((size_t)P * 4);
   keys_out.reserve((size_t)P * 4);
   post_.reserve((size_t)P * 8);
-  df.reserve((size_t)(T + 1) * 4);
-  SR_HIP(hipMemsetAsync(df.p, 0, (size_t)(T + 1) * 4, s));
   {
     ProfScope prof("lex_rebuild_keys", s, 0.0, (double)P * 16.0);
     hipLaunchKernelGGL(lex_keys_kernel, dim3((unsigned)ceil_div(P, 256)), dim3(256), 0, s,
                        fterm_.as<int32_t>(), fval_.as<uint64_t>(), live_.as<uint8_t>(), (int64_t)P,
-                       (uint32_t)T, keys_in.as<uint32_t>(), df.as<int>());
+                       (uint32_t)T, keys_in.as<uint32_t>());
     SR_LAUNCH_CHECK();
   }
-  size_t tb_sort = 0, tb_scan = 0;
+  size_t tb_sort = 0;
   SR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, keys_in.as<uint32_t>(),
                                             keys_out.as<uint32_t>(), fval_.as<uint64_t>(),
                                             post_.as<uint64_t>(), P, 0, end_bit, s));
-  SR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, df.as<int>(), off_.as<int64_t>(),
-                                          (int)(T + 1), s));
-  tmp.reserve(std::max(tb_sort, tb_scan));
+  tmp.reserve(tb_sort);
   {
     ProfScope prof("lex_rebuild_sort", s, 0.0, (double)P * 24.0);
     SR_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb_sort, keys_in.as<uint32_t>(),
                                               keys_out.as<uint32_t>(), fval_.as<uint64_t>(),
                                               post_.as<uint64_t>(), P, 0, end_bit, s));
   }
-  SR_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb_scan, df.as<int>(), off_.as<int64_t>(),
-                                          (int)(T + 1), s));
-  SR_HIP(hipMemcpyAsync(df_host_.data(), df.p, (size_t)T * 4, hipMemcpyDeviceToHost, s));
-  SR_HIP(hipMemcpyAsync(&nnz_, off_.as<int64_t>() + T, 8, hipMemcpyDeviceToHost, s));
-  SR_HIP(hipStreamSynchronize(s));
+  hipLaunchKernelGGL(lex_offsets_kernel, dim3((unsigned)ceil_div(T + 1, 256)), dim3(256), 0, s,
+                     keys_out.as<uint32_t>(), (int64_t)P, T, off_.as<int64_t>());
+  SR_LAUNCH_CHECK();
   off_host_.resize((size_t)T + 1);
-  int64_t acc = 0;
-  for (int64_t t = 0; t < T; ++t) {
-    off_host_[(size_t)t] = acc;
-    acc += df_host_[(size_t)t];
-  }
-  off_host_[(size_t)T] = acc;
-  SR_CHECK(acc == nnz_, "lex: rebuild count mismatch");
+  SR_HIP(hipMemcpyAsync(off_host_.data(), off_.p, (size_t)(T + 1) * 8, hipMemcpyDeviceToHost, s));
+  SR_HIP(hipStreamSynchronize(s));
+  nnz_ = off_host_[(size_t)T];
+  for (int64_t t = 0; t < T; ++t) df_host_[(size_t)t] = (int32_t)(off_host_[(size_t)t + 1] - off_host_[(size_t)t]);
   dirty_ = false;
 }
 
@@ -428,58 +570,84 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
     }
     cap[(size_t)b] = std::min<int64_t>(cap[(size_t)b], rows_);
   }
-  // query blocks: the dense accumulator (QB x rows u32) within ~2 GiB
+  // query blocks: candidate keys within LEX_KEY_BUDGET; grid (queries, row blocks), so the
+  // workgroups in flight belong to many queries
   const int64_t rows = std::max<int64_t>(rows_, 1);
-  const int QB = (int)std::max<int64_t>(1, std::min<int64_t>(B, ((int64_t)2 << 30) / (rows * 4)));
+  const int NB = (int)ceil_div(rows, LEX_RB);
+  SR_CHECK(NB <= 65535, "lex.search: more than 2^30 rows per index");
   const float adl = avgdl();
-  if (acc_rows_ < rows || acc_q_ < QB) {
-    SR_HIP(hipStreamSynchronize(s));
-    acc_.release();
-    acc_.reserve((size_t)QB * rows * 4);
-    SR_HIP(hipMemsetAsync(acc_.p, 0, (size_t)QB * rows * 4, s));
-    acc_rows_ = rows;
-    acc_q_ = QB;
+  static bool attr_set = false;
+  if (!attr_set) {
+    SR_HIP(hipFuncSetAttribute((const void*)lex_score_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LEX_RB * 4));
+    SR_HIP(hipFuncSetAttribute((const void*)lex_select_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(LexSelSmem)));
+    attr_set = true;
   }
-  for (int b0 = 0; b0 < B; b0 += QB) {
-    const int qb = std::min(QB, B - b0);
-    std::vector<int64_t> toff((size_t)qb + 1, 0);
-    for (int i = 0; i < qb; ++i) toff[(size_t)i + 1] = toff[(size_t)i] + cap[(size_t)(b0 + i)];
-    std::vector<LexChunk> ch;
+  for (int b0 = 0; b0 < B;) {
+    int qb = 0;
+    int64_t nkeys = 0;
+    while (b0 + qb < B && qb < 65535 && (qb == 0 || nkeys + cap[(size_t)(b0 + qb)] <= LEX_KEY_BUDGET))
+      nkeys += cap[(size_t)(b0 + qb++)];
+    std::vector<int64_t> koff((size_t)qb + 1, 0);
+    std::vector<int> slot_off((size_t)qb + 1, 0);
+    std::vector<LexTerm> slots;
+    int64_t scored = 0;
     for (int i = 0; i < qb; ++i) {
+      koff[(size_t)i + 1] = koff[(size_t)i] + cap[(size_t)(b0 + i)];
       for (const QT& e : qt[(size_t)(b0 + i)]) {
-        const int64_t st = off_host_[(size_t)e.term], len = df_host_[(size_t)e.term];
-        const float w = idf(len);
-        for (int64_t c = 0; c < len; c += LEX_CHUNK)
-          ch.push_back({st + c, (int32_t)std::min<int64_t>(LEX_CHUNK, len - c), i, w, e.mult});
+        const int64_t len = df_host_[(size_t)e.term];
+        slots.push_back({off_host_[(size_t)e.term], (int32_t)len, idf(len), e.mult, 0});
+        scored += len;
       }
+      slot_off[(size_t)i + 1] = (int)slots.size();
     }
-    const size_t b_ch = ch.size() * sizeof(LexChunk), b_off = (size_t)(qb + 1) * 8;
-    const size_t b_cnt = (size_t)qb * 4, b_tl = (size_t)std::max<int64_t>(toff[(size_t)qb], 1) * 4;
-    ws_.reserve(b_ch + b_off + b_cnt + b_tl + 64);
+    const int nslots = (int)slots.size();
+    const size_t b_sl = std::max<size_t>(slots.size(), 1) * sizeof(LexTerm);
+    const size_t b_so = (size_t)(qb + 1) * 4, b_ko = (size_t)(qb + 1) * 8, b_cnt = (size_t)qb * 4;
+    const size_t b_bnd = (size_t)std::max(nslots, 1) * (NB + 1) * 4;
+    const size_t b_keys = (size_t)std::max<int64_t>(koff[(size_t)qb], 1) * 8;
+    size_t o = 0;
+    auto carve = [&](size_t bytes) {
+      const size_t at = o;
+      o += (size_t)round_up((int64_t)bytes, 256);
+      return at;
+    };
+    const size_t o_sl = carve(b_sl), o_so = carve(b_so), o_ko = carve(b_ko), o_cnt = carve(b_cnt),
+                 o_bnd = carve(b_bnd), o_keys = carve(b_keys);
+    ws_.reserve(o);
     char* w = ws_.as<char>();
-    LexChunk* d_ch = reinterpret_cast<LexChunk*>(w);
-    int64_t* d_toff = reinterpret_cast<int64_t*>(w + round_up(b_ch, 16));
-    int* d_cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(d_toff) + round_up(b_off, 16));
-    int32_t* d_tl = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d_cnt) + round_up(b_cnt, 16));
-    if (b_ch) SR_HIP(hipMemcpyAsync(d_ch, ch.data(), b_ch, hipMemcpyHostToDevice, s));
-    SR_HIP(hipMemcpyAsync(d_toff, toff.data(), b_off, hipMemcpyHostToDevice, s));
+    LexTerm* d_sl = reinterpret_cast<LexTerm*>(w + o_sl);
+    int* d_so = reinterpret_cast<int*>(w + o_so);
+    int64_t* d_ko = reinterpret_cast<int64_t*>(w + o_ko);
+    int* d_cnt = reinterpret_cast<int*>(w + o_cnt);
+    int32_t* d_bnd = reinterpret_cast<int32_t*>(w + o_bnd);
+    uint64_t* d_keys = reinterpret_cast<uint64_t*>(w + o_keys);
+    if (nslots) SR_HIP(hipMemcpyAsync(d_sl, slots.data(), slots.size() * sizeof(LexTerm), hipMemcpyHostToDevice, s));
+    SR_HIP(hipMemcpyAsync(d_so, slot_off.data(), b_so, hipMemcpyHostToDevice, s));
+    SR_HIP(hipMemcpyAsync(d_ko, koff.data(), b_ko, hipMemcpyHostToDevice, s));
     SR_HIP(hipMemsetAsync(d_cnt, 0, b_cnt, s));
-    if (!ch.empty()) {
-      ProfScope prof("lex_score", s, 0.0, (double)(toff[(size_t)qb]) * 16.0);
-      hipLaunchKernelGGL(lex_score_kernel, dim3((unsigned)ch.size()), dim3(LEX_THREADS), 0, s, d_ch,
-                         post_.as<uint64_t>(), dlen_.as<int32_t>(), elig, rows, adl, k1_, b_,
-                         acc_.as<uint32_t>(), d_cnt, d_toff, d_tl);
+    if (nslots) {
+      const int64_t nb = (int64_t)nslots * (NB + 1);
+      hipLaunchKernelGGL(lex_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, s, d_sl,
+                         nslots, NB, post_.as<uint64_t>(), d_bnd);
+      SR_LAUNCH_CHECK();
+      ProfScope prof("lex_score", s, 0.0, (double)scored * 12.0);
+      hipLaunchKernelGGL(lex_score_kernel, dim3((unsigned)qb, (unsigned)NB), dim3(LEX_THREADS),
+                         LEX_RB * 4, s, d_sl, d_so, d_bnd, NB, post_.as<uint64_t>(),
+                         dlen_.as<int32_t>(), elig, rows_, adl, k1_, b_, d_cnt, d_ko, d_keys);
       SR_LAUNCH_CHECK();
     }
     {
-      ProfScope prof("lex_select", s, 0.0, (double)(toff[(size_t)qb]) * 8.0);
-      hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), 0, s, acc_.as<uint32_t>(),
-                         rows, d_cnt, d_toff, d_tl, k, out_score + (int64_t)b0 * k,
+      ProfScope prof("lex_select", s, 0.0, (double)koff[(size_t)qb] * 8.0);
+      hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), sizeof(LexSelSmem), s,
+                         d_keys, d_cnt, d_ko, k, out_score + (int64_t)b0 * k,
                          out_rows + (int64_t)b0 * k);
       SR_LAUNCH_CHECK();
     }
     // the host vectors above back async copies: finish the block before they go away
     SR_HIP(hipStreamSynchronize(s));
+    b0 += qb;
   }
   end(s);
 }
@@ -616,7 +784,6 @@ void LexIndex::load_rows(const std::vector<int32_t>& dl, const std::vector<uint8
       sum_dl_ += dl[(size_t)r];
     }
   for (int32_t t : ft) vocab_ = std::max<int64_t>(vocab_, (int64_t)t + 1);
-  acc_rows_ = 0;  // the accumulator is re-sized (and zeroed) at the next search
   dirty_ = true;
   ++version_;
 }

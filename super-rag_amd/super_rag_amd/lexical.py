@@ -133,12 +133,20 @@ class NativeLexIndex:
         """Append documents (token-id lists); returns the first row id."""
         if not len(docs):
             return self.stats()["rows"]
-        off, terms, tf, dl = doc_arrays(docs)
+        return self.add_arrays(*doc_arrays(docs))
+
+    def add_arrays(self, off, terms, tf, dl) -> int:
+        """Bulk append of pre-tokenised documents in the C-ABI layout (doc_arrays output:
+        off int64[n+1], distinct terms int32 with counts tf int32, lengths dl int32)."""
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        terms = np.ascontiguousarray(terms, dtype=np.int32)
+        tf = np.ascontiguousarray(tf, dtype=np.int32)
+        dl = np.ascontiguousarray(dl, dtype=np.int32)
+        n = len(off) - 1
         if terms.size == 0:
-            terms = np.zeros(1, dtype=np.int32)
-            tf = np.ones(1, dtype=np.int32)
+            terms, tf = np.zeros(1, np.int32), np.ones(1, np.int32)
         first = ctypes.c_int64(0)
-        N.call("sr_lex_add", self._h, N.ptr(off), N.ptr(terms), N.ptr(tf), N.ptr(dl), len(docs),
+        N.call("sr_lex_add", self._h, N.ptr(off), N.ptr(terms), N.ptr(tf), N.ptr(dl), n,
                ctypes.byref(first))
         return int(first.value)
 

@@ -188,3 +188,20 @@ def test_bm25_large_corpus_exact():
     so, ro = bm25_topk(_oracle(docs, np.ones(n, bool)), qs, k)
     np.testing.assert_array_equal(r, ro)
     np.testing.assert_array_equal(s, so)
+
+
+def test_bm25_ties_beyond_the_lds_collect_capacity():
+    # 20k rows with the same score for the query: more keys share the top histogram bin than the
+    # selection's LDS holds -> the exact radix select over HBM path; ties resolve by row id
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    docs = [[5, 6]] * 20000 + [[5, 5, 6]] * 3 + [[7]] * 50
+    lex = NativeLexIndex()
+    lex.add(docs)
+    qs = [[5], [6], [5, 6], [7]]
+    for k in (10, 1024):
+        s, r = lex.search(qs, k)
+        so, ro = bm25_topk(_oracle(docs, np.ones(len(docs), bool)), qs, k)
+        np.testing.assert_array_equal(r, ro)
+        np.testing.assert_array_equal(s, so)
+    assert r[0, :3].tolist() == [20000, 20001, 20002] and r[0, 3] == 0
