@@ -51,6 +51,7 @@ extern "C" {
 
 #define SR_DTYPE_F32 0
 #define SR_DTYPE_F16 1
+#define SR_DTYPE_FP8_E4M3 2   /* OCP e4m3fn (scan copy of the store, sr_store_set_scan_dtype)  */
 
 #define SR_POOL_CLS 0         /* BGE models: hidden state of the first token             */
 #define SR_POOL_MEAN 1        /* attention-mask weighted mean over tokens                */
@@ -103,6 +104,13 @@ int sr_store_search_masked(sr_store* s, const float* q, int B, int k, const uint
  * once at the end to check the candidate-overflow flag (and reruns the exact slow path if set). */
 int sr_store_search_dev(sr_store* s, const void* q, int q_dtype, int B, int k, float* out_sim,
                         int64_t* out_rows, int64_t row_offset, void* stream);
+/* Scan precision (BASELINE config 5 "fp8 MFMA GEMM path"): SR_DTYPE_F16 (default) or
+ * SR_DTYPE_FP8_E4M3: an fp8 copy of the rows (per-row power-of-two scale) is scanned with the
+ * block-scaled fp8 MFMA (half the HBM bytes of the fp16 scan), the top max(2k, k + 32) candidates
+ * are re-scored exactly on the fp16 rows, and the exact top k is returned (same result as the fp16
+ * scan whenever the fp8 stage keeps the true top k among its candidates; recall measured in
+ * tests/test_gpu_store.py and bench).  Quantises every row when switched on. */
+int sr_store_set_scan_dtype(sr_store* s, int dtype);
 /* Snapshot (checkpoint/resume of the corpus; SeekDB persisted rows server-side). */
 int sr_store_save(sr_store* s, const char* path);
 int sr_store_load(const char* path, int device, sr_store** out);

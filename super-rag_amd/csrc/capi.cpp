@@ -244,6 +244,14 @@ int sr_store_search_dev(sr_store* s, const void* q, int q_dtype, int B, int k, f
   SR_API_END
 }
 
+int sr_store_set_scan_dtype(sr_store* s, int dtype) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->set_scan_dtype(dtype);
+  SR_API_END
+}
+
 int sr_store_save(sr_store* s, const char* path) {
   SR_API_BEGIN
   SR_NONNULL(s);

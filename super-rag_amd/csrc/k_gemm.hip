@@ -63,6 +63,25 @@ __device__ __forceinline__ half8 read_frag(const half_t* lds_tile, int row, int 
   return *reinterpret_cast<const half8*>(lds_tile + off);
 }
 
+// fp8 fragment of a 128-byte K-step row: the lane's two 16-byte chunks c and c + 4 (the same two
+// reads as the f16 K-step's two halves) as ONE 32-byte operand of the block-scaled fp8 MFMA.  The
+// MFMA pairs A and B elements by their (lane group, byte) slot, so any slot -> k map shared by A
+// and B is exact (checked with integer data: tools/diag/mfma8_layout.hip).
+typedef int int8v __attribute__((ext_vector_type(8)));
+typedef int int4v_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int8v read_frag8(const half_t* lds_tile, int row, int chunk) {
+  const int4v_ lo = __builtin_bit_cast(int4v_, read_frag(lds_tile, row, chunk));
+  const int4v_ hi = __builtin_bit_cast(int4v_, read_frag(lds_tile, row, chunk + 4));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// Unit vectors are stored / staged as e4m3(256 x): |256 x_i| <= 256 < 448 never saturates and the
+// E8M0 block scales 119 = 2^-8 on A and B undo the factor inside the MFMA (exact power of two), so
+// the accumulators are plain cosines.
+__device__ __forceinline__ float4v mfma8(int8v a, int8v b, float4v c) {
+  // fmt 0 / 0 = fp8 e4m3 (OCP); E8M0 block scales 119 = 2^-8
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 119, 0, 119);
+}
+
 // Exact-GELU x * Phi(x) with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
 // the fp16 rounding of the output): branch-free, one v_rcp + one v_exp + 7 FMA per element,
 // about a third of the instructions of the library erff in this VALU-heavy epilogue.
@@ -359,7 +378,9 @@ struct PipeEpi {
 
 // EPI_SCAN epilogue (K1 threshold mode on the GEMM main loop): lane owns
 // sim(row n = nw0 + 16i + 4(lane>>4) + r, query q = mw0 + 16j + (lane&15)) of the chunk; keys of
-// live rows with sim >= tau[q] are appended to q's candidate list (cap entries, overflow counted).
+// rows with sim >= tau[q] are appended to q's candidate list (cap entries, overflow counted).
+// Reading the rows' live flags here cost a load per row per tile on the critical path (and VGPRs
+// the fp8 main loop needs): the selection filters tombstoned rows instead.
 __device__ __forceinline__ void scan_epilogue(float4v (&acc)[8][4], int nw0, int mw0, int lane, int B,
                                               int nrows, const float* __restrict__ tau,
                                               const uint8_t* __restrict__ live,
@@ -370,21 +391,20 @@ __device__ __forceinline__ void scan_epilogue(float4v (&acc)[8][4], int nw0, int
     const int q = mw0 + 16 * j + (lane & 15);
     t[j] = q < B ? tau[q] : INFINITY;
   }
+  // (no live flags here: tombstoned rows' keys are dropped by the selection, topk_select)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int nb = nw0 + 16 * i + 4 * (lane >> 4);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int n = nb + r;
-      if (n >= nrows) continue;
-      if (live != nullptr && live[n] == 0) continue;
+      if (nb + r >= nrows) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float sim = acc[i][j][r];
         if (sim >= t[j]) {  // false for padded queries (t = inf)
           const int q = mw0 + 16 * j + (lane & 15);
           const int pos = atomicAdd(reinterpret_cast<int*>(lf.stat_out) + q, 1);
-          if (pos < cap) cand[(int64_t)q * cap + pos] = make_key(sim, (uint32_t)(lf.stat_ld + n));
+          if (pos < cap) cand[(int64_t)q * cap + pos] = make_key(sim, (uint32_t)(lf.stat_ld + nb + r));
         }
       }
     }
@@ -430,6 +450,16 @@ __device__ __forceinline__ void stage_offsets(uint32_t (&voff)[NI], int64_t ld, 
     __builtin_amdgcn_sched_barrier(0);                                     \
   } while (0)
 
+// The same for a phase of 8 (fp8) MFMAs: R reads after the first MFMAs, about one per MFMA.
+#define SR_INTERLEAVE8(R)                                                  \
+  do {                                                                     \
+    _Pragma("unroll") for (int _r = 0; _r < 8; ++_r) {                     \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                   \
+      __builtin_amdgcn_sched_group_barrier(0x100, ((R) + 7) / 8, 0);       \
+    }                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+  } while (0)
+
 // PERSIST: one workgroup per CU walks a contiguous per-XCD tile range.  The next tile's first two
 // K-steps are staged (glds) right after the last K-step's barrier, before the epilogue, and the
 // epilogue's stores are left in flight: the next tile's first waits count them (vmcnt(8 + 32) /
@@ -445,6 +475,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     void* __restrict__ Y, int64_t ldy, int M, int N, int K, const LnFold lf) {
   constexpr int BN = 256, BM = 256;
   constexpr int STAGE = (BN + BM) * GBK;  // halfs per buffer (64 KiB)
+  // fp8 operands (EPI_SCAN8): K, lda count 2-byte units, so the staging below moves the same
+  // 128-byte K-step rows; a K-step then holds 128 fp8 elements
+  constexpr bool F8 = EPI == EPI_SCAN8;
+  constexpr bool SCAN = EPI == EPI_SCAN || EPI == EPI_SCAN8;
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
@@ -515,6 +549,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 
   float4v acc[8][4];
   half8 aX[4], aY[4], bX[4], bY[4];
+  int8v f0[2], f1[2], fb[4];  // fp8 path: A row pairs (ping-pong) and B
 
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
@@ -604,15 +639,86 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // fp8 K-step (128 elements): four phases of 8 block-scaled MFMAs (each covers a 16 x 16 x 128
+  // block, twice the f16 MFMA's time), A row pairs ping-ponging between f0 / f1: q0 A[0,1] x B
+  // (reads A[2,3]), q1 A[2,3] (reads A[4,5]), q2 A[4,5] (reads A[6,7]), barrier + staging as in
+  // the f16 K-step, q3 A[6,7] (reads K-step kt+1's A[0,1] and B, in two halves).
+  auto kstep8 = [&](int kt, const int SN, const bool RN, bool lenient, int mn, int nn,
+                    bool more_) __attribute__((always_inline)) {
+    half_t* cur = lds + (kt & 1) * STAGE;
+    const half_t* nxt = lds + ((kt + 1) & 1) * STAGE;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      int8v (&use)[2] = (q & 1) ? f1 : f0;
+      int8v (&fill)[2] = (q & 1) ? f0 : f1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fill[i] = read_frag8(cur, arow + 16 * (2 * q + 2 + i), c0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[2 * q + i][j] = mfma8(use[i], fb[j], acc[2 * q + i][j]);
+      SR_INTERLEAVE8(4);
+    }
+    (void)lenient;
+    SR_WAITCNT(0, 0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (SN == 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
+    if (SN == 2) {
+      if (more_) {
+        if (grp == 0)
+          stage(0, lds, mn, nn);
+        else
+          stage(1, lds + STAGE, mn, nn);
+      }
+    }
+    // q3 in two halves so B needs no second register set: A[6,7] x B[0,1], then K-step kt+1's
+    // A[0,1] and B[0,1] are read into the freed registers while A[6,7] x B[2,3] runs, then its
+    // B[2,3] (consumed last in the next q0)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[6 + i][j] = mfma8(f1[i], fb[j], acc[6 + i][j]);
+    if (RN) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) f0[i] = read_frag8(nxt, arow + 16 * i, c0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = read_frag8(nxt + BN * GBK, brow + 16 * j, c0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 2; j < 4; ++j) acc[6 + i][j] = mfma8(f1[i], fb[j], acc[6 + i][j]);
+    if (RN) {
+#pragma unroll
+      for (int j = 2; j < 4; ++j) fb[j] = read_frag8(nxt + BN * GBK, brow + 16 * j, c0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto step = [&](int kt, const int SN, const bool RN, bool lenient, int mn, int nn,
+                  bool more_) __attribute__((always_inline)) {
+    if constexpr (F8)
+      kstep8(kt, SN, RN, lenient, mn, nn, more_);
+    else
+      kstep(kt, SN, RN, lenient, mn, nn, more_);
+  };
+
   for (;;) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) aY[i] = read_frag(lds, arow + 16 * i, c0);
+      for (int i = 0; i < 2; ++i) f0[i] = read_frag8(lds, arow + 16 * i, c0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bX[j] = read_frag(lds + BN * GBK, brow + 16 * j, c0);
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag8(lds + BN * GBK, brow + 16 * j, c0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) aY[i] = read_frag(lds, arow + 16 * i, c0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bX[j] = read_frag(lds + BN * GBK, brow + 16 * j, c0);
+    }
 
     const int t_next = t + t_step;
     const bool more = PERSIST && t_next < t_end && nk > 1;
@@ -620,20 +726,20 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     int kt = 0;
     bool lenient = stores_pending;
     for (; kt + 2 < nk; ++kt) {
-      kstep(kt, 1, true, lenient, 0, 0, false);
+      step(kt, 1, true, lenient, 0, 0, false);
       lenient = false;
     }
     if (kt + 1 < nk) {
-      kstep(kt++, 0, true, lenient, 0, 0, false);
+      step(kt++, 0, true, lenient, 0, 0, false);
       lenient = false;
     }
     if constexpr (PERSIST)
-      kstep(kt, 2, false, lenient, m0n, n0n, more);
+      step(kt, 2, false, lenient, m0n, n0n, more);
     else
-      kstep(kt, 0, false, lenient, 0, 0, false);
+      step(kt, 0, false, lenient, 0, 0, false);
 
     // (EPI_SCAN issues a data-dependent number of atomics / stores: never counted as pending)
-    const bool full = EPI != EPI_SCAN && m0 + BM <= M;
+    const bool full = !SCAN && m0 + BM <= M;
     if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
       const int g = lane >> 4, odd = g & 1;
       const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
@@ -679,7 +785,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
       if (sacc == 12345.678f) reinterpret_cast<float*>(Y)[tid] = sacc;
-    } else if constexpr (EPI == EPI_SCAN) {
+    } else if constexpr (SCAN) {
       scan_epilogue(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                     reinterpret_cast<const uint8_t*>(R), reinterpret_cast<uint64_t*>(Y), (int)ldy, lf);
     } else if (full) {
@@ -1021,9 +1127,37 @@ void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* l
   lf.stat_ld = r0;
   const int64_t tiles = ceil_div(n, 256);
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
-  hipLaunchKernelGGL((gemm_pipe_kernel<EPI_SCAN, true>), grid, block, 0, s, Q, ldc,
+  static const bool diag_noepi = std::getenv("SR_SCAN_DIAG_NOEPI") != nullptr;  // timing only
+  auto kern = diag_noepi ? gemm_pipe_kernel<EPI_SCAN, true, 2> : gemm_pipe_kernel<EPI_SCAN, true>;
+  hipLaunchKernelGGL(kern, grid, block, 0, s, Q, ldc,
                      corpus + r0 * ldc, tau, (const void*)(live ? live + r0 : nullptr), (int64_t)0,
                      (void*)cand, (int64_t)cap, B, (int)n, (int)ldc, lf);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t* live, int64_t r0,
+                              int64_t r1, const uint8_t* Q8, int B, const float* tau, uint64_t* cand,
+                              int* cnt, int cap, hipStream_t s) {
+  SR_CHECK(B > 0 && B <= 256, "cosine_scan_gemm8: 1..256 queries");
+  SR_CHECK(ld8 % 128 == 0 && ld8 >= 256, "cosine_scan_gemm8: row bytes must be a multiple of 128, >= 256");
+  if (r1 <= r0) return;
+  const int64_t n = r1 - r0;
+  SR_CHECK(n < (1ll << 31), "cosine_scan_gemm8: chunk too large");
+  const double rows = (double)n;
+  ProfScope prof("cosine_scan8", s, 2.0 * rows * ld8 * B, rows * ld8 + (double)B * ld8);
+  LnFold lf;
+  lf.stat_out = reinterpret_cast<float*>(cnt);  // (EPI_SCAN field re-use, see LnFold)
+  lf.stat_ld = r0;
+  const int64_t tiles = ceil_div(n, 256);
+  const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+  // operands as 2-byte units: K = ld8 / 2 (the staging moves bytes)
+  static const bool diag_noepi = std::getenv("SR_SCAN_DIAG_NOEPI") != nullptr;  // timing only
+  auto kern = diag_noepi ? gemm_pipe_kernel<EPI_SCAN8, true, 2> : gemm_pipe_kernel<EPI_SCAN8, true>;
+  hipLaunchKernelGGL(kern, grid, block, 0, s,
+                     reinterpret_cast<const half_t*>(Q8), ld8 / 2,
+                     reinterpret_cast<const half_t*>(corpus8 + r0 * ld8), tau,
+                     (const void*)(live ? live + r0 : nullptr), (int64_t)0, (void*)cand, (int64_t)cap,
+                     B, (int)n, (int)(ld8 / 2), lf);
   SR_LAUNCH_CHECK();
 }
 

@@ -137,7 +137,7 @@ struct SelectSmem {
 __global__ __launch_bounds__(SEL_THREADS, 1) void topk_select_kernel(
     uint64_t* __restrict__ cand, int* __restrict__ cnt, int cap, float* __restrict__ tau, int k,
     int* __restrict__ overflow, int final_pass, float* __restrict__ out_sim,
-    int64_t* __restrict__ out_rows, int64_t row_offset) {
+    int64_t* __restrict__ out_rows, int64_t row_offset, const uint8_t* __restrict__ live) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   SelectSmem& S = *reinterpret_cast<SelectSmem*>(smem_raw);
   const int q = blockIdx.x, tid = threadIdx.x;
@@ -145,12 +145,13 @@ __global__ __launch_bounds__(SEL_THREADS, 1) void topk_select_kernel(
   if (n_raw > cap && tid == 0) atomicOr(overflow, 1);
   const int n_in = min(n_raw, cap);
   uint64_t* list = cand + (int64_t)q * cap;
-  // Load non-zero keys (zero = dead row in a dense chunk) into LDS.
+  // Load non-zero keys (zero = dead row in a dense chunk) of live rows into LDS (the GEMM scan's
+  // threshold epilogue does not read the live flags: tombstoned rows are dropped here).
   if (tid == 0) S.sh.nsel = 0;
   __syncthreads();
   for (int i = tid; i < n_in; i += blockDim.x) {
     const uint64_t key = list[i];
-    if (key != 0ull) {
+    if (key != 0ull && (live == nullptr || live[key_row(key)] != 0)) {
       const int p = atomicAdd(&S.sh.nsel, 1);
       S.keys[p] = key;
     }
@@ -351,13 +352,14 @@ int select_capacity() { return SEL_CAP; }
 
 void launch_topk_select(uint64_t* cand, int* cnt, int cap, float* tau, int B, int k,
                         int* overflow, bool final_pass, float* out_sim, int64_t* out_rows,
-                        int64_t row_offset, hipStream_t s) {
+                        int64_t row_offset, hipStream_t s, const uint8_t* live) {
   SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "topk: k must be in [1, 1024]");
   SR_CHECK(cap <= SEL_CAP, "topk: candidate capacity too large");
   ensure_select_attrs();
   ProfScope prof("topk_select", s, 0.0, (double)B * cap * 8.0);
   hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(SEL_THREADS), sizeof(SelectSmem), s, cand,
-                     cnt, cap, tau, k, overflow, final_pass ? 1 : 0, out_sim, out_rows, row_offset);
+                     cnt, cap, tau, k, overflow, final_pass ? 1 : 0, out_sim, out_rows, row_offset,
+                     live);
   SR_LAUNCH_CHECK();
 }
 

@@ -21,7 +21,10 @@ enum Epilogue {
   EPI_LNR16_STATS = 8,    // y = acc + b + LN(R) (R un-normalised)      -> fp16 + row statistics
   // K1 on the GEMM main loop (internal: launch_cosine_scan_gemm): W = corpus rows, X = queries,
   // epilogue = threshold filter appending (sim, row) keys to per-query candidate lists
-  EPI_SCAN = 9
+  EPI_SCAN = 9,
+  // the same on OCP fp8-e4m3 operands e4m3(256 x) of unit vectors (block-scaled MFMA
+  // v_mfma_scale_f32_16x16x128_f8f6f4, E8M0 block scales 2^-8 undo the factor)
+  EPI_SCAN8 = 10
 };
 
 // Per-row statistics hand-over between GEMMs (Chan-combinable partials over 128-column spans):
@@ -34,7 +37,7 @@ struct LnFold {
   const float* gamma = nullptr;    // LNR: LayerNorm weight of the residual rows (its beta is
                                    //      pre-added to the GEMM bias)
   float* stat_out = nullptr;       // *_STATS: [M][N / 128] partials of the output rows
-  // EPI_SCAN re-uses the fields (kernel-argument SGPRs are scarce in the persistent kernels):
+  // EPI_SCAN(8) re-uses the fields (kernel-argument SGPRs are scarce in the persistent kernels):
   // stat_out = per-query candidate counts (int*), stat_ld = global row id of the chunk's first
   // row; bias = tau[B], R = live flags of the chunk, Y = candidate keys [B][cap] (ldy = cap).
 };
@@ -52,6 +55,10 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
 void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 // K1 for large query blocks (B in (128, 256]) on the pipelined GEMM: rows [r0, r1) of the corpus
 // against B queries; non-dense threshold mode only (same contract as launch_cosine_scan).
+// fp8 rows e4m3(256 x) (ld8 bytes, a multiple of 128, >= 256) of unit vectors; sims are cosines.
+void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t* live, int64_t r0,
+                              int64_t r1, const uint8_t* Q8, int B, const float* tau, uint64_t* cand,
+                              int* cnt, int cap, hipStream_t s);
 void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* live, int64_t r0,
                              int64_t r1, const half_t* Q, int B, const float* tau, uint64_t* cand,
                              int* cnt, int cap, hipStream_t s);
@@ -101,7 +108,8 @@ void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uin
                         uint64_t* cand, int* cnt, int cap, hipStream_t s);
 void launch_topk_select(uint64_t* cand, int* cnt, int cap, float* tau, int B, int k,
                         int* overflow, bool final_pass, float* out_sim, int64_t* out_rows,
-                        int64_t row_offset, hipStream_t s);
+                        int64_t row_offset, hipStream_t s,
+                        const uint8_t* live = nullptr);
 void launch_topk_merge(const float* sims, const int64_t* rows, int P, int B, int k, int k_out,
                        float* out_sim, int64_t* out_rows, hipStream_t s);
 void launch_fill_int(int* p, int n, int v, hipStream_t s);

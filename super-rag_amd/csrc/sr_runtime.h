@@ -73,6 +73,9 @@ class Store {
                   int64_t row_offset, hipStream_t s, const uint8_t* elig = nullptr);
   // device eligibility mask live & allow (cached per mask_key and store version); null for null
   const uint8_t* eligibility(const uint8_t* allow, int64_t mask_key);
+  // scan dtype: SR_DTYPE_F16 (default) or SR_DTYPE_FP8_E4M3 (fp8 copy + exact fp16 re-scoring)
+  void set_scan_dtype(int dtype);
+  int scan_dtype() const { return fp8_ ? SR_DTYPE_FP8_E4M3 : SR_DTYPE_F16; }
   void save(const char* path);
   static Store* load(const char* path, int device);
   void compact(int64_t* old_to_new);
@@ -91,6 +94,11 @@ class Store {
   // Runs the chunked scan/select schedule for one block of <= 256 normalised queries.
   void search_block(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
                     int64_t row_offset, hipStream_t s, bool safe, const uint8_t* live);
+  void search_block8(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
+                     int64_t row_offset, hipStream_t s, bool safe, const uint8_t* live);
+  int ld8() const;
+  void grow_fp8();
+  void quantize_rows(int64_t r0, int64_t n, hipStream_t s);
 
   int dim_, ld_, device_;
   int64_t n_rows_ = 0, n_live_ = 0, capacity_ = 0;
@@ -101,6 +109,9 @@ class Store {
   // search workspace
   DevBuf qbuf_, qstage_, cand_, cnt_, tau_, overflow_, osim_, orows_, scratch_;
   int ws_queries_ = 0;
+  // fp8 scan: e4m3(256 x) copy of the rows (ld8 bytes each), query staging, fp8-stage candidates
+  bool fp8_ = false;
+  DevBuf corpus8_, q8_, approx_;
   // filtered search: device eligibility mask (live & allow) and what it was built from
   DevBuf mask_;
   int64_t version_ = 0, mask_key_ = 0, mask_version_ = -1, mask_rows_ = -1;

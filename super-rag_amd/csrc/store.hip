@@ -34,6 +34,54 @@ __global__ void gather_rows_kernel(const half_t* __restrict__ src, int ld,
   half8* d = reinterpret_cast<half8*>(dst + r * ld);
   for (int c = threadIdx.x; c < ld / 8; c += blockDim.x) d[c] = s[c];
 }
+// OCP e4m3fn (bias 7, max 448, no infinities), round to nearest even; |v| <= 448 by construction.
+__device__ __forceinline__ uint32_t e4m3_rne(float v) {
+  const uint32_t sign = v < 0.f ? 0x80u : 0u;
+  const float a = fabsf(v);
+  if (a < 0.015625f) {  // below 2^-6: subnormal steps of 2^-9
+    const uint32_t m = (uint32_t)rintf(a * 512.f);  // 0 .. 8 (8 = the smallest normal)
+    return sign | m;
+  }
+  int e;
+  (void)frexpf(a, &e);  // a = f * 2^e, f in [0.5, 1)  ->  a = (1 + m / 8) * 2^(e - 1)
+  const float m = rintf((ldexpf(a, 1 - e) - 1.f) * 8.f);  // 0 .. 8 (8 carries into the exponent)
+  const uint32_t code = (uint32_t)(e - 1 + 7) * 8u + (uint32_t)m;
+  return sign | code;
+}
+
+// fp16 unit rows (ld halfs) -> e4m3(256 x) rows (ld8 bytes, zero padded): |256 x| <= 256 < 448, so
+// one fixed power of two serves every row and query (the scan MFMA's E8M0 scales undo it).
+__global__ void quantize_rows_fp8_kernel(const half_t* __restrict__ src, int ld, int dim,
+                                         int64_t n, uint8_t* __restrict__ dst, int ld8) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  const half_t* x = src + r * ld;
+  uint8_t* d = dst + r * ld8;
+  for (int c = lane; c < ld8; c += 64)
+    d[c] = c < dim ? (uint8_t)e4m3_rne((float)x[c] * 256.f) : (uint8_t)0;
+}
+
+// exact fp16 re-scoring of a query's fp8-stage candidates: key (sim, row) per candidate slot
+// (0 = empty), count = kk
+__global__ void rescore_kernel(const half_t* __restrict__ corpus, int ld, int dim,
+                               const half_t* __restrict__ qn, const int64_t* __restrict__ rows,
+                               int kk, uint64_t* __restrict__ cand, int cap, int* __restrict__ cnt) {
+  const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const half_t* qv = qn + (int64_t)q * ld;
+  for (int c = wave; c < kk; c += blockDim.x >> 6) {
+    const int64_t row = rows[(int64_t)q * kk + c];
+    float acc = 0.f;
+    if (row >= 0) {
+      const half_t* x = corpus + row * ld;
+      for (int i = lane; i < dim; i += 64) acc = fmaf((float)qv[i], (float)x[i], acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) cand[(int64_t)q * cap + c] = row >= 0 ? make_key(acc, (uint32_t)row) : 0ull;
+  }
+  if (threadIdx.x == 0) cnt[q] = kk;
+}
+
 __global__ void f16_to_f32_rows_kernel(const half_t* __restrict__ src, int ld,
                                        const int64_t* __restrict__ rows, int64_t n, int dim,
                                        float* __restrict__ out) {
@@ -84,6 +132,45 @@ void Store::ensure_capacity(int64_t rows) {
   std::swap(live_.bytes, nl.bytes);
   capacity_ = cap;
   live_host_.resize((size_t)cap, 0);
+  if (fp8_) grow_fp8();
+}
+
+int Store::ld8() const { return (int)round_up(dim_, 128) < 256 ? 256 : (int)round_up(dim_, 128); }
+
+void Store::grow_fp8() {
+  DevBuf nc;
+  nc.reserve((size_t)capacity_ * ld8());
+  if (n_rows_ > 0 && corpus8_.p)
+    SR_HIP(hipMemcpyAsync(nc.p, corpus8_.p, (size_t)n_rows_ * ld8(), hipMemcpyDeviceToDevice, stream_));
+  SR_HIP(hipStreamSynchronize(stream_));
+  std::swap(corpus8_.p, nc.p);
+  std::swap(corpus8_.bytes, nc.bytes);
+}
+
+void Store::quantize_rows(int64_t r0, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(quantize_rows_fp8_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s,
+                     corpus_.as<half_t>() + r0 * ld_, ld_, dim_, n, corpus8_.as<uint8_t>() + r0 * ld8(),
+                     ld8());
+  SR_LAUNCH_CHECK();
+}
+
+void Store::set_scan_dtype(int dtype) {
+  SR_CHECK(dtype == SR_DTYPE_F16 || dtype == SR_DTYPE_FP8_E4M3, "store: scan dtype must be f16 or fp8");
+  DeviceGuard g(device_);
+  begin(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
+  if (dtype == SR_DTYPE_F16) {
+    fp8_ = false;
+    corpus8_.release();
+  } else if (!fp8_) {
+    SR_CHECK(ld8() <= 2048, "store: the fp8 scan supports dim <= 2048");
+    fp8_ = true;
+    grow_fp8();
+    quantize_rows(0, n_rows_, stream_);
+  }
+  end(stream_);
+  SR_HIP(hipStreamSynchronize(stream_));
 }
 
 void Store::add_host(const float* vecs, int64_t n, int64_t* out_rows) {
@@ -114,6 +201,7 @@ int64_t Store::add_dev(const void* vecs, int dtype, int64_t n, hipStream_t s) {
     ensure_capacity(n_rows_ + n);
   }
   launch_normalize_rows(vecs, dtype, n, dim_, corpus_.as<half_t>() + first * ld_, ld_, s);
+  if (fp8_) quantize_rows(first, n, s);
   SR_HIP(hipMemsetAsync(live_.as<uint8_t>() + first, 1, (size_t)n, s));
   end(s);
   std::fill(live_host_.begin() + first, live_host_.begin() + first + n, 1);
@@ -177,12 +265,67 @@ void Store::ensure_query_ws(int B) {
   cnt_.reserve(kQueryBlock * sizeof(int));
   tau_.reserve(kQueryBlock * sizeof(float));
   overflow_.reserve(sizeof(int));
+  q8_.reserve((size_t)kQueryBlock * 2048);
+  approx_.reserve((size_t)round_up((int64_t)kQueryBlock * SR_MAX_TOPK * 4, 256) +
+                  (size_t)kQueryBlock * SR_MAX_TOPK * 8);
   SR_HIP(hipStreamSynchronize(stream_));
   ws_queries_ = nq;
 }
 
+// fp8 scan (set_scan_dtype(SR_DTYPE_FP8_E4M3)): the same chunk / threshold schedule on the fp8 rows
+// (half the bytes, block-scaled MFMA) keeps the top kk = min(max(2k, k + 32), 1024) by the
+// fp8-stage similarity; those candidates are re-scored exactly on the fp16 rows and the top k of
+// the exact scores returned.  Exact whenever the fp8 stage's top kk contains the true top k.
+void Store::search_block8(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
+                          int64_t row_offset, hipStream_t s, bool safe, const uint8_t* live) {
+  const int cap = select_capacity();
+  const int kk = std::min(std::min(std::max(2 * k, k + 32), SR_MAX_TOPK), cap / 4);
+  uint64_t* cand = cand_.as<uint64_t>();
+  int* cnt = cnt_.as<int>();
+  float* tau = tau_.as<float>();
+  int* ovf = overflow_.as<int>();
+  const int64_t n = n_rows_;
+  uint8_t* q8 = q8_.as<uint8_t>();
+  hipLaunchKernelGGL(quantize_rows_fp8_kernel, dim3((unsigned)ceil_div(B, 4)), dim3(256), 0, s, qn,
+                     ld_, dim_, (int64_t)B, q8, ld8());
+  SR_LAUNCH_CHECK();
+  float* asim = approx_.as<float>();
+  int64_t* arow = reinterpret_cast<int64_t*>(approx_.as<char>() + round_up((int64_t)kQueryBlock * SR_MAX_TOPK * 4, 256));
+  launch_fill_int(cnt, B, 0, s);
+  launch_fill_float(tau, B, -INFINITY, s);
+  if (n == 0) {
+    launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, true, asim, arow, 0, s, live);
+  } else {
+    const int64_t dense = std::min<int64_t>(n, safe ? (int64_t)(cap - kk) : kDenseRows);
+    launch_cosine_scan_gemm8(corpus8_.as<uint8_t>(), ld8(), live, 0, dense, q8, B, tau, cand, cnt,
+                             cap, s);
+    launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, dense == n, asim, arow, 0, s, live);
+    const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(8, (cap - kk) / (2 * kk)));
+    int64_t r = dense;
+    while (r < n) {
+      const int64_t step = safe ? (int64_t)(cap - kk) : std::max<int64_t>(r * growth, kDenseRows);
+      const int64_t next = std::min(n, r + step);
+      launch_cosine_scan_gemm8(corpus8_.as<uint8_t>(), ld8(), live, r, next, q8, B, tau, cand, cnt,
+                               cap, s);
+      launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, next == n, asim, arow, 0, s, live);
+      r = next;
+    }
+  }
+  {
+    ProfScope prof("rescore", s, 2.0 * B * kk * dim_, (double)B * kk * ld_ * 2.0);
+    hipLaunchKernelGGL(rescore_kernel, dim3(B), dim3(256), 0, s, corpus_.as<half_t>(), ld_, dim_, qn,
+                       arow, kk, cand, cap, cnt);
+    SR_LAUNCH_CHECK();
+  }
+  launch_topk_select(cand, cnt, cap, tau, B, k, ovf, true, out_sim, out_rows, row_offset, s, live);
+}
+
 void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t* out_rows,
                          int64_t row_offset, hipStream_t s, bool safe, const uint8_t* live) {
+  if (fp8_) {
+    search_block8(qn, B, k, out_sim, out_rows, row_offset, s, safe, live);
+    return;
+  }
   const int cap = select_capacity();
   uint64_t* cand = cand_.as<uint64_t>();
   int* cnt = cnt_.as<int>();
@@ -192,20 +335,20 @@ void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t
   const int64_t n = n_rows_;
   if (n == 0) {
     launch_fill_int(cnt, B, 0, s);
-    launch_topk_select(cand, cnt, cap, tau, B, k, ovf, true, out_sim, out_rows, row_offset, s);
+    launch_topk_select(cand, cnt, cap, tau, B, k, ovf, true, out_sim, out_rows, row_offset, s, live);
     return;
   }
   const int64_t dense = std::min<int64_t>(n, safe ? (int64_t)(cap - k) : kDenseRows);
   launch_cosine_scan(true, C, ld_, live, 0, dense, qn, B, tau, cand, cnt, cap, s);
   launch_fill_int(cnt, B, (int)dense, s);
-  launch_topk_select(cand, cnt, cap, tau, B, k, ovf, dense == n, out_sim, out_rows, row_offset, s);
+  launch_topk_select(cand, cnt, cap, tau, B, k, ovf, dense == n, out_sim, out_rows, row_offset, s, live);
   const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(8, (cap - k) / (2 * k)));
   int64_t r = dense;
   while (r < n) {
     const int64_t step = safe ? (int64_t)(cap - k) : std::max<int64_t>(r * growth, kDenseRows);
     const int64_t next = std::min(n, r + step);
     launch_cosine_scan(false, C, ld_, live, r, next, qn, B, tau, cand, cnt, cap, s);
-    launch_topk_select(cand, cnt, cap, tau, B, k, ovf, next == n, out_sim, out_rows, row_offset, s);
+    launch_topk_select(cand, cnt, cap, tau, B, k, ovf, next == n, out_sim, out_rows, row_offset, s, live);
     r = next;
   }
 }
@@ -386,6 +529,10 @@ void Store::compact(int64_t* old_to_new) {
   n_rows_ = m;
   n_live_ = m;
   ++version_;
+  if (fp8_) {
+    quantize_rows(0, m, stream_);
+    SR_HIP(hipStreamSynchronize(stream_));
+  }
 }
 
 }  // namespace sr

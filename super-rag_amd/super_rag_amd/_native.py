@@ -22,6 +22,7 @@ SR_ERR_STATE = -5
 
 SR_DTYPE_F32 = 0
 SR_DTYPE_F16 = 1
+SR_DTYPE_FP8_E4M3 = 2
 SR_POOL_CLS = 0
 SR_POOL_MEAN = 1
 SR_MAX_TOPK = 1024
@@ -74,6 +75,7 @@ SIGNATURES = {
                                        c_void_p]),
     "sr_store_search_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                     c_int64, c_void_p]),
+    "sr_store_set_scan_dtype": (c_int, [c_void_p, c_int]),
     "sr_store_save": (c_int, [c_void_p, c_char_p]),
     "sr_store_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
     "sr_store_compact": (c_int, [c_void_p, c_void_p]),

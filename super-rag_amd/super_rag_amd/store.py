@@ -77,6 +77,12 @@ class NativeStore:
         N.call("sr_store_compact", self._h, N.ptr(m))
         return m[:n]
 
+    def set_scan_dtype(self, dtype: str) -> None:
+        """"fp16" (default) or "fp8": scan an OCP e4m3 copy of the rows with the block-scaled fp8
+        MFMA and re-score the candidates exactly on the fp16 rows (sr_store_set_scan_dtype)."""
+        code = {"fp16": N.SR_DTYPE_F16, "fp8": N.SR_DTYPE_FP8_E4M3}[dtype]
+        N.call("sr_store_set_scan_dtype", self._h, code)
+
     def save(self, path: str) -> None:
         N.call("sr_store_save", self._h, path.encode())
 

@@ -239,3 +239,39 @@ def test_masked_search_k_best_eligible_rows():
         assert sorted(row[: len(elig)].tolist()) == elig and (row[len(elig):] == -1).all()
     with pytest.raises(Exception):
         s.search(q, 10, allow=allow[:-1])
+
+
+@pytest.mark.parametrize("dim,B,k", [(768, 256, 10), (1024, 64, 100), (100, 7, 5), (64, 300, 1)])
+def test_fp8_scan_rescored_matches_fp16(dim, B, k):
+    # fp8 scan (block-scaled MFMA on e4m3 rows) + exact fp16 re-scoring of its top max(2k, k+32):
+    # the returned rows are the fp16 store's top k (recall), their distances exact fp16 scores.
+    n = 50_000
+    x = _clustered(n, dim, seed=21)
+    q = _queries(x, B, seed=22)
+    s16, s8 = _store(dim), _store(dim)
+    s16.add(x)
+    s8.add(x[: n // 2])
+    s8.set_scan_dtype("fp8")
+    s8.add(x[n // 2:])                      # rows added after the switch are quantised on add
+    dead = np.random.default_rng(3).choice(n, 500, replace=False)
+    s16.remove(dead)
+    s8.remove(dead)
+    d16, r16 = s16.search(q, k)
+    d8, r8 = s8.search(q, k)
+    assert recall_at_k(r8, r16) >= 0.99
+    assert not np.isin(r8, dead).any()
+    for b in range(B):
+        common = {int(r): i for i, r in enumerate(r16[b])}
+        for i, r in enumerate(r8[b]):
+            if int(r) in common:
+                assert abs(d8[b, i] - d16[b, common[int(r)]]) <= 2e-6
+    assert (np.diff(d8, axis=1) >= 0).all()
+    # compaction re-quantises; switching back to fp16 gives the fp16 results exactly
+    s8.compact()
+    s16.compact()
+    d8c, r8c = s8.search(q, k)
+    d16c, r16c = s16.search(q, k)
+    assert recall_at_k(r8c, r16c) >= 0.99
+    s8.set_scan_dtype("fp16")
+    d, r = s8.search(q, k)
+    np.testing.assert_array_equal(r, r16c)
