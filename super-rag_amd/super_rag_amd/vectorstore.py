@@ -172,12 +172,22 @@ class MI355XVectorStoreConnector:
         self.fulltext = bool(ctx.get("fulltext", False)) or self.hybrid
         self.hybrid_k_each = ctx.get("hybrid_k_each")
         self.rrf_rank_const = int(ctx.get("rrf_rank_const", 1))
+        self.scan_dtype = str(ctx.get("scan_dtype", "fp16"))   # "fp8": e4m3 scan + fp16 re-score
         self.store = self
         if self.snapshot_dir and _get(self.collection_name) is None:
             c = _Collection.restore(self.collection_name, self.snapshot_dir, self.device)
             if c is not None:
                 with _registry_lock:
                     _collections.setdefault(self.collection_name, c)
+        c = _get(self.collection_name)
+        if c is not None:
+            self._apply_scan_dtype(c)
+
+    def _apply_scan_dtype(self, c: _Collection) -> None:
+        if getattr(c, "scan_dtype", "fp16") != self.scan_dtype and hasattr(c.store, "set_scan_dtype"):
+            with c.lock:
+                c.store.set_scan_dtype(self.scan_dtype)
+                c.scan_dtype = self.scan_dtype
 
     # -- collection lifecycle ---------------------------------------------------------------------
     def _get_or_create(self, dim: int) -> _Collection:
@@ -186,7 +196,8 @@ class MI355XVectorStoreConnector:
             if c is None:
                 c = _Collection(self.collection_name, int(dim), self.device)
                 _collections[self.collection_name] = c
-            return c
+        self._apply_scan_dtype(c)
+        return c
 
     def create_collection(self, **kwargs: Any):
         vector_size = int(kwargs.get("vector_size") or self.vector_size)
