@@ -150,6 +150,25 @@ int sr_lex_stats(sr_lex* x, int64_t* n_rows, int64_t* n_live, int64_t* n_posting
  * sr_store_search_masked. */
 int sr_lex_search(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
                   const uint8_t* allow, int64_t mask_key, float* out_score, int64_t* out_rows);
+/* Corpus-wide statistics of a row-sharded lexical corpus, so every shard scores with the same N,
+ * avgdl and document frequencies (then per-shard results merge into exactly one index's):
+ * n_live / sum_dl summed over the shards (sr_lex_totals), df[i] of terms[i] summed (sr_lex_df)
+ * for every term of the queries. */
+typedef struct sr_lex_global {
+  int64_t n_live;
+  int64_t sum_dl;
+  const int32_t* terms;
+  const int64_t* df;
+  int n_terms;
+} sr_lex_global;
+int sr_lex_totals(sr_lex* x, int64_t* n_live, int64_t* sum_dl);
+int sr_lex_df(sr_lex* x, const int32_t* terms, int n, int64_t* out_df);
+/* Device outputs (B x k on the index's device, score fp32 / row int64 + row_offset; -inf / -1 past
+ * the matches), asynchronous on `stream` after the host-side term preparation; global may be NULL
+ * (this index's own statistics). */
+int sr_lex_search_dev(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                      const sr_lex_global* global, float* out_score, int64_t* out_rows,
+                      int64_t row_offset, void* stream);
 int sr_lex_save(sr_lex* x, const char* path);
 int sr_lex_load(const char* path, int device, sr_lex** out);
 int sr_lex_compact(sr_lex* x, int64_t* old_to_new);
@@ -162,6 +181,10 @@ void sr_lex_destroy(sr_lex* x);
 int sr_rrf_fuse(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
                 int rank_const, double min_score, int k_out, double* out_score,
                 int64_t* out_rows, int device);
+/* Same on device buffers, asynchronous on `stream` of `device`. */
+int sr_rrf_fuse_dev(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
+                    int rank_const, double min_score, int k_out, double* out_score,
+                    int64_t* out_rows, int device, void* stream);
 /* Hybrid retrieval on one device: dense top-k_each (sr_store_search semantics) and BM25
  * top-k_each of the same queries, fused on the device by rrf into B x k (out_score = rrf score).
  * q: B x dim host fp32; the lexical query as in sr_lex_search; allow optional (mask_key as in

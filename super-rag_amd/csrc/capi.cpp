@@ -353,6 +353,44 @@ int sr_lex_search(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, 
   SR_API_END
 }
 
+int sr_lex_totals(sr_lex* x, int64_t* n_live, int64_t* sum_dl) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->totals(n_live, sum_dl);
+  SR_API_END
+}
+
+int sr_lex_df(sr_lex* x, const int32_t* terms, int n, int64_t* out_df) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  SR_CHECK(n >= 0, "lex.df: negative count");
+  if (n > 0) {
+    SR_NONNULL(terms);
+    SR_NONNULL(out_df);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->df(terms, n, out_df);
+  SR_API_END
+}
+
+int sr_lex_search_dev(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                      const sr_lex_global* global, float* out_score, int64_t* out_rows,
+                      int64_t row_offset, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  if (B > 0) {
+    SR_NONNULL(qoff);
+    SR_NONNULL(out_score);
+    SR_NONNULL(out_rows);
+    if (qoff[B] > 0) SR_NONNULL(qterms);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->search_dev(qoff, qterms, B, k, nullptr, 0, out_score, out_rows,
+                      reinterpret_cast<hipStream_t>(stream), global, row_offset);
+  SR_API_END
+}
+
 int sr_lex_save(sr_lex* x, const char* path) {
   SR_API_BEGIN
   SR_NONNULL(x);
@@ -420,6 +458,20 @@ int sr_rrf_fuse(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, in
     throw;
   }
   SR_HIP(hipStreamDestroy(st));
+  SR_API_END
+}
+
+int sr_rrf_fuse_dev(const int64_t* rows_a, int ka, const int64_t* rows_b, int kb, int B,
+                    int rank_const, double min_score, int k_out, double* out_score,
+                    int64_t* out_rows, int device, void* stream) {
+  SR_API_BEGIN
+  SR_CHECK(B >= 0, "rrf: negative batch");
+  if (B == 0) return SR_OK;
+  SR_NONNULL(out_score);
+  SR_NONNULL(out_rows);
+  sr::DeviceGuard g(device);
+  sr::launch_rrf_fuse(rows_a, ka, rows_b, kb, B, rank_const, min_score, k_out, out_score, out_rows,
+                      reinterpret_cast<hipStream_t>(stream));
   SR_API_END
 }
 

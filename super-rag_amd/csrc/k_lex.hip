@@ -212,7 +212,7 @@ struct LexSelSmem {
 __global__ __launch_bounds__(SEL_THREADS, 1) void lex_select_kernel(
     const uint64_t* __restrict__ keys, const int* __restrict__ kcnt,
     const int64_t* __restrict__ koff, int k, float* __restrict__ out_score,
-    int64_t* __restrict__ out_rows) {
+    int64_t* __restrict__ out_rows, int64_t row_offset) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   LexSelSmem& S = *reinterpret_cast<LexSelSmem*>(smem_raw);
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(SEL_THREADS, 1) void lex_select_kernel(
     const bool ok = i < m;
     const uint64_t kk = ok ? S.sh.sel[i] : 0ull;
     out_score[(int64_t)q * k + i] = ok ? (float)(uint32_t)(kk >> 32) / LEX_SCALE : -INFINITY;
-    out_rows[(int64_t)q * k + i] = ok ? (int64_t)(0xffffffffu - (uint32_t)kk) : -1;
+    out_rows[(int64_t)q * k + i] = ok ? (int64_t)(0xffffffffu - (uint32_t)kk) + row_offset : -1;
   }
 }
 
@@ -524,19 +524,36 @@ const uint8_t* LexIndex::eligibility(const uint8_t* allow, int64_t mask_key, hip
   return mask_.as<uint8_t>();
 }
 
-float LexIndex::idf(int64_t df) const {
+float LexIndex::idf(int64_t df, int64_t n_live) {
   // Lucene's BM25 idf (always positive), in double then rounded to fp32 once.
-  const double N = (double)live_n_, d = (double)df;
+  const double N = (double)n_live, d = (double)df;
   return (float)std::log(1.0 + (N - d + 0.5) / (d + 0.5));
 }
 
-float LexIndex::avgdl() const {
-  return live_n_ > 0 ? (float)((double)sum_dl_ / (double)live_n_) : 1.f;
+float LexIndex::avgdl(int64_t sum_dl, int64_t n_live) {
+  return n_live > 0 ? (float)((double)sum_dl / (double)n_live) : 1.f;
+}
+
+void LexIndex::totals(int64_t* n_live, int64_t* sum_dl) const {
+  if (n_live) *n_live = live_n_;
+  if (sum_dl) *sum_dl = sum_dl_;
+}
+
+void LexIndex::df(const int32_t* terms, int n, int64_t* out) {
+  DeviceGuard g(device_);
+  begin(stream_);
+  rebuild(stream_);
+  end(stream_);
+  for (int i = 0; i < n; ++i) {
+    const int32_t t = terms[i];
+    out[i] = (t >= 0 && t < vocab_) ? df_host_[(size_t)t] : 0;
+  }
 }
 
 void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k,
                           const uint8_t* allow, int64_t mask_key, float* out_score,
-                          int64_t* out_rows, hipStream_t s) {
+                          int64_t* out_rows, hipStream_t s, const sr_lex_global* glob,
+                          int64_t row_offset) {
   SR_CHECK(B >= 0, "lex.search: negative batch");
   SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "lex.search: top_k must be in [1, 1024]");
   if (B == 0) return;
@@ -570,12 +587,31 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
     }
     cap[(size_t)b] = std::min<int64_t>(cap[(size_t)b], rows_);
   }
+  // statistics: this index's live rows, or the caller's corpus-wide ones (row-sharded corpus:
+  // every shard then scores with the same N, avgdl and df, so merged results equal one index's)
+  int64_t N_live = live_n_, sum_dl = sum_dl_;
+  std::vector<std::pair<int32_t, int64_t>> gdf;
+  if (glob) {
+    SR_CHECK(glob->n_live >= 0 && glob->sum_dl >= 0 && (glob->n_terms == 0 || (glob->terms && glob->df)),
+             "lex.search: invalid global statistics");
+    N_live = glob->n_live;
+    sum_dl = glob->sum_dl;
+    gdf.reserve((size_t)glob->n_terms);
+    for (int i = 0; i < glob->n_terms; ++i) gdf.push_back({glob->terms[i], glob->df[i]});
+    std::sort(gdf.begin(), gdf.end());
+  }
+  auto term_df = [&](int32_t t) -> int64_t {
+    if (!glob) return df_host_[(size_t)t];
+    auto it = std::lower_bound(gdf.begin(), gdf.end(), std::make_pair(t, (int64_t)INT64_MIN));
+    SR_CHECK(it != gdf.end() && it->first == t, "lex.search: query term missing from the global df table");
+    return it->second;
+  };
   // query blocks: candidate keys within LEX_KEY_BUDGET; grid (queries, row blocks), so the
   // workgroups in flight belong to many queries
   const int64_t rows = std::max<int64_t>(rows_, 1);
   const int NB = (int)ceil_div(rows, LEX_RB);
   SR_CHECK(NB <= 65535, "lex.search: more than 2^30 rows per index");
-  const float adl = avgdl();
+  const float adl = avgdl(sum_dl, N_live);
   static bool attr_set = false;
   if (!attr_set) {
     SR_HIP(hipFuncSetAttribute((const void*)lex_score_kernel,
@@ -597,7 +633,7 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
       koff[(size_t)i + 1] = koff[(size_t)i] + cap[(size_t)(b0 + i)];
       for (const QT& e : qt[(size_t)(b0 + i)]) {
         const int64_t len = df_host_[(size_t)e.term];
-        slots.push_back({off_host_[(size_t)e.term], (int32_t)len, idf(len), e.mult, 0});
+        slots.push_back({off_host_[(size_t)e.term], (int32_t)len, idf(term_df(e.term), N_live), e.mult, 0});
         scored += len;
       }
       slot_off[(size_t)i + 1] = (int)slots.size();
@@ -642,7 +678,7 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
       ProfScope prof("lex_select", s, 0.0, (double)koff[(size_t)qb] * 8.0);
       hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), sizeof(LexSelSmem), s,
                          d_keys, d_cnt, d_ko, k, out_score + (int64_t)b0 * k,
-                         out_rows + (int64_t)b0 * k);
+                         out_rows + (int64_t)b0 * k, row_offset);
       SR_LAUNCH_CHECK();
     }
     // the host vectors above back async copies: finish the block before they go away

@@ -187,7 +187,10 @@ class LexIndex {
   // query b: terms qterms[qoff[b] .. qoff[b+1]) (repeats count); outputs on the device (search_dev,
   // on stream s) or the host
   void search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
-                  int64_t mask_key, float* out_score, int64_t* out_rows, hipStream_t s);
+                  int64_t mask_key, float* out_score, int64_t* out_rows, hipStream_t s,
+                  const sr_lex_global* glob = nullptr, int64_t row_offset = 0);
+  void totals(int64_t* n_live, int64_t* sum_dl) const;
+  void df(const int32_t* terms, int n, int64_t* out);
   void search_host(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
                    int64_t mask_key, float* out_score, int64_t* out_rows);
   void stats(int64_t* rows, int64_t* live, int64_t* postings, int64_t* vocab, double* avgdl);
@@ -203,8 +206,8 @@ class LexIndex {
  private:
   void rebuild(hipStream_t s);
   const uint8_t* eligibility(const uint8_t* allow, int64_t mask_key, hipStream_t s);
-  float idf(int64_t df) const;
-  float avgdl() const;
+  static float idf(int64_t df, int64_t n_live);
+  static float avgdl(int64_t sum_dl, int64_t n_live);
   void forward(std::vector<int32_t>& fterm, std::vector<uint64_t>& fval);
   void load_rows(const std::vector<int32_t>& dl, const std::vector<uint8_t>& live,
                  const std::vector<int32_t>& ft, const std::vector<uint64_t>& fv);

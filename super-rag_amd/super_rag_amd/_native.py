@@ -86,12 +86,18 @@ SIGNATURES = {
     "sr_lex_stats": (c_int, [c_void_p, P_I64, P_I64, P_I64, P_I64, POINTER(c_double)]),
     "sr_lex_search": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64,
                               c_void_p, c_void_p]),
+    "sr_lex_totals": (c_int, [c_void_p, P_I64, P_I64]),
+    "sr_lex_df": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "sr_lex_search_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_int64, c_void_p]),
     "sr_lex_save": (c_int, [c_void_p, c_char_p]),
     "sr_lex_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
     "sr_lex_compact": (c_int, [c_void_p, c_void_p]),
     "sr_lex_destroy": (None, [c_void_p]),
     "sr_rrf_fuse": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_double, c_int,
                             c_void_p, c_void_p, c_int]),
+    "sr_rrf_fuse_dev": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_double, c_int,
+                                c_void_p, c_void_p, c_int, c_void_p]),
     "sr_hybrid_search": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                  c_int, c_int, c_double, c_void_p, c_int64, c_void_p, c_void_p]),
     "sr_topk_merge_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,

@@ -91,6 +91,12 @@ def query_arrays(queries: Sequence[Sequence[int]]):
     return qoff, qterms
 
 
+class LexGlobalC(ctypes.Structure):
+    """sr_lex_global: corpus-wide statistics of a row-sharded lexical corpus."""
+    _fields_ = [("n_live", ctypes.c_int64), ("sum_dl", ctypes.c_int64), ("terms", ctypes.c_void_p),
+                ("df", ctypes.c_void_p), ("n_terms", ctypes.c_int)]
+
+
 def _mask(allow, n_rows: int):
     a = np.ascontiguousarray(np.asarray(allow, dtype=np.uint8))
     if a.shape != (n_rows,):
@@ -183,6 +189,45 @@ class NativeLexIndex:
                None if a is None else N.ptr(a), int(mask_key), N.ptr(scores), N.ptr(rows))
         return scores, rows
 
+    def totals(self):
+        """(live rows, summed document length) of this index."""
+        n, d = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.call("sr_lex_totals", self._h, ctypes.byref(n), ctypes.byref(d))
+        return int(n.value), int(d.value)
+
+    def df(self, terms) -> np.ndarray:
+        """Live document frequency of each term id (0 for unknown terms)."""
+        t = np.ascontiguousarray(np.asarray(terms, dtype=np.int32))
+        out = np.zeros(t.shape[0], dtype=np.int64)
+        if t.size:
+            N.call("sr_lex_df", self._h, N.ptr(t), t.shape[0], N.ptr(out))
+        return out
+
+    def search_dev(self, qoff, qterms, k: int, global_stats=None, row_offset: int = 0,
+                   out_score=None, out_rows=None, stream=None):
+        """Device outputs: (score [B,k] fp32, rows [B,k] int64 + row_offset) torch tensors.
+        qoff / qterms: host arrays (query_arrays); global_stats: (n_live, sum_dl, terms, df) of the
+        whole row-sharded corpus, or None for this index's own statistics."""
+        import torch
+        qoff = np.ascontiguousarray(qoff, dtype=np.int64)
+        qterms = np.ascontiguousarray(qterms, dtype=np.int32)
+        Bq = len(qoff) - 1
+        dev = torch.device("cuda", self.device)
+        if out_score is None:
+            out_score = torch.empty((Bq, k), dtype=torch.float32, device=dev)
+        if out_rows is None:
+            out_rows = torch.empty((Bq, k), dtype=torch.int64, device=dev)
+        g = None
+        if global_stats is not None:
+            n_live, sum_dl, gt, gdf = global_stats
+            gt = np.ascontiguousarray(gt, dtype=np.int32)
+            gdf = np.ascontiguousarray(gdf, dtype=np.int64)
+            g = LexGlobalC(int(n_live), int(sum_dl), gt.ctypes.data, gdf.ctypes.data, int(gt.size))
+        N.call("sr_lex_search_dev", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+               None if g is None else ctypes.byref(g), N.ptr(out_score), N.ptr(out_rows),
+               int(row_offset), N.stream_handle(stream))
+        return out_score, out_rows
+
     def hybrid(self, store, queries, query_terms, k: int, k_each: Optional[int] = None,
                rank_const: int = 1, min_score: float = float("-inf"), allow=None, mask_key: int = 0):
         """hybrid_search over (store, this index)."""
@@ -202,6 +247,21 @@ def rrf_fuse(rows_a, rows_b, k: int, rank_const: int = 1, min_score: float = 0.0
     rows = np.empty((Bq, k), dtype=np.int64)
     N.call("sr_rrf_fuse", N.ptr(a), a.shape[1], N.ptr(b), b.shape[1], Bq, int(rank_const),
            float(min_score), int(k), N.ptr(scores), N.ptr(rows), int(device))
+    return scores, rows
+
+
+def rrf_fuse_dev(rows_a, rows_b, k: int, rank_const: int = 1, min_score: float = float("-inf"),
+                 stream=None):
+    """rrf of two ranked row lists per query on the device (torch int64 [B, ka], [B, kb], -1
+    padded) -> (score [B, k] fp64, rows [B, k] int64) device tensors."""
+    import torch
+    a, b = rows_a.contiguous(), rows_b.contiguous()
+    Bq = a.shape[0]
+    scores = torch.empty((Bq, k), dtype=torch.float64, device=a.device)
+    rows = torch.empty((Bq, k), dtype=torch.int64, device=a.device)
+    N.call("sr_rrf_fuse_dev", N.ptr(a), a.shape[1], N.ptr(b), b.shape[1], Bq, int(rank_const),
+           float(min_score), int(k), N.ptr(scores), N.ptr(rows), a.device.index or 0,
+           N.stream_handle(stream))
     return scores, rows
 
 

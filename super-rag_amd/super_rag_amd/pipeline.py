@@ -9,6 +9,12 @@ all-gathered (C1), every rank scans its shard for all world*B queries, the per-s
 are exchanged with one all_to_all (C2: each rank receives the lists of ITS queries) and merged by
 K2, and each rank reranks its own B queries.  Passage tokens for the cross-encoder are replicated
 per GPU (N x Lp int32, 3.8 GB at 10M x 94) so the pair packer never crosses ranks.
+
+Hybrid mode (``lexical=`` a NativeLexIndex over the shard's rows, BASELINE config 5): the rerank
+candidates are the rrf fusion (graphiti rrf, search_utils.py:1762-1778) of the dense top-k_each and
+the BM25 top-k_each of the query tokens.  Sharded, every shard scores BM25 with the corpus-wide N,
+avgdl and document frequencies (all-reduced per batch), both per-shard lists go through the same
+all_to_all + K2 merge, so the fused candidates equal a single index's.
 """
 from __future__ import annotations
 
@@ -25,14 +31,16 @@ class PipelineResult:
     rows: torch.Tensor         # [B, k_final] int64 global row ids (reranked order)
     logits: torch.Tensor       # [B, k_final] fp32 cross-encoder logits
     cand_rows: torch.Tensor    # [B, K] int64 search candidates (distance order)
-    cand_sims: torch.Tensor    # [B, K] fp32 cosine similarity (distance = 1 - sim)
+    cand_sims: torch.Tensor    # [B, K] fp32 cosine similarity (distance = 1 - sim); rrf score
+                               # of the fused candidates in hybrid mode
 
 
 class SearchPipeline:
     def __init__(self, embedder: Encoder, reranker: Encoder, store: NativeStore,
                  passage_tok: torch.Tensor, passage_len: torch.Tensor, k_candidates: int = 100,
                  k_final: int = 10, pair_len: int = 128, shard_offset: int = 0, group=None,
-                 merge_fn=topk_merge_dev):
+                 merge_fn=topk_merge_dev, lexical=None, k_each: int | None = None,
+                 rank_const: int = 1):
         self.embedder = embedder
         self.reranker = reranker
         self.store = store
@@ -44,6 +52,9 @@ class SearchPipeline:
         self.offset = int(shard_offset)
         self.group = group
         self.merge_fn = merge_fn
+        self.lexical = lexical
+        self.k_each = int(k_each or self.K)
+        self.rank_const = int(rank_const)
         import torch.distributed as dist
         self.world = dist.get_world_size(group) if (group is not None or
                                                      (dist.is_available() and dist.is_initialized())) else 1
@@ -66,6 +77,10 @@ class SearchPipeline:
         dist.all_gather_into_tensor(allq, qx, group=self.group)
         sims, rows = self.store.search_dev(allq.to(dev) if host else allq, self.K,
                                            row_offset=self.offset)
+        return self._exchange(sims, rows, B, self.K, host, dev)
+
+    def _exchange(self, sims, rows, B, k, host, dev):
+        import torch.distributed as dist
         if host:
             sims, rows = sims.cpu(), rows.cpu()
         rs = torch.empty_like(sims)
@@ -74,8 +89,54 @@ class SearchPipeline:
         dist.all_to_all_single(rr, rows, group=self.group)
         if host:
             rs, rr = rs.to(dev), rr.to(dev)
-        return self.merge_fn(rs.view(self.world, B, self.K), rr.view(self.world, B, self.K),
-                             self.K, device=q_emb.device.index or 0)
+        return self.merge_fn(rs.view(self.world, B, k), rr.view(self.world, B, k), k,
+                             device=dev.index or 0)
+
+    def retrieve_hybrid(self, q_emb: torch.Tensor, q_tok: torch.Tensor, q_len: torch.Tensor):
+        """Dense top-k_each + BM25 top-k_each (query tokens) fused by rrf -> (rrf score, rows)
+        [B, K] of this rank's queries."""
+        import numpy as np
+        from .lexical import query_arrays, rrf_fuse_dev
+        B = q_emb.shape[0]
+        dev = q_emb.device
+        ke = self.k_each
+        if self.world == 1:
+            allq, toks, lens = q_emb, q_tok, q_len
+        else:
+            import torch.distributed as dist
+            host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda
+
+            def gather(x):
+                x = x.contiguous().cpu() if host else x.contiguous()
+                out = torch.empty((self.world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype,
+                                  device=x.device)
+                dist.all_gather_into_tensor(out, x, group=self.group)
+                return out.to(dev) if host else out
+            allq, toks, lens = gather(q_emb), gather(q_tok), gather(q_len)
+        t_np, l_np = toks.cpu().numpy(), lens.cpu().numpy()
+        queries = [t_np[i, :l_np[i]] for i in range(t_np.shape[0])]
+        qoff, qterms = query_arrays(queries)
+        stats = None
+        if self.world > 1:
+            import torch.distributed as dist
+            host = dist.get_backend(self.group) == "gloo"
+            terms = np.unique(qterms[: qoff[-1]]).astype(np.int32)
+            n_live, sum_dl = self.lexical.totals()
+            v = torch.from_numpy(np.concatenate([[n_live, sum_dl], self.lexical.df(terms)]).astype(np.int64))
+            v = v if host else v.to(dev)
+            dist.all_reduce(v, group=self.group)
+            v = v.cpu().numpy()
+            stats = (int(v[0]), int(v[1]), terms, v[2:])
+        sims, rows = self.store.search_dev(allq, ke, row_offset=self.offset)
+        lsc, lrows = self.lexical.search_dev(qoff, qterms, ke, global_stats=stats,
+                                             row_offset=self.offset)
+        if self.world > 1:
+            import torch.distributed as dist
+            host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda
+            sims, rows = self._exchange(sims, rows, B, ke, host, dev)
+            lsc, lrows = self._exchange(lsc, lrows, B, ke, host, dev)
+        score, fused = rrf_fuse_dev(rows, lrows, self.K, self.rank_const)
+        return score.float(), fused
 
     def rerank(self, q_tok: torch.Tensor, q_len: torch.Tensor, cand_rows: torch.Tensor):
         B = cand_rows.shape[0]
@@ -89,6 +150,9 @@ class SearchPipeline:
 
     def run(self, q_ids, q_mask, q_tok, q_len) -> PipelineResult:
         q = self.embed(q_ids, q_mask)
-        sims, rows = self.retrieve(q)
+        if self.lexical is not None:
+            sims, rows = self.retrieve_hybrid(q, q_tok, q_len)
+        else:
+            sims, rows = self.retrieve(q)
         final_rows, final_logits = self.rerank(q_tok, q_len, rows)
         return PipelineResult(final_rows, final_logits, rows, sims)

@@ -69,6 +69,49 @@ def test_pipeline_stages_match_oracle(res16):
         np.testing.assert_allclose(flog[b], lg_ref[b, [got[r] for r in final[b]]], atol=tol)
 
 
+def test_hybrid_pipeline_candidates_are_rrf_of_dense_and_bm25():
+    # hybrid SearchPipeline (config 5): candidates = rrf(dense top-k_each, BM25 top-k_each over the
+    # passage tokens with the query tokens); BM25 side against the oracle, bit-exact
+    import torch
+    from oracle.bm25 import LexCorpus, bm25_topk, rrf_rows
+    from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
+    from super_rag_amd.lexical import NativeLexIndex, doc_arrays
+    from super_rag_amd.pipeline import SearchPipeline
+    from super_rag_amd.store import NativeStore
+    es = ModelSpec("e", "bert", 2000, 128, 2, 2, 256, 64, 2, 1e-12, 0)
+    rs = ModelSpec("r", "xlmr", 600, 128, 2, 2, 256, 80, 1, 1e-5, 1, classifier=1, bos_id=0,
+                   eos_id=2, pad_id=1, residual_fp16=True)
+    emb, rer = Encoder(es, weights=random_weights(es, 1, "test")), Encoder(rs, weights=random_weights(rs, 2, "test"))
+    rng = np.random.default_rng(4)
+    N, B, K, ke, k, S = 12000, 16, 40, 30, 5, 48
+    corpus = rng.standard_normal((N, 128)).astype(np.float32)
+    p_tok = ((rng.zipf(1.3, (N, 40)) - 1) % 590 + 5).astype(np.int32)
+    p_len = rng.integers(1, 41, N).astype(np.int32)
+    store = NativeStore(128)
+    store.add(corpus)
+    docs = [p_tok[i, :p_len[i]].tolist() for i in range(N)]
+    lex = NativeLexIndex()
+    lex.add(docs)
+    q_ids = rng.integers(5, 2000, (B, 16)).astype(np.int32)
+    q_ids[:, 0] = 101
+    q_tok = ((rng.zipf(1.3, (B, 10)) - 1) % 590 + 5).astype(np.int32)
+    q_len = rng.integers(1, 11, B).astype(np.int32)
+    t = lambda a: torch.from_numpy(a).cuda()
+    pipe = SearchPipeline(emb, rer, store, t(p_tok), t(p_len), k_candidates=K, k_final=k,
+                          pair_len=S, lexical=lex, k_each=ke)
+    res = pipe.run(t(q_ids), t(np.ones_like(q_ids)), t(q_tok), t(q_len))
+    q16 = pipe.embed(t(q_ids), t(np.ones_like(q_ids)))
+    _, dense = store.search_dev(q16, ke)
+    queries = [q_tok[i, :q_len[i]].tolist() for i in range(B)]
+    _, lexical = bm25_topk(LexCorpus(*doc_arrays(docs)), queries, ke)
+    so, ro = rrf_rows(dense.cpu().numpy(), lexical, K, 1)
+    np.testing.assert_array_equal(res.cand_rows.cpu().numpy(), ro)
+    np.testing.assert_allclose(res.cand_sims.cpu().numpy(), so.astype(np.float32))
+    final = res.rows.cpu().numpy()
+    for b in range(B):
+        assert set(final[b].tolist()) <= set(ro[b].tolist())
+
+
 def _sharded_worker(rank, world, port, out_q):
     # one rank of a world-size-2 SearchPipeline sharing the box's GPU (gloo exchange staged through
     # host memory; the same code runs over RCCL, one rank per GPU, in bench.py)
@@ -83,13 +126,14 @@ def _sharded_worker(rank, world, port, out_q):
     try:
         torch.cuda.set_device(0)
         res = _run_pipeline(rank, world)
-        out_q.put((rank, res))
+        res_h = _run_pipeline(rank, world, hybrid=True)
+        out_q.put((rank, (res, res_h)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def _run_pipeline(rank, world, sharded=True):
+def _run_pipeline(rank, world, sharded=True, hybrid=False):
     # rank's B queries; sharded: over rows [r0, r1) of the corpus (shard_offset r0) inside a
     # world-size process group, else over the whole corpus in a single process
     import torch
@@ -115,8 +159,16 @@ def _run_pipeline(rank, world, sharded=True):
     store = NativeStore(128)
     store.add(corpus[r0:r1])
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    lex = None
+    if hybrid:
+        # BM25 over the shard's passage tokens (ids folded onto a small Zipf vocabulary so
+        # documents share terms); corpus-wide statistics are all-reduced by the pipeline
+        from super_rag_amd.lexical import NativeLexIndex
+        lex = NativeLexIndex()
+        lex.add([(p_tok[i, :p_len[i]] % 97 + 5).tolist() for i in range(r0, r1)])
+        q_tok = q_tok % 97 + 5
     pipe = SearchPipeline(emb, rer, store, t(p_tok), t(p_len), k_candidates=K, k_final=k,
-                          pair_len=S, shard_offset=r0)
+                          pair_len=S, shard_offset=r0, lexical=lex, k_each=16 if hybrid else None)
     mine = slice(rank * B, (rank + 1) * B)
     res = pipe.run(t(q_ids[mine]), t(np.ones_like(q_ids[mine])), t(q_tok[mine]), t(q_len[mine]))
     torch.cuda.synchronize()
@@ -136,7 +188,9 @@ def test_two_rank_sharded_pipeline_equals_single_process():
     procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(world))
+    got_both = dict(q.get(timeout=240) for _ in range(world))
+    got = {r: v[0] for r, v in got_both.items()}
+    got_h = {r: v[1] for r, v in got_both.items()}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -144,6 +198,12 @@ def test_two_rank_sharded_pipeline_equals_single_process():
     import torch.distributed as dist
     assert not dist.is_initialized()
     full = {r: _run_pipeline(r, world, sharded=False) for r in range(world)}
+    full_h = {r: _run_pipeline(r, world, sharded=False, hybrid=True) for r in range(world)}
+    for r in range(world):
+        # hybrid: global BM25 statistics make the sharded fused candidates equal one index's
+        np.testing.assert_array_equal(got_h[r]["cand_rows"], full_h[r]["cand_rows"])
+        np.testing.assert_array_equal(got_h[r]["cand_sims"], full_h[r]["cand_sims"])
+        np.testing.assert_array_equal(got_h[r]["rows"], full_h[r]["rows"])
     for r in range(world):
         np.testing.assert_array_equal(got[r]["cand_rows"], full[r]["cand_rows"])
         np.testing.assert_allclose(got[r]["cand_sims"], full[r]["cand_sims"], atol=1e-6)
