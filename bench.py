@@ -49,9 +49,40 @@ def parse():
     ap.add_argument("--cpu-queries", type=int, default=2)
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
+    ap.add_argument("--workload", default="config4", choices=["config4", "config5"],
+                    help="config4 (default, the BASELINE metric) or config5: bge-m3 embed, 6.25M x "
+                         "1024 rows per GPU scanned in fp8, BM25 over the passage tokens fused by "
+                         "rrf (hybrid), rerank")
     ap.add_argument("--dist-backend", default=os.environ.get("SR_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.workload == "config5":
+        a.embed_model, a.dim = "bge-m3", 1024
+        if a.corpus_rows == 10_000_000:  # default: the 50M / 8-GPU shard size per GPU (weak)
+            a.corpus_rows = 6_250_000 * int(os.environ.get("WORLD_SIZE", "1"))
+        a.no_cpu_baseline = True
+    return a
+
+
+def build_lexical(p_tok, p_len, device):
+    """BM25 index of passage-token rows (device [n, L] int32, full length): each row's distinct
+    tokens and counts are found on the GPU (sort + run starts), then handed to sr_lex_add."""
+    from super_rag_amd.lexical import NativeLexIndex
+    lex = NativeLexIndex(device=device)
+    n, L = p_tok.shape
+    step = 1 << 20
+    for c0 in range(0, n, step):
+        t, _ = torch.sort(p_tok[c0:c0 + step].long(), dim=1)
+        new = torch.ones_like(t, dtype=torch.bool)
+        new[:, 1:] = t[:, 1:] != t[:, :-1]
+        flat = new.flatten()
+        starts = torch.nonzero(flat).flatten()
+        ends = torch.cat([starts[1:], torch.tensor([flat.numel()], device=t.device)])
+        off = torch.zeros(t.shape[0] + 1, dtype=torch.int64, device=t.device)
+        off[1:] = torch.cumsum(new.sum(1), 0)
+        lex.add_arrays(off.cpu().numpy(), t.flatten()[flat].int().cpu().numpy(),
+                       (ends - starts).int().cpu().numpy(), p_len[c0:c0 + step].cpu().numpy())
+    return lex
 
 
 def gen_corpus_chunk(r0, r1, dim, centers, dev):
@@ -116,6 +147,8 @@ def main():
         store.add_dev(chunk)
         del chunk
     torch.cuda.synchronize()
+    if a.workload == "config5":
+        store.set_scan_dtype("fp8")   # config 5: the fp8 MFMA scan (exact fp16 re-scoring)
     # replicated passage token table for the cross-encoder (content tokens, no specials)
     gp = torch.Generator(device=dev)
     gp.manual_seed(5)
@@ -138,8 +171,10 @@ def main():
                              dtype=torch.int32)
         qlen = torch.full((a.batch,), lq, dtype=torch.int32, device=dev)
         batches.append((ids, mask, qtok, qlen))
+    lexical = build_lexical(p_tok[r0:r1], p_len[r0:r1], local) if a.workload == "config5" else None
     pipe = SearchPipeline(embedder, reranker, store, p_tok, p_len, k_candidates=a.k_cand,
-                          k_final=a.k, pair_len=a.pair_len, shard_offset=r0)
+                          k_final=a.k, pair_len=a.pair_len, shard_offset=r0, lexical=lexical,
+                          k_each=a.k_cand)
     setup_s = time.time() - t_setup
 
     # ---- warmup + timed region -----------------------------------------------------------------
@@ -231,14 +266,22 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, es, rs, w_embed, w_rerank, centers.cpu(), batches[0], p_tok, N_total)
 
+    workload = ("config4: bge-base-en embed (S=32) + exact cosine top-100 over "
+                f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
+                f"rerank of 100 pairs (S={a.pair_len}) -> top-{a.k}")
+    metric = "queries/sec (embed+ANN top-10+rerank) over 10M x 768-d; recall@10"
+    if a.workload == "config5":
+        workload = (f"config5: bge-m3 embed (S={a.q_len}) + fp8 cosine top-{a.k_cand} over "
+                    f"{N_total} x {a.dim} rows (row-sharded, fp16 re-scored) + BM25 top-{a.k_cand} "
+                    f"over the passage tokens, rrf-fused on the device + {a.rerank_model} rerank of "
+                    f"{a.k_cand} pairs (S={a.pair_len}) -> top-{a.k}")
+        metric = "queries/sec (config 5: bge-m3 embed + hybrid fp8-dense/BM25 retrieval + rerank)"
     line = {
-        "metric": "queries/sec (embed+ANN top-10+rerank) over 10M x 768-d; recall@10",
+        "metric": metric,
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f16", "data": "synthetic",
-        "config": {"workload": "config4: bge-base-en embed (S=32) + exact cosine top-100 over "
-                               f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
-                               f"rerank of 100 pairs (S={a.pair_len}) -> top-{a.k}",
+        "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
                    "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
                    "parallelism": f"corpus row-shard x{world}, query DP x{world}"},
