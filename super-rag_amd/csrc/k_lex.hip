@@ -130,19 +130,51 @@ __global__ __launch_bounds__(LEX_THREADS) void lex_score_kernel(
   extern __shared__ __attribute__((aligned(16))) uint32_t acc[];
   const int q = blockIdx.x, blk = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int s0 = slot_off[q], s1 = slot_off[q + 1];
-  int total = 0;
-  for (int t = s0; t < s1; ++t)
-    total += bnd[(int64_t)t * (NB + 1) + blk + 1] - bnd[(int64_t)t * (NB + 1) + blk];
-  if (total == 0) return;  // uniform: no posting of this query in this row block
-  for (int i = tid; i < LEX_RB; i += LEX_THREADS) acc[i] = 0u;
+  // The query's terms are handled in batches of 64 slots: their block ranges [lo, hi) come in with
+  // one parallel load into LDS, and the batch's postings are processed as ONE flat range (a term
+  // has few postings per 8192-row block: a loop per term left most threads idle and chained a
+  // dependent load per term).
+  constexpr int TB = 64;
+  __shared__ int s_lo[TB], s_pre[TB + 1], s_total;
+  __shared__ LexTerm s_term[TB];
+  if (tid == 0) s_total = 0;
   __syncthreads();
+  int mine_total = 0;
+  for (int t = s0 + tid; t < s1; t += LEX_THREADS)
+    mine_total += bnd[(int64_t)t * (NB + 1) + blk + 1] - bnd[(int64_t)t * (NB + 1) + blk];
+  mine_total = (int)wave_sum((float)mine_total);  // exact: counts < 2^24 per workgroup
+  if (lane == 0 && mine_total) atomicAdd(&s_total, mine_total);
+  __syncthreads();
+  if (s_total == 0) return;  // uniform: no posting of this query in this row block
+  for (int i = tid; i < LEX_RB; i += LEX_THREADS) acc[i] = 0u;
   const float one_minus_b = 1.f - b, k1p1 = k1 + 1.f;
   const int64_t r0 = (int64_t)blk * LEX_RB;
-  for (int t = s0; t < s1; ++t) {
-    const LexTerm e = terms[t];
-    const int lo = bnd[(int64_t)t * (NB + 1) + blk], hi = bnd[(int64_t)t * (NB + 1) + blk + 1];
-    for (int p = lo + tid; p < hi; p += LEX_THREADS) {
-      const uint64_t v = post[e.start + p];
+  for (int tb = s0; tb < s1; tb += TB) {
+    const int nt = s1 - tb < TB ? s1 - tb : TB;
+    __syncthreads();  // previous batch done with s_*
+    if (tid < nt) {
+      const int t = tb + tid;
+      const int lo = bnd[(int64_t)t * (NB + 1) + blk], hi = bnd[(int64_t)t * (NB + 1) + blk + 1];
+      s_lo[tid] = lo;
+      s_pre[tid + 1] = hi - lo;
+      s_term[tid] = terms[t];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_pre[0] = 0;
+      for (int i = 0; i < nt; ++i) s_pre[i + 1] += s_pre[i];
+    }
+    __syncthreads();
+    const int tot = s_pre[nt];
+    for (int p = tid; p < tot; p += LEX_THREADS) {
+      int lo_t = 0, hi_t = nt - 1;  // term of flat posting p: last t with s_pre[t] <= p
+      while (lo_t < hi_t) {
+        const int mid = (lo_t + hi_t + 1) >> 1;
+        if (s_pre[mid] <= p) lo_t = mid;
+        else hi_t = mid - 1;
+      }
+      const LexTerm& e = s_term[lo_t];
+      const uint64_t v = post[e.start + s_lo[lo_t] + (p - s_pre[lo_t])];
       const uint32_t row = (uint32_t)(v >> 32);
       if (elig && !elig[row]) continue;
       const float tf = (float)(uint32_t)v;
