@@ -53,6 +53,9 @@ def parse():
                     help="config4 (default, the BASELINE metric) or config5: bge-m3 embed, 6.25M x "
                          "1024 rows per GPU scanned in fp8, BM25 over the passage tokens fused by "
                          "rrf (hybrid), rerank")
+    ap.add_argument("--fp8-ffn", action="store_true",
+                    help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
+                         "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
     ap.add_argument("--dist-backend", default=os.environ.get("SR_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     a = ap.parse_args()
@@ -132,6 +135,8 @@ def main():
     w_rerank = random_weights(rs, seed=12, style="hf")
     embedder = Encoder(es, device=local, weights=w_embed, max_tokens=a.batch * a.q_len)
     reranker = Encoder(rs, device=local, weights=w_rerank, max_tokens=524288)
+    if a.fp8_ffn:
+        reranker.set_fp8_ffn(True)
 
     # ---- corpus shard (rows [r0, r1) of the global 10M) -----------------------------------------
     N_total = a.corpus_rows
@@ -280,7 +285,8 @@ def main():
         "metric": metric,
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f16", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": "f16+fp8ffn" if a.fp8_ffn else "f16",
+        "data": "synthetic",
         "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
                    "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",

@@ -52,8 +52,25 @@ def _t(w, name):
 
 
 @torch.no_grad()
-def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None) -> torch.Tensor:
-    """Final hidden states [B, S, d] in fp32."""
+def e4m3(x: torch.Tensor) -> torch.Tensor:
+    """OCP e4m3fn rounding (nearest even, saturating at +-448) back to fp32."""
+    return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(torch.float32)
+
+
+def fp8_rows(wt: torch.Tensor) -> torch.Tensor:
+    """The fp8 FFN mode's weight copy: per row the largest power of two 2^e with
+    max|w| 2^e <= 448, e4m3(w 2^e) 2^-e (the device quantises the fp16 weight)."""
+    amax = wt.abs().amax(1, keepdim=True)
+    e = torch.floor(torch.log2(448.0 / amax.clamp_min(1e-30)))
+    e = torch.where(amax * torch.exp2(e + 1) <= 448.0, e + 1, e)
+    e = torch.where(amax * torch.exp2(e) > 448.0, e - 1, e)
+    return e4m3(wt * torch.exp2(e)) * torch.exp2(-e)
+
+
+def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
+                  fp8_ffn: bool = False) -> torch.Tensor:
+    """Final hidden states [B, S, d] in fp32.  fp8_ffn: the library's fp8 FFN mode — the FFN
+    activations 2 GELU(.) rounded to e4m3 and multiplied by fp8_rows(fp16(W2 / 2))."""
     ids = torch.as_tensor(np.asarray(ids), dtype=torch.long)
     mask = torch.as_tensor(np.asarray(mask), dtype=torch.float32)
     B, S = ids.shape
@@ -78,7 +95,12 @@ def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None) -> torch.Te
         h = _ln(lin(ctx, "attention.output.dense") + h, _t(w, p + "attention.output.LayerNorm.weight"),
                 _t(w, p + "attention.output.LayerNorm.bias"), cfg.ln_eps)
         f = torch.nn.functional.gelu(lin(h, "intermediate.dense"))
-        h = _ln(lin(f, "output.dense") + h, _t(w, p + "output.LayerNorm.weight"),
+        if fp8_ffn:
+            w2 = fp8_rows((0.5 * _t(w, p + "output.dense.weight")).half().float())
+            o = e4m3(2.0 * f) @ w2.T + _t(w, p + "output.dense.bias")
+        else:
+            o = lin(f, "output.dense")
+        h = _ln(o + h, _t(w, p + "output.LayerNorm.weight"),
                 _t(w, p + "output.LayerNorm.bias"), cfg.ln_eps)
     return h
 
@@ -98,9 +120,9 @@ def embed(cfg: RefConfig, w: dict, ids, mask, type_ids=None, pool: str = "cls") 
 
 
 @torch.no_grad()
-def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None) -> np.ndarray:
+def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None, fp8_ffn: bool = False) -> np.ndarray:
     """RoBERTa classification head on the first token: [P, num_labels] raw logits."""
-    h = encode_hidden(cfg, w, ids, mask, type_ids)[:, 0]
+    h = encode_hidden(cfg, w, ids, mask, type_ids, fp8_ffn)[:, 0]
     t = torch.tanh(h @ _t(w, "classifier.dense.weight").T + _t(w, "classifier.dense.bias"))
     return (t @ _t(w, "classifier.out_proj.weight").T + _t(w, "classifier.out_proj.bias")).numpy()
 

@@ -600,6 +600,14 @@ int sr_cross_score_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
   SR_API_END
 }
 
+int sr_encoder_set_fp8_ffn(sr_encoder* e, int on) {
+  SR_API_BEGIN
+  SR_NONNULL(e);
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  e->impl->set_fp8_ffn(on != 0);
+  SR_API_END
+}
+
 void sr_encoder_destroy(sr_encoder* e) {
   if (!e) return;
   delete e->impl;

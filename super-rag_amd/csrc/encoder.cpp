@@ -148,6 +148,18 @@ bool Encoder::fold_enabled() const {
   return !(e && e[0] == '0');
 }
 
+void Encoder::set_fp8_ffn(bool on) {
+  if (on) {
+    SR_CHECK(fold_enabled(), "encoder: fp8 FFN needs the LN-folded fp16-residual path");
+    SR_CHECK(cfg_.intermediate % 128 == 0 && cfg_.intermediate >= 256,
+             "encoder: fp8 FFN needs intermediate % 128 == 0, >= 256");
+  }
+  if (on != fp8_ffn_) {
+    fp8_ffn_ = on;
+    fold_ready_ = false;  // re-derive the folded weights (and the e4m3 W2 copy)
+  }
+}
+
 void Encoder::prepare_fold(hipStream_t s) {
   if (fold_ready_) return;
   const int64_t D = cfg_.hidden, F = cfg_.intermediate;
@@ -161,6 +173,12 @@ void Encoder::prepare_fold(hipStream_t s) {
                           L.d1.as<float>(), s);
     L.w2h.reserve((size_t)D * F * sizeof(half_t));  // 0.5 W2: FFN1 stores 2 GELU (exact scale)
     launch_scale_f16(L.w2.as<half_t>(), 0.5f, L.w2h.as<half_t>(), D * F, s);
+    if (fp8_ffn_) {
+      L.w2_8.reserve((size_t)D * F);
+      L.w2e.reserve((size_t)D);
+      launch_quantize_rows_fp8(L.w2h.as<half_t>(), (int)D, (int)F, L.w2_8.as<uint8_t>(),
+                               L.w2e.as<uint8_t>(), s);
+    }
     L.b2_f.reserve((size_t)D * sizeof(float));  // FFN2 bias + beta of LN1 (rebuilt residual)
     launch_vec_add(L.b2.as<float>(), L.ln1b.as<float>(), L.b2_f.as<float>(), (int)D, s);
     if (l == 0) continue;  // layer 0 reads the (normalised) embedding LayerNorm output
@@ -300,14 +318,18 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         LnFold l1;
         l1.mr = mA;
         l1.colsum = L.c1.as<float>();
-        launch_gemm(EPI_LNF_GELU_F16, Uo, d, L.w1_f.as<half_t>(), L.d1.as<float>(), nullptr, 0, ffn,
-                    F, Mr, F, d, s, &l1);
+        launch_gemm(fp8_ffn_ ? EPI_LNF_GELU_F8 : EPI_LNF_GELU_F16, Uo, d, L.w1_f.as<half_t>(),
+                    L.d1.as<float>(), nullptr, 0, ffn, F, Mr, F, d, s, &l1);
         LnFold l2;
         l2.mr = mA;
         l2.gamma = L.ln1g.as<float>();
         l2.stat_out = sB;
-        launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2h.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo, d,
-                    Mr, d, F, s, &l2);
+        if (fp8_ffn_)  // ffn holds e4m3 bytes (F per row)
+          launch_gemm_f8w(reinterpret_cast<const uint8_t*>(ffn), F, L.w2_8.as<uint8_t>(),
+                          L.w2e.as<uint8_t>(), L.b2_f.as<float>(), Uo, d, Uo, d, Mr, d, F, s, &l2);
+        else
+          launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2h.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo,
+                      d, Mr, d, F, s, &l2);
         launch_ln_stats_finalize(sB, nparts, cfg_.ln_eps, Mr, mB, s);
       }
       // final LayerNorm (LN2 of the last block) of the rows that are consumed -> h16

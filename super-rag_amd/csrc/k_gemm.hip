@@ -77,9 +77,9 @@ __device__ __forceinline__ int8v read_frag8(const half_t* lds_tile, int row, int
 // Unit vectors are stored / staged as e4m3(256 x): |256 x_i| <= 256 < 448 never saturates and the
 // E8M0 block scales 119 = 2^-8 on A and B undo the factor inside the MFMA (exact power of two), so
 // the accumulators are plain cosines.
-__device__ __forceinline__ float4v mfma8(int8v a, int8v b, float4v c) {
-  // fmt 0 / 0 = fp8 e4m3 (OCP); E8M0 block scales 119 = 2^-8
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 119, 0, 119);
+__device__ __forceinline__ float4v mfma8(int8v a, int8v b, float4v c, int sa, int sb) {
+  // fmt 0 / 0 = fp8 e4m3 (OCP); E8M0 block scales of A (lane's row) and B
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
 // Exact-GELU x * Phi(x) with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
@@ -231,12 +231,13 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
                                                 const void* __restrict__ R, int64_t ldr,
                                                 void* __restrict__ Y, int64_t ldy,
                                                 const LnFold& lf) {
-  constexpr bool LNF = EPI == EPI_LNF_F16 || EPI == EPI_LNF_GELU_F16;
+  constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;  // e4m3 bytes instead of fp16
+  constexpr bool LNF = EPI == EPI_LNF_F16 || EPI == EPI_LNF_GELU_F16 || OUT8;
   constexpr bool RESN = EPI == EPI_BIAS_RES_F16 || EPI == EPI_RES16_STATS;
   constexpr bool LNR = EPI == EPI_LNR16_STATS;
   constexpr bool STATS = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS;
   constexpr bool GELU = EPI == EPI_BIAS_GELU_F16;
-  constexpr bool GELU2 = EPI == EPI_LNF_GELU_F16;  // stores 2 * GELU (consumer weight halved)
+  constexpr bool GELU2 = EPI == EPI_LNF_GELU_F16 || OUT8;  // stores 2 * GELU (consumer weight halved)
   static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
@@ -323,9 +324,16 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = gelu2_erf(v[r]);
       }
+      if constexpr (OUT8) {
+        uint2 q8;
+        q8.x = e4m3x4(v[0], v[1], v[2], v[3]);
+        q8.y = e4m3x4(v[4], v[5], v[6], v[7]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+      } else {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
-      *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
+        for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
+        *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
+      }
     }
     if constexpr (STATS) {
       // partner lanes (xor 16 / 32) share the row m, so they are active together
@@ -477,8 +485,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr int STAGE = (BN + BM) * GBK;  // halfs per buffer (64 KiB)
   // fp8 operands (EPI_SCAN8): K, lda count 2-byte units, so the staging below moves the same
   // 128-byte K-step rows; a K-step then holds 128 fp8 elements
-  constexpr bool F8 = EPI == EPI_SCAN8;
+  constexpr bool F8W = EPI == EPI_LNR16_STATS_F8;  // fp8 activations x fp8 weights (row scales)
+  constexpr bool F8 = EPI == EPI_SCAN8 || F8W;
   constexpr bool SCAN = EPI == EPI_SCAN || EPI == EPI_SCAN8;
+  constexpr int EPI_OUT = F8W ? EPI_LNR16_STATS : EPI;  // the epilogue that runs
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
@@ -550,6 +560,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   float4v acc[8][4];
   half8 aX[4], aY[4], bX[4], bY[4];
   int8v f0[2], f1[2], fb[4];  // fp8 path: A row pairs (ping-pong) and B
+  int sa[8];                  // fp8 weights: E8M0 exponent of each A (W) fragment row
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sa[i] = 119;  // the scan: 2^-8 on both operands
 
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
@@ -656,7 +669,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[2 * q + i][j] = mfma8(use[i], fb[j], acc[2 * q + i][j]);
+        for (int j = 0; j < 4; ++j) acc[2 * q + i][j] = mfma8(use[i], fb[j], acc[2 * q + i][j], sa[2 * q + i], F8W ? 127 : 119);
       SR_INTERLEAVE8(4);
     }
     (void)lenient;
@@ -678,7 +691,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[6 + i][j] = mfma8(f1[i], fb[j], acc[6 + i][j]);
+      for (int j = 0; j < 2; ++j) acc[6 + i][j] = mfma8(f1[i], fb[j], acc[6 + i][j], sa[6 + i], F8W ? 127 : 119);
     if (RN) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) f0[i] = read_frag8(nxt, arow + 16 * i, c0);
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 2; j < 4; ++j) acc[6 + i][j] = mfma8(f1[i], fb[j], acc[6 + i][j]);
+      for (int j = 2; j < 4; ++j) acc[6 + i][j] = mfma8(f1[i], fb[j], acc[6 + i][j], sa[6 + i], F8W ? 127 : 119);
     if (RN) {
 #pragma unroll
       for (int j = 2; j < 4; ++j) fb[j] = read_frag8(nxt + BN * GBK, brow + 16 * j, c0);
@@ -708,6 +721,14 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (F8W) {
+      const uint8_t* wexp = reinterpret_cast<const uint8_t*>(lf.colsum);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = n0 + arow + 16 * i;
+        sa[i] = wexp[n < N ? n : N - 1];
+      }
+    }
     if constexpr (F8) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) f0[i] = read_frag8(lds, arow + 16 * i, c0);
@@ -789,11 +810,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       scan_epilogue(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                     reinterpret_cast<const uint8_t*>(R), reinterpret_cast<uint64_t*>(Y), (int)ldy, lf);
     } else if (full) {
-      PipeEpi<EPI>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr,
-                                        Y, ldy, lf);
+      PipeEpi<EPI_OUT>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R,
+                                            ldr, Y, ldy, lf);
     } else {
-      PipeEpi<EPI>::template run<true>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr,
-                                       Y, ldy, lf);
+      PipeEpi<EPI_OUT>::template run<true>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R,
+                                           ldr, Y, ldy, lf);
     }
     if (!more) break;
     // next tile: K-step 0 (group 0's 16 glds) landed; younger: the epilogue's NSTORE stores
@@ -1107,6 +1128,7 @@ static const char* epi_name(int epi) {
     case EPI_LNF_GELU_F16: return "gemm_f16_lnfold_gelu";
     case EPI_RES16_STATS: return "gemm_f16_residual16_stats";
     case EPI_LNR16_STATS: return "gemm_f16_lnres16_stats";
+    case EPI_LNF_GELU_F8: return "gemm_f16_lnfold_gelu_out8";
     default: return "gemm_f16_bias_tanh";
   }
 }
@@ -1161,6 +1183,62 @@ void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t
   SR_LAUNCH_CHECK();
 }
 
+void launch_gemm_f8w(const uint8_t* X8, int64_t lda, const uint8_t* W8, const uint8_t* wexp,
+                     const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy, int M,
+                     int N, int K, hipStream_t stream, const LnFold* lf) {
+  SR_CHECK(K % 128 == 0 && K >= 256, "gemm_f8w: K must be a multiple of 128, >= 256");
+  SR_CHECK(N % 256 == 0, "gemm_f8w: N must be a multiple of 256");
+  SR_CHECK(lda % 16 == 0 && ldy % 8 == 0 && ldr % 8 == 0, "gemm_f8w: 16-byte rows");
+  SR_CHECK(lf && lf->mr && lf->gamma && lf->stat_out && wexp, "gemm_f8w: LnFold mr / gamma / stat_out, wexp");
+  if (M <= 0) return;
+  ProfScope prof("gemm_f8_lnres16_stats", stream, 2.0 * M * (double)N * K,
+                 (double)M * K + (double)N * K + 4.0 * (double)M * N);
+  LnFold lfv = *lf;
+  lfv.colsum = reinterpret_cast<const float*>(wexp);  // (field re-use: the weight rows' exponents)
+  const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
+  // operands as 2-byte units: K / 2, lda / 2 (the staging moves bytes)
+  if (tiles >= 512) {
+    const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+    hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNR16_STATS_F8, true>), grid, block, 0, stream,
+                       reinterpret_cast<const half_t*>(X8), lda / 2, reinterpret_cast<const half_t*>(W8),
+                       bias, R, ldr, Y, ldy, M, N, K / 2, lfv);
+  } else {
+    hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNR16_STATS_F8, false>), dim3((unsigned)tiles), dim3(512), 0,
+                       stream, reinterpret_cast<const half_t*>(X8), lda / 2,
+                       reinterpret_cast<const half_t*>(W8), bias, R, ldr, Y, ldy, M, N, K / 2, lfv);
+  }
+  SR_LAUNCH_CHECK();
+}
+
+__global__ void quantize_rows_fp8_exp_kernel(const half_t* __restrict__ W, int N, int K,
+                                             uint8_t* __restrict__ W8, uint8_t* __restrict__ wexp) {
+  const int n = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  const half_t* w = W + (int64_t)n * K;
+  float amax = 0.f;
+  for (int k = lane; k < K; k += 64) amax = fmaxf(amax, fabsf((float)w[k]));
+  amax = wave_max(amax);
+  int e = 0;
+  if (amax > 0.f) {
+    int ex;
+    (void)frexpf(448.f / amax, &ex);
+    e = ex - 1;
+    while (ldexpf(amax, e + 1) <= 448.f) ++e;
+    while (ldexpf(amax, e) > 448.f) --e;
+  }
+  e = e > 127 ? 127 : (e < -127 ? -127 : e);
+  for (int k = lane; k < K; k += 64) W8[(int64_t)n * K + k] = (uint8_t)e4m3_rne(ldexpf((float)w[k], e));
+  if (lane == 0) wexp[n] = (uint8_t)(127 - e);
+}
+
+void launch_quantize_rows_fp8(const half_t* W, int N, int K, uint8_t* W8, uint8_t* wexp,
+                              hipStream_t s) {
+  if (N <= 0) return;
+  hipLaunchKernelGGL(quantize_rows_fp8_exp_kernel, dim3((unsigned)ceil_div(N, 4)), dim3(256), 0, s,
+                     W, N, K, W8, wexp);
+  SR_LAUNCH_CHECK();
+}
+
 static int g_force_tile = -1;
 void gemm_force_tile(int t) { g_force_tile = t; }
 static int forced_tile() {
@@ -1188,17 +1266,19 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   SR_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128");
   SR_CHECK(lda % 8 == 0 && ldy % 4 == 0, "gemm: leading dimensions must keep 16-byte rows");
   const bool fold = epi >= EPI_LNF_F16;
-  SR_CHECK(epi >= 0 && epi <= EPI_LNR16_STATS, "gemm: unknown epilogue");
+  SR_CHECK((epi >= 0 && epi <= EPI_LNR16_STATS) || epi == EPI_LNF_GELU_F8, "gemm: unknown epilogue");
   SR_CHECK(!fold || (lf && N % 256 == 0), "gemm: LayerNorm-folded epilogues need LnFold, N % 256");
-  SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNR16_STATS) || lf->mr,
+  SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNF_GELU_F8 ||
+             epi == EPI_LNR16_STATS) || lf->mr,
            "gemm: LN-folded operand needs its row statistics");
-  SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16) || lf->colsum, "gemm: LNF needs colsum");
+  SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNF_GELU_F8) || lf->colsum,
+           "gemm: LNF needs colsum");
   SR_CHECK(epi != EPI_LNR16_STATS || lf->gamma, "gemm: LNR needs the LayerNorm weight");
   SR_CHECK(!(epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS) || lf->stat_out,
            "gemm: *_STATS epilogue needs stat_out");
   if (M <= 0) return;
   const bool out32 = epi == EPI_BIAS_RES_F32 || epi == EPI_BIAS_TANH_F32;
-  const double out_b = out32 ? 4.0 : 2.0;
+  const double out_b = out32 ? 4.0 : epi == EPI_LNF_GELU_F8 ? 1.0 : 2.0;
   const double res_b = epi == EPI_BIAS_RES_F32 ? 4.0
                        : (epi == EPI_BIAS_RES_F16 || epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS) ? 2.0
                                                                                                      : 0.0;
@@ -1209,10 +1289,12 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   int v = variant >= 0 ? variant : forced_tile();
   if (v < 0) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_SMALL;
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
-  if (v == GEMM_PP && K % 32 != 0) v = GEMM_PIPE;
+  if (v == GEMM_PP && (K % 32 != 0 || epi == EPI_LNF_GELU_F8)) v = GEMM_PIPE;
   if (fold && (v == GEMM_SMALL || v == GEMM_BIG)) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_PIPE;
   const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST || v == GEMM_PP) && !out32;
   SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
+  SR_CHECK(epi != EPI_LNF_GELU_F8 || v == GEMM_PIPE || v == GEMM_PIPE_PERSIST,
+           "gemm: the fp8-output epilogue runs on the pipelined kernels");
   const LnFold lfv = lf ? *lf : LnFold{};
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
@@ -1283,6 +1365,7 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
       SR_PIPE_CASE(EPI_LNF_GELU_F16)
       SR_PIPE_CASE(EPI_RES16_STATS)
       SR_PIPE_CASE(EPI_LNR16_STATS)
+      SR_PIPE_CASE(EPI_LNF_GELU_F8)
       default: SR_CHECK(false, "gemm: unknown epilogue");
     }
 #undef SR_PIPE_CASE

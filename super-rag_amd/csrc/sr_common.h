@@ -77,6 +77,29 @@ __device__ __forceinline__ uint64_t make_key(float sim, uint32_t row) {
 __device__ __forceinline__ float key_sim(uint64_t key) { return unordered_bits((uint32_t)(key >> 32)); }
 __device__ __forceinline__ uint32_t key_row(uint64_t key) { return 0xffffffffu - (uint32_t)key; }
 
+// OCP e4m3fn (bias 7, max 448, no infinities), round to nearest even, saturating at +-448.
+__device__ __forceinline__ uint32_t e4m3_rne(float v) {
+  const uint32_t sign = v < 0.f ? 0x80u : 0u;
+  const float a = fminf(fabsf(v), 448.f);
+  if (a < 0.015625f) {  // below 2^-6: subnormal steps of 2^-9
+    const uint32_t m = (uint32_t)rintf(a * 512.f);  // 0 .. 8 (8 = the smallest normal)
+    return sign | m;
+  }
+  int e;
+  (void)frexpf(a, &e);  // a = f * 2^e, f in [0.5, 1)  ->  a = (1 + m / 8) * 2^(e - 1)
+  const float m = rintf((ldexpf(a, 1 - e) - 1.f) * 8.f);  // 0 .. 8 (8 carries into the exponent)
+  return sign | ((uint32_t)(e - 1 + 7) * 8u + (uint32_t)m);
+}
+
+// Four floats -> four e4m3 bytes with v_cvt_pk_fp8_f32 (gfx950: OCP e4m3, round to nearest even;
+// bit-identical to e4m3_rne after the clamp, checked on 2^24 values: tools/diag/cvt_fp8.hip).
+__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
+  auto cl = [](float x) { return fminf(fmaxf(x, -448.f), 448.f); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(cl(a), cl(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(cl(c), cl(d), w, true);
+  return (uint32_t)w;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

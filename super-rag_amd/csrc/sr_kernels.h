@@ -24,7 +24,12 @@ enum Epilogue {
   EPI_SCAN = 9,
   // the same on OCP fp8-e4m3 operands e4m3(256 x) of unit vectors (block-scaled MFMA
   // v_mfma_scale_f32_16x16x128_f8f6f4, E8M0 block scales 2^-8 undo the factor)
-  EPI_SCAN8 = 10
+  EPI_SCAN8 = 10,
+  // fp8 FFN (Encoder fp8_ffn mode): FFN1 = EPI_LNF_GELU_F16 storing OCP e4m3(2 GELU) bytes; FFN2 =
+  // EPI_LNR16_STATS on e4m3 activations x e4m3 weights (per-row power-of-two scales of the weight
+  // as the block-scaled MFMA's E8M0 A scales; launch_gemm_f8w)
+  EPI_LNF_GELU_F8 = 11,
+  EPI_LNR16_STATS_F8 = 12
 };
 
 // Per-row statistics hand-over between GEMMs (Chan-combinable partials over 128-column spans):
@@ -55,6 +60,15 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
 void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 // K1 for large query blocks (B in (128, 256]) on the pipelined GEMM: rows [r0, r1) of the corpus
 // against B queries; non-dense threshold mode only (same contract as launch_cosine_scan).
+// Y = EPI_LNR16_STATS(X8 . W8^T) on OCP e4m3 operands: X8 [M][K] bytes (lda bytes), W8 [N][K] bytes
+// with per-row E8M0 exponents wexp[N] (W = W8 * 2^(wexp - 127)); K % 128 == 0, K >= 256.
+void launch_gemm_f8w(const uint8_t* X8, int64_t lda, const uint8_t* W8, const uint8_t* wexp,
+                     const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy, int M,
+                     int N, int K, hipStream_t stream, const LnFold* lf);
+// W [N][K] fp16 -> W8 [N][K] e4m3 of W * 2^e_n (largest power of two with max|W_n| 2^e_n <= 448),
+// wexp[n] = 127 - e_n
+void launch_quantize_rows_fp8(const half_t* W, int N, int K, uint8_t* W8, uint8_t* wexp,
+                              hipStream_t s);
 // fp8 rows e4m3(256 x) (ld8 bytes, a multiple of 128, >= 256) of unit vectors; sims are cosines.
 void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t* live, int64_t r0,
                               int64_t r1, const uint8_t* Q8, int B, const float* tau, uint64_t* cand,

@@ -34,21 +34,6 @@ __global__ void gather_rows_kernel(const half_t* __restrict__ src, int ld,
   half8* d = reinterpret_cast<half8*>(dst + r * ld);
   for (int c = threadIdx.x; c < ld / 8; c += blockDim.x) d[c] = s[c];
 }
-// OCP e4m3fn (bias 7, max 448, no infinities), round to nearest even; |v| <= 448 by construction.
-__device__ __forceinline__ uint32_t e4m3_rne(float v) {
-  const uint32_t sign = v < 0.f ? 0x80u : 0u;
-  const float a = fabsf(v);
-  if (a < 0.015625f) {  // below 2^-6: subnormal steps of 2^-9
-    const uint32_t m = (uint32_t)rintf(a * 512.f);  // 0 .. 8 (8 = the smallest normal)
-    return sign | m;
-  }
-  int e;
-  (void)frexpf(a, &e);  // a = f * 2^e, f in [0.5, 1)  ->  a = (1 + m / 8) * 2^(e - 1)
-  const float m = rintf((ldexpf(a, 1 - e) - 1.f) * 8.f);  // 0 .. 8 (8 carries into the exponent)
-  const uint32_t code = (uint32_t)(e - 1 + 7) * 8u + (uint32_t)m;
-  return sign | code;
-}
-
 // fp16 unit rows (ld halfs) -> e4m3(256 x) rows (ld8 bytes, zero padded): |256 x| <= 256 < 448, so
 // one fixed power of two serves every row and query (the scan MFMA's E8M0 scales undo it).
 __global__ void quantize_rows_fp8_kernel(const half_t* __restrict__ src, int ld, int dim,

@@ -188,6 +188,11 @@ class Encoder:
             N.call("sr_encoder_set_weight", self._h, name.encode(), N.ptr(a), a.size)
         N.call("sr_encoder_ready", self._h)
 
+    def set_fp8_ffn(self, on: bool = True) -> None:
+        """Opt-in fp8 FFN precision mode (LN-folded fp16-residual encoders, e.g. cross-encoders):
+        FFN1 writes e4m3 activations, FFN2 runs the block-scaled fp8 MFMA (sr_encoder_set_fp8_ffn)."""
+        N.call("sr_encoder_set_fp8_ffn", self._h, 1 if on else 0)
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             N.load().sr_encoder_destroy(self._h)

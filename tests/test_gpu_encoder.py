@@ -220,3 +220,40 @@ def test_bge_m3_widths_long_sequences(S):
     lg = Encoder(rr, weights=wr).cross_score(ids, mask)
     lg_ref = R.cross_logits(_ref_cfg(rr), wr, ids, mask)
     assert np.abs(lg - lg_ref).max() <= 1e-2 * (1.0 + np.abs(lg_ref).max())
+
+
+@pytest.mark.parametrize("S", [16, 130])
+def test_fp8_ffn_cross_encoder(S):
+    # fp8 FFN mode: FFN1 stores e4m3(2 GELU), FFN2 runs the block-scaled fp8 MFMA on an e4m3 copy
+    # of W2 / 2 with per-row power-of-two scales.  Against the oracle restating exactly that
+    # quantisation (oracle/encoder_ref.py fp8_ffn) the band is the fp16 path's; against the plain
+    # fp32 model the logits move by the fp8 rounding.
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("xlmr", d=256, H=4, F=512, L=3, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=32, style="test")
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 33, S, seed=S + 1)
+    got16 = enc.cross_score(ids, mask)
+    enc.set_fp8_ffn(True)
+    got8 = enc.cross_score(ids, mask)
+    ref8 = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8_ffn=True)
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)
+    scale = 1.0 + np.abs(ref).max()
+    assert not np.array_equal(got8, got16)
+    assert np.abs(got8 - ref8).max() <= 8e-3 * scale
+    assert np.abs(got8 - ref).max() <= 5e-2 * scale
+    enc.set_fp8_ffn(False)
+    np.testing.assert_array_equal(enc.cross_score(ids, mask), got16)
+
+
+def test_fp8_ffn_persistent_tiles():
+    # enough rows (143k tokens) for the persistent fp8 FFN2 / e4m3-output FFN1 kernels
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("xlmr", d=256, H=4, F=512, L=2, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=33, style="test")
+    enc = Encoder(spec, weights=w, max_tokens=1 << 18)
+    enc.set_fp8_ffn(True)
+    ids, mask = _batch(spec, 1100, 130, seed=7, ragged=False)
+    got8 = enc.cross_score(ids, mask)
+    ref8 = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8_ffn=True)
+    assert np.abs(got8 - ref8).max() <= 8e-3 * (1.0 + np.abs(ref8).max())

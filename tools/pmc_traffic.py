@@ -28,7 +28,8 @@ EPI_NAMES = {0: "gemm_f16_bias", 1: "gemm_f16_bias_gelu", 2: "gemm_f16_bias_resi
              6: "gemm_f16_lnfold_gelu", 7: "gemm_f16_residual16_stats",
              8: "gemm_f16_lnres16_stats",
              9: "cosine_scan",    # K1 threshold chunks on the GEMM main loop (EPI_SCAN)
-             10: "cosine_scan8"}  # the fp8 scan (EPI_SCAN8)
+             10: "cosine_scan8",  # the fp8 scan (EPI_SCAN8)
+             11: "gemm_f16_lnfold_gelu_out8", 12: "gemm_f8_lnres16_stats"}
 
 
 def logical(name):
