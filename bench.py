@@ -28,6 +28,7 @@ import torch  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_F16_TFLOPS = 2500.0    # dense fp16/bf16 MFMA spec (no sparsity)
+PEAK_F8_TFLOPS = 5000.0     # dense fp8 MFMA spec (no sparsity)
 
 
 def parse():
@@ -56,6 +57,9 @@ def parse():
     ap.add_argument("--fp8-ffn", action="store_true",
                     help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
                          "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
+    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2),
+                    help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
+                         "e4m3 residual copies (dtype f16+fp8ffn / f16+fp8gemm)")
     ap.add_argument("--dist-backend", default=os.environ.get("SR_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     a = ap.parse_args()
@@ -136,7 +140,9 @@ def main():
     embedder = Encoder(es, device=local, weights=w_embed, max_tokens=a.batch * a.q_len)
     reranker = Encoder(rs, device=local, weights=w_rerank, max_tokens=524288)
     if a.fp8_ffn:
-        reranker.set_fp8_ffn(True)
+        a.fp8 = max(a.fp8, 1)
+    if a.fp8:
+        reranker.set_fp8(a.fp8)
 
     # ---- corpus shard (rows [r0, r1) of the global 10M) -----------------------------------------
     N_total = a.corpus_rows
@@ -232,8 +238,9 @@ def main():
     avg_ms = dom["total_ms"] / dom["launches"]
     if dom["flops"] > 0 and not dom_name.startswith("cosine_scan"):
         achieved = dom["flops"] / (dom["total_ms"] * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_F16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": None}
+        peak = PEAK_F8_TFLOPS if dom_name.startswith("gemm_f8") else PEAK_F16_TFLOPS
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None}
     else:
         achieved = dom["bytes"] / (dom["total_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
@@ -249,7 +256,7 @@ def main():
         # measured by the PMC pass: frac of the spec peak vs of the peak at the held clock
         roof["pmc_clock_ghz"] = pmc["clock_ghz"]
         roof["pmc_mfma_util"] = pmc.get("mfma_util")
-        roof["peak_at_held_clock"] = round(PEAK_F16_TFLOPS * pmc["clock_ghz"] / 2.4, 1)
+        roof["peak_at_held_clock"] = round(roof["peak"] * pmc["clock_ghz"] / 2.4, 1)
     step_ms = dt / a.steps * 1e3
     kern = {k: {"ms_per_step": round(v["total_ms"] / a.steps, 3), "launches": v["launches"],
                 ("tflops" if v["flops"] > 0 else "gbs"):
@@ -285,7 +292,7 @@ def main():
         "metric": metric,
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f16+fp8ffn" if a.fp8_ffn else "f16",
+        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm")[a.fp8],
         "data": "synthetic",
         "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,

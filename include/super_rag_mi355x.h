@@ -239,11 +239,13 @@ int sr_cross_score(sr_encoder* e, const int32_t* ids, const int32_t* mask,
                    const int32_t* type_ids, int P, int S, float* out_logits);
 int sr_cross_score_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
                        const int32_t* type_ids, int P, int S, float* out_logits, void* stream);
-/* fp8 FFN mode (BASELINE config 5 "fp8 MFMA GEMM path"; LN-folded fp16-residual encoders, e.g.
- * the cross-encoders): FFN1 stores OCP e4m3 activations and FFN2 runs the block-scaled fp8 MFMA
- * against an e4m3 copy of its weight (per-row power-of-two scales).  An opt-in precision mode:
- * logits move by ~1e-2 relative (tests/test_gpu_encoder.py); off by default. */
-int sr_encoder_set_fp8_ffn(sr_encoder* e, int on);
+/* fp8 precision modes (BASELINE config 5 "fp8 MFMA GEMM path"; LN-folded fp16-residual encoders,
+ * e.g. the cross-encoders).  1: FFN1 stores OCP e4m3 activations and FFN2 runs the block-scaled
+ * fp8 MFMA against an e4m3 copy of its weight (per-row power-of-two scales); 2: also FFN1 and the
+ * QKV GEMMs of layers >= 1 on e4m3 copies of the residual sums (written by the residual
+ * epilogues) and of the folded weights.  0 (default): fp16.  Opt-in: logits move by the fp8
+ * rounding (tests/test_gpu_encoder.py). */
+int sr_encoder_set_fp8(sr_encoder* e, int mode);
 void sr_encoder_destroy(sr_encoder* e);
 
 /* ------------------------------------------------------------------------------------------------

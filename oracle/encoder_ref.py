@@ -67,10 +67,24 @@ def fp8_rows(wt: torch.Tensor) -> torch.Tensor:
     return e4m3(wt * torch.exp2(e)) * torch.exp2(-e)
 
 
+def _fold8(u, g, beta, wt, bias, eps):
+    """fp8 mode 2's LayerNorm-folded GEMM LN(u) W^T + b on e4m3 operands: the device keeps the
+    pre-LN residual sum u (fp16) and its row statistics, multiplies e4m3(u) by the e4m3 row copy
+    of the folded weight W' = fp16(W diag(gamma)) and undoes the normalisation in the epilogue:
+    rstd (e4m3(u) W'^T - mu colsum(W')) + (W beta + b)  (super-rag_amd/csrc/encoder.cpp fp8_ >= 2)."""
+    mu = u.mean(-1, keepdim=True)
+    rstd = torch.rsqrt(((u - mu) ** 2).mean(-1, keepdim=True) + eps)
+    wq = fp8_rows((wt * g[None, :]).half().float())
+    return rstd * (e4m3(u.half().float()) @ wq.T - mu * wq.sum(1)) + (wt @ beta + bias)
+
+
 def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
-                  fp8_ffn: bool = False) -> torch.Tensor:
-    """Final hidden states [B, S, d] in fp32.  fp8_ffn: the library's fp8 FFN mode — the FFN
-    activations 2 GELU(.) rounded to e4m3 and multiplied by fp8_rows(fp16(W2 / 2))."""
+                  fp8_ffn: bool = False, fp8: int = 0) -> torch.Tensor:
+    """Final hidden states [B, S, d] in fp32.  fp8 (the library's opt-in precision modes;
+    fp8_ffn=True is fp8=1): 1 = the FFN activations 2 GELU(.) rounded to e4m3 and multiplied by
+    fp8_rows(fp16(W2 / 2)); 2 = also FFN1 and the QKV of layers >= 1 as _fold8 on the pre-LN
+    residual sums."""
+    fp8 = max(fp8, 1 if fp8_ffn else 0)
     ids = torch.as_tensor(np.asarray(ids), dtype=torch.long)
     mask = torch.as_tensor(np.asarray(mask), dtype=torch.float32)
     B, S = ids.shape
@@ -87,21 +101,34 @@ def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
         p = f"encoder.layer.{l}."
         def lin(x, n):
             return x @ _t(w, p + n + ".weight").T + _t(w, p + n + ".bias")
-        q = lin(h, "attention.self.query").view(B, S, H, dh).transpose(1, 2)
-        k = lin(h, "attention.self.key").view(B, S, H, dh).transpose(1, 2)
-        v = lin(h, "attention.self.value").view(B, S, H, dh).transpose(1, 2)
+        if fp8 >= 2 and l > 0:
+            pp = f"encoder.layer.{l - 1}.output.LayerNorm."
+            wqkv = torch.cat([_t(w, p + f"attention.self.{n}.weight") for n in ("query", "key", "value")])
+            bqkv = torch.cat([_t(w, p + f"attention.self.{n}.bias") for n in ("query", "key", "value")])
+            q, k, v = _fold8(u2, _t(w, pp + "weight"), _t(w, pp + "bias"), wqkv, bqkv,
+                             cfg.ln_eps).split(d, dim=-1)
+        else:
+            q, k, v = lin(h, "attention.self.query"), lin(h, "attention.self.key"), lin(h, "attention.self.value")
+        q = q.reshape(B, S, H, dh).transpose(1, 2)
+        k = k.reshape(B, S, H, dh).transpose(1, 2)
+        v = v.reshape(B, S, H, dh).transpose(1, 2)
         s = q @ k.transpose(-1, -2) / math.sqrt(dh) + bias
         ctx = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, S, d)
-        h = _ln(lin(ctx, "attention.output.dense") + h, _t(w, p + "attention.output.LayerNorm.weight"),
-                _t(w, p + "attention.output.LayerNorm.bias"), cfg.ln_eps)
-        f = torch.nn.functional.gelu(lin(h, "intermediate.dense"))
-        if fp8_ffn:
+        u1 = lin(ctx, "attention.output.dense") + h
+        g1, b1 = _t(w, p + "attention.output.LayerNorm.weight"), _t(w, p + "attention.output.LayerNorm.bias")
+        h = _ln(u1, g1, b1, cfg.ln_eps)
+        if fp8 >= 2:
+            f = torch.nn.functional.gelu(_fold8(u1, g1, b1, _t(w, p + "intermediate.dense.weight"),
+                                                _t(w, p + "intermediate.dense.bias"), cfg.ln_eps))
+        else:
+            f = torch.nn.functional.gelu(lin(h, "intermediate.dense"))
+        if fp8:
             w2 = fp8_rows((0.5 * _t(w, p + "output.dense.weight")).half().float())
             o = e4m3(2.0 * f) @ w2.T + _t(w, p + "output.dense.bias")
         else:
             o = lin(f, "output.dense")
-        h = _ln(o + h, _t(w, p + "output.LayerNorm.weight"),
-                _t(w, p + "output.LayerNorm.bias"), cfg.ln_eps)
+        u2 = o + h
+        h = _ln(u2, _t(w, p + "output.LayerNorm.weight"), _t(w, p + "output.LayerNorm.bias"), cfg.ln_eps)
     return h
 
 
@@ -120,9 +147,10 @@ def embed(cfg: RefConfig, w: dict, ids, mask, type_ids=None, pool: str = "cls") 
 
 
 @torch.no_grad()
-def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None, fp8_ffn: bool = False) -> np.ndarray:
+def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None, fp8_ffn: bool = False,
+                 fp8: int = 0) -> np.ndarray:
     """RoBERTa classification head on the first token: [P, num_labels] raw logits."""
-    h = encode_hidden(cfg, w, ids, mask, type_ids, fp8_ffn)[:, 0]
+    h = encode_hidden(cfg, w, ids, mask, type_ids, fp8_ffn, fp8)[:, 0]
     t = torch.tanh(h @ _t(w, "classifier.dense.weight").T + _t(w, "classifier.dense.bias"))
     return (t @ _t(w, "classifier.out_proj.weight").T + _t(w, "classifier.out_proj.bias")).numpy()
 

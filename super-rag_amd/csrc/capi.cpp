@@ -600,11 +600,11 @@ int sr_cross_score_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
   SR_API_END
 }
 
-int sr_encoder_set_fp8_ffn(sr_encoder* e, int on) {
+int sr_encoder_set_fp8(sr_encoder* e, int mode) {
   SR_API_BEGIN
   SR_NONNULL(e);
   std::lock_guard<std::mutex> lk(e->impl->mu);
-  e->impl->set_fp8_ffn(on != 0);
+  e->impl->set_fp8(mode);
   SR_API_END
 }
 

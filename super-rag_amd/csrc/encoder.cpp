@@ -148,15 +148,17 @@ bool Encoder::fold_enabled() const {
   return !(e && e[0] == '0');
 }
 
-void Encoder::set_fp8_ffn(bool on) {
-  if (on) {
-    SR_CHECK(fold_enabled(), "encoder: fp8 FFN needs the LN-folded fp16-residual path");
-    SR_CHECK(cfg_.intermediate % 128 == 0 && cfg_.intermediate >= 256,
-             "encoder: fp8 FFN needs intermediate % 128 == 0, >= 256");
+void Encoder::set_fp8(int mode) {
+  SR_CHECK(mode >= 0 && mode <= 2, "encoder: fp8 mode must be 0, 1 or 2");
+  if (mode) {
+    SR_CHECK(fold_enabled(), "encoder: fp8 modes need the LN-folded fp16-residual path");
+    SR_CHECK(cfg_.intermediate % 128 == 0 && cfg_.intermediate >= 256 &&
+                 (mode < 2 || (cfg_.hidden % 128 == 0 && cfg_.hidden >= 256)),
+             "encoder: fp8 GEMMs need K % 128 == 0, K >= 256");
   }
-  if (on != fp8_ffn_) {
-    fp8_ffn_ = on;
-    fold_ready_ = false;  // re-derive the folded weights (and the e4m3 W2 copy)
+  if (mode != fp8_) {
+    fp8_ = mode;
+    fold_ready_ = false;  // re-derive the folded weights (and their e4m3 copies)
   }
 }
 
@@ -173,11 +175,20 @@ void Encoder::prepare_fold(hipStream_t s) {
                           L.d1.as<float>(), s);
     L.w2h.reserve((size_t)D * F * sizeof(half_t));  // 0.5 W2: FFN1 stores 2 GELU (exact scale)
     launch_scale_f16(L.w2.as<half_t>(), 0.5f, L.w2h.as<half_t>(), D * F, s);
-    if (fp8_ffn_) {
+    if (fp8_ >= 1) {
       L.w2_8.reserve((size_t)D * F);
       L.w2e.reserve((size_t)D);
       launch_quantize_rows_fp8(L.w2h.as<half_t>(), (int)D, (int)F, L.w2_8.as<uint8_t>(),
                                L.w2e.as<uint8_t>(), s);
+    }
+    if (fp8_ >= 2) {
+      L.w1_8.reserve((size_t)F * D);
+      L.w1e.reserve((size_t)F);
+      L.c1_8.reserve((size_t)F * sizeof(float));
+      launch_quantize_rows_fp8(L.w1_f.as<half_t>(), (int)F, (int)D, L.w1_8.as<uint8_t>(),
+                               L.w1e.as<uint8_t>(), s);
+      launch_colsum_fp8(L.w1_8.as<uint8_t>(), L.w1e.as<uint8_t>(), (int)F, (int)D,
+                        L.c1_8.as<float>(), s);
     }
     L.b2_f.reserve((size_t)D * sizeof(float));  // FFN2 bias + beta of LN1 (rebuilt residual)
     launch_vec_add(L.b2.as<float>(), L.ln1b.as<float>(), L.b2_f.as<float>(), (int)D, s);
@@ -191,6 +202,15 @@ void Encoder::prepare_fold(hipStream_t s) {
     launch_fold_ln_weight(L.wqkv32.as<float>(), P.ln2g.as<float>(), P.ln2b.as<float>(),
                           L.bqkv.as<float>(), (int)(3 * D), (int)D, L.wqkv_f.as<half_t>(),
                           L.cqkv.as<float>(), L.dqkv.as<float>(), s);
+    if (fp8_ >= 2) {
+      L.wqkv8.reserve((size_t)3 * D * D);
+      L.wqkve.reserve((size_t)3 * D);
+      L.cqkv8.reserve((size_t)3 * D * sizeof(float));
+      launch_quantize_rows_fp8(L.wqkv_f.as<half_t>(), (int)(3 * D), (int)D, L.wqkv8.as<uint8_t>(),
+                               L.wqkve.as<uint8_t>(), s);
+      launch_colsum_fp8(L.wqkv8.as<uint8_t>(), L.wqkve.as<uint8_t>(), (int)(3 * D), (int)D,
+                        L.cqkv8.as<float>(), s);
+    }
   }
   fold_ready_ = true;
 }
@@ -215,6 +235,7 @@ void Encoder::ensure_ws(int64_t tokens, int B) {
   ctx_.reserve((size_t)tokens * d * sizeof(half_t));
   y32_.reserve((size_t)tokens * d * sizeof(float));
   ffn_.reserve((size_t)tokens * F * sizeof(half_t));
+  u8_.reserve((size_t)tokens * d);
   if (cfg_.residual_fp16) {
     statA_.reserve((size_t)tokens * (d / 128 + 1) * 2 * sizeof(float));
     statB_.reserve((size_t)tokens * (d / 128 + 1) * 2 * sizeof(float));
@@ -287,6 +308,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       float* sB = statB_.as<float>();
       float* mA = mrA_.as<float>();
       float* mB = mrB_.as<float>();
+      uint8_t* u8 = u8_.as<uint8_t>();
       for (size_t l = 0; l < layers_.size(); ++l) {
         const Layer& L = layers_[l];
         const bool last = cls_only && l + 1 == layers_.size();
@@ -294,6 +316,13 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         if (l == 0) {
           launch_gemm(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
                       3 * d, M, 3 * d, d, s);
+        } else if (fp8_ >= 2) {  // A = e4m3 copy of u (written by the previous FFN2)
+          LnFold lq;
+          lq.mr = mB;
+          lq.colsum = L.cqkv8.as<float>();
+          lq.wexp = L.wqkve.as<uint8_t>();
+          launch_gemm_f8w(EPI_LNF_F16, u8, d, L.wqkv8.as<uint8_t>(), L.dqkv.as<float>(), nullptr, 0,
+                          qkv, 3 * d, M, 3 * d, d, s, &lq);
         } else {  // A = u of the previous block, its LN2 folded into W'
           LnFold lq;
           lq.mr = mB;
@@ -310,7 +339,10 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         lo.stat_ld = last ? S : 1;
         lo.gamma = P ? P->ln2g.as<float>() : nullptr;
         lo.stat_out = sA;
-        launch_gemm(l == 0 ? EPI_RES16_STATS : EPI_LNR16_STATS, ctx, d, L.wo.as<half_t>(),
+        lo.y8 = fp8_ >= 2 ? u8 : nullptr;  // e4m3 copy of u1 for the fp8 FFN1
+        const int eo = fp8_ >= 2 ? (l == 0 ? EPI_RES16_STATS_Y8 : EPI_LNR16_STATS_Y8)
+                                 : (l == 0 ? EPI_RES16_STATS : EPI_LNR16_STATS);
+        launch_gemm(eo, ctx, d, L.wo.as<half_t>(),
                     (l == 0 ? L.bo : L.bo_f).as<float>(), U, last ? (int64_t)S * d : d, Uo, d, Mr,
                     d, d, s, &lo);
         launch_ln_stats_finalize(sA, nparts, cfg_.ln_eps, Mr, mA, s);
@@ -318,15 +350,24 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         LnFold l1;
         l1.mr = mA;
         l1.colsum = L.c1.as<float>();
-        launch_gemm(fp8_ffn_ ? EPI_LNF_GELU_F8 : EPI_LNF_GELU_F16, Uo, d, L.w1_f.as<half_t>(),
-                    L.d1.as<float>(), nullptr, 0, ffn, F, Mr, F, d, s, &l1);
+        if (fp8_ >= 2) {
+          l1.colsum = L.c1_8.as<float>();
+          l1.wexp = L.w1e.as<uint8_t>();
+          launch_gemm_f8w(EPI_LNF_GELU_F8, u8, d, L.w1_8.as<uint8_t>(), L.d1.as<float>(), nullptr, 0,
+                          ffn, F, Mr, F, d, s, &l1);
+        } else {
+          launch_gemm(fp8_ ? EPI_LNF_GELU_F8 : EPI_LNF_GELU_F16, Uo, d, L.w1_f.as<half_t>(),
+                      L.d1.as<float>(), nullptr, 0, ffn, F, Mr, F, d, s, &l1);
+        }
         LnFold l2;
         l2.mr = mA;
         l2.gamma = L.ln1g.as<float>();
         l2.stat_out = sB;
-        if (fp8_ffn_)  // ffn holds e4m3 bytes (F per row)
-          launch_gemm_f8w(reinterpret_cast<const uint8_t*>(ffn), F, L.w2_8.as<uint8_t>(),
-                          L.w2e.as<uint8_t>(), L.b2_f.as<float>(), Uo, d, Uo, d, Mr, d, F, s, &l2);
+        l2.wexp = L.w2e.as<uint8_t>();
+        l2.y8 = (fp8_ >= 2 && !last) ? u8 : nullptr;  // e4m3 copy of u2 for the next QKV
+        if (fp8_)  // ffn holds e4m3 bytes (F per row)
+          launch_gemm_f8w(l2.y8 ? EPI_LNR16_STATS_Y8 : EPI_LNR16_STATS, reinterpret_cast<const uint8_t*>(ffn), F,
+                          L.w2_8.as<uint8_t>(), L.b2_f.as<float>(), Uo, d, Uo, d, Mr, d, F, s, &l2);
         else
           launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2h.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo,
                       d, Mr, d, F, s, &l2);

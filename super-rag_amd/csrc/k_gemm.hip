@@ -232,10 +232,11 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
                                                 void* __restrict__ Y, int64_t ldy,
                                                 const LnFold& lf) {
   constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;  // e4m3 bytes instead of fp16
+  constexpr bool Y8 = EPI == EPI_RES16_STATS_Y8 || EPI == EPI_LNR16_STATS_Y8;  // + e4m3 copy
   constexpr bool LNF = EPI == EPI_LNF_F16 || EPI == EPI_LNF_GELU_F16 || OUT8;
-  constexpr bool RESN = EPI == EPI_BIAS_RES_F16 || EPI == EPI_RES16_STATS;
-  constexpr bool LNR = EPI == EPI_LNR16_STATS;
-  constexpr bool STATS = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS;
+  constexpr bool RESN = EPI == EPI_BIAS_RES_F16 || EPI == EPI_RES16_STATS || EPI == EPI_RES16_STATS_Y8;
+  constexpr bool LNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
+  constexpr bool STATS = (RESN && EPI != EPI_BIAS_RES_F16) || LNR;
   constexpr bool GELU = EPI == EPI_BIAS_GELU_F16;
   constexpr bool GELU2 = EPI == EPI_LNF_GELU_F16 || OUT8;  // stores 2 * GELU (consumer weight halved)
   static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
@@ -333,6 +334,14 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 #pragma unroll
         for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
         *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
+        if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+          {
+            uint2 q8;
+            q8.x = e4m3x4((float)hv[p][0], (float)hv[p][1], (float)hv[p][2], (float)hv[p][3]);
+            q8.y = e4m3x4((float)hv[p][4], (float)hv[p][5], (float)hv[p][6], (float)hv[p][7]);
+            *reinterpret_cast<uint2*>(lf.y8 + (int64_t)m * ldy + nlane + 32 * p) = q8;
+          }
+        }
       }
     }
     if constexpr (STATS) {
@@ -476,7 +485,7 @@ __device__ __forceinline__ void stage_offsets(uint32_t (&voff)[NI], int64_t ld, 
 // MFMAs instead of stalling the CU.
 // DIAG (timing experiments only, wrong results): 1 = no glds inside the K-loop (LDS re-read),
 // 2 = no epilogue (one masked store per lane keeps the accumulators live).
-template <int EPI, bool PERSIST, int DIAG = 0>
+template <int EPI, bool PERSIST, int DIAG = 0, bool F8IN = false>
 __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
@@ -485,10 +494,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr int STAGE = (BN + BM) * GBK;  // halfs per buffer (64 KiB)
   // fp8 operands (EPI_SCAN8): K, lda count 2-byte units, so the staging below moves the same
   // 128-byte K-step rows; a K-step then holds 128 fp8 elements
-  constexpr bool F8W = EPI == EPI_LNR16_STATS_F8;  // fp8 activations x fp8 weights (row scales)
+  constexpr bool F8W = F8IN;  // fp8 activations x fp8 weights (row exponents in lf.wexp)
   constexpr bool F8 = EPI == EPI_SCAN8 || F8W;
   constexpr bool SCAN = EPI == EPI_SCAN || EPI == EPI_SCAN8;
-  constexpr int EPI_OUT = F8W ? EPI_LNR16_STATS : EPI;  // the epilogue that runs
+  constexpr int EPI_OUT = EPI;
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
@@ -722,7 +731,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
     if constexpr (F8W) {
-      const uint8_t* wexp = reinterpret_cast<const uint8_t*>(lf.colsum);
+      const uint8_t* wexp = lf.wexp;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int n = n0 + arow + 16 * i;
@@ -1129,6 +1138,8 @@ static const char* epi_name(int epi) {
     case EPI_RES16_STATS: return "gemm_f16_residual16_stats";
     case EPI_LNR16_STATS: return "gemm_f16_lnres16_stats";
     case EPI_LNF_GELU_F8: return "gemm_f16_lnfold_gelu_out8";
+    case EPI_RES16_STATS_Y8: return "gemm_f16_residual16_stats_y8";
+    case EPI_LNR16_STATS_Y8: return "gemm_f16_lnres16_stats_y8";
     default: return "gemm_f16_bias_tanh";
   }
 }
@@ -1183,30 +1194,81 @@ void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t
   SR_LAUNCH_CHECK();
 }
 
-void launch_gemm_f8w(const uint8_t* X8, int64_t lda, const uint8_t* W8, const uint8_t* wexp,
-                     const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy, int M,
-                     int N, int K, hipStream_t stream, const LnFold* lf) {
+void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8, const float* bias,
+                     const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
+                     hipStream_t stream, const LnFold* lf) {
+  SR_CHECK(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F8 || epi == EPI_RES16_STATS ||
+               epi == EPI_LNR16_STATS || epi == EPI_RES16_STATS_Y8 || epi == EPI_LNR16_STATS_Y8,
+           "gemm_f8w: unsupported epilogue");
+  const bool y8 = epi == EPI_RES16_STATS_Y8 || epi == EPI_LNR16_STATS_Y8;
+  const bool lnr = epi == EPI_LNR16_STATS || epi == EPI_LNR16_STATS_Y8;
+  const bool stats = lnr || epi == EPI_RES16_STATS || epi == EPI_RES16_STATS_Y8;
   SR_CHECK(K % 128 == 0 && K >= 256, "gemm_f8w: K must be a multiple of 128, >= 256");
   SR_CHECK(N % 256 == 0, "gemm_f8w: N must be a multiple of 256");
   SR_CHECK(lda % 16 == 0 && ldy % 8 == 0 && ldr % 8 == 0, "gemm_f8w: 16-byte rows");
-  SR_CHECK(lf && lf->mr && lf->gamma && lf->stat_out && wexp, "gemm_f8w: LnFold mr / gamma / stat_out, wexp");
+  SR_CHECK(lf && lf->wexp, "gemm_f8w: the weight rows' exponents (LnFold.wexp)");
+  SR_CHECK((stats && !lnr) || lf->mr, "gemm_f8w: LN-folded operand needs its row statistics");
+  SR_CHECK(stats || lf->colsum, "gemm_f8w: LNF needs colsum");
+  SR_CHECK(!lnr || lf->gamma, "gemm_f8w: LNR needs the LayerNorm weight");
+  SR_CHECK(!stats || lf->stat_out, "gemm_f8w: stat_out");
+  SR_CHECK(!y8 || lf->y8, "gemm_f8w: the e4m3-copy epilogues need LnFold.y8");
   if (M <= 0) return;
-  ProfScope prof("gemm_f8_lnres16_stats", stream, 2.0 * M * (double)N * K,
-                 (double)M * K + (double)N * K + 4.0 * (double)M * N);
-  LnFold lfv = *lf;
-  lfv.colsum = reinterpret_cast<const float*>(wexp);  // (field re-use: the weight rows' exponents)
+  const char* name = epi == EPI_LNF_F16 ? "gemm_f8_lnfold" : epi == EPI_LNF_GELU_F8 ? "gemm_f8_lnfold_gelu_out8"
+                     : !stats ? "gemm_f8" : !lnr ? (y8 ? "gemm_f8_residual16_stats_y8" : "gemm_f8_residual16_stats")
+                     : (y8 ? "gemm_f8_lnres16_stats_y8" : "gemm_f8_lnres16_stats");
+  const double out_b = epi == EPI_LNF_GELU_F8 ? 1.0 : 2.0, res_b = stats ? 2.0 : 0.0;
+  ProfScope prof(name, stream, 2.0 * M * (double)N * K,
+                 (double)M * K + (double)N * K + (out_b + res_b + (y8 ? 1.0 : 0.0)) * (double)M * N);
+  const LnFold lfv = *lf;
   const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
+  const bool persist = tiles >= 512;
+  const dim3 grid(persist ? (unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8))) : (unsigned)tiles);
   // operands as 2-byte units: K / 2, lda / 2 (the staging moves bytes)
-  if (tiles >= 512) {
-    const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
-    hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNR16_STATS_F8, true>), grid, block, 0, stream,
-                       reinterpret_cast<const half_t*>(X8), lda / 2, reinterpret_cast<const half_t*>(W8),
-                       bias, R, ldr, Y, ldy, M, N, K / 2, lfv);
-  } else {
-    hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNR16_STATS_F8, false>), dim3((unsigned)tiles), dim3(512), 0,
-                       stream, reinterpret_cast<const half_t*>(X8), lda / 2,
-                       reinterpret_cast<const half_t*>(W8), bias, R, ldr, Y, ldy, M, N, K / 2, lfv);
+  const half_t* x = reinterpret_cast<const half_t*>(X8);
+  const half_t* w = reinterpret_cast<const half_t*>(W8);
+#define SR_F8_CASE(E)                                                                            \
+  case E:                                                                                        \
+    if (persist)                                                                                 \
+      hipLaunchKernelGGL((gemm_pipe_kernel<E, true, 0, true>), grid, dim3(512), 0, stream, x,     \
+                         lda / 2, w, bias, R, ldr, Y, ldy, M, N, K / 2, lfv);                    \
+    else                                                                                         \
+      hipLaunchKernelGGL((gemm_pipe_kernel<E, false, 0, true>), grid, dim3(512), 0, stream, x,    \
+                         lda / 2, w, bias, R, ldr, Y, ldy, M, N, K / 2, lfv);                    \
+    break;
+  switch (epi) {
+    SR_F8_CASE(EPI_LNF_F16)
+    SR_F8_CASE(EPI_LNF_GELU_F8)
+    SR_F8_CASE(EPI_RES16_STATS)
+    SR_F8_CASE(EPI_LNR16_STATS)
+    SR_F8_CASE(EPI_RES16_STATS_Y8)
+    SR_F8_CASE(EPI_LNR16_STATS_Y8)
+    default: break;
   }
+#undef SR_F8_CASE
+  SR_LAUNCH_CHECK();
+}
+
+__device__ __forceinline__ float e4m3_decode(uint32_t b) {
+  const uint32_t e = (b >> 3) & 15u, m = b & 7u;
+  const float v = e ? ldexpf(1.f + (float)m * 0.125f, (int)e - 7) : ldexpf((float)m, -9);
+  return (b & 0x80u) ? -v : v;
+}
+
+__global__ void colsum_fp8_kernel(const uint8_t* __restrict__ W8, const uint8_t* __restrict__ wexp,
+                                  int N, int K, float* __restrict__ colsum) {
+  const int n = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int k = lane; k < K; k += 64) acc += e4m3_decode(W8[(int64_t)n * K + k]);
+  acc = wave_sum(acc);
+  if (lane == 0) colsum[n] = ldexpf(acc, (int)wexp[n] - 127);
+}
+
+void launch_colsum_fp8(const uint8_t* W8, const uint8_t* wexp, int N, int K, float* colsum,
+                       hipStream_t s) {
+  if (N <= 0) return;
+  hipLaunchKernelGGL(colsum_fp8_kernel, dim3((unsigned)ceil_div(N, 4)), dim3(256), 0, s, W8, wexp,
+                     N, K, colsum);
   SR_LAUNCH_CHECK();
 }
 
@@ -1266,21 +1328,27 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   SR_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128");
   SR_CHECK(lda % 8 == 0 && ldy % 4 == 0, "gemm: leading dimensions must keep 16-byte rows");
   const bool fold = epi >= EPI_LNF_F16;
-  SR_CHECK((epi >= 0 && epi <= EPI_LNR16_STATS) || epi == EPI_LNF_GELU_F8, "gemm: unknown epilogue");
+  SR_CHECK((epi >= 0 && epi <= EPI_LNR16_STATS) || epi == EPI_LNF_GELU_F8 ||
+               epi == EPI_RES16_STATS_Y8 || epi == EPI_LNR16_STATS_Y8, "gemm: unknown epilogue");
+  SR_CHECK(!(epi == EPI_RES16_STATS_Y8 || epi == EPI_LNR16_STATS_Y8) || (lf && lf->y8),
+           "gemm: the e4m3-copy epilogues need LnFold.y8");
   SR_CHECK(!fold || (lf && N % 256 == 0), "gemm: LayerNorm-folded epilogues need LnFold, N % 256");
   SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNF_GELU_F8 ||
-             epi == EPI_LNR16_STATS) || lf->mr,
+             epi == EPI_LNR16_STATS || epi == EPI_LNR16_STATS_Y8) || lf->mr,
            "gemm: LN-folded operand needs its row statistics");
   SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNF_GELU_F8) || lf->colsum,
            "gemm: LNF needs colsum");
-  SR_CHECK(epi != EPI_LNR16_STATS || lf->gamma, "gemm: LNR needs the LayerNorm weight");
-  SR_CHECK(!(epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS) || lf->stat_out,
+  SR_CHECK(!(epi == EPI_LNR16_STATS || epi == EPI_LNR16_STATS_Y8) || lf->gamma,
+           "gemm: LNR needs the LayerNorm weight");
+  SR_CHECK(!(epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS || epi == EPI_RES16_STATS_Y8 ||
+             epi == EPI_LNR16_STATS_Y8) || lf->stat_out,
            "gemm: *_STATS epilogue needs stat_out");
   if (M <= 0) return;
   const bool out32 = epi == EPI_BIAS_RES_F32 || epi == EPI_BIAS_TANH_F32;
   const double out_b = out32 ? 4.0 : epi == EPI_LNF_GELU_F8 ? 1.0 : 2.0;
   const double res_b = epi == EPI_BIAS_RES_F32 ? 4.0
-                       : (epi == EPI_BIAS_RES_F16 || epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS) ? 2.0
+                       : (epi == EPI_BIAS_RES_F16 || epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS ||
+                          epi == EPI_RES16_STATS_Y8 || epi == EPI_LNR16_STATS_Y8) ? 2.0
                                                                                                      : 0.0;
   const double bytes = 2.0 * ((double)M * K + (double)N * K) + (out_b + res_b) * (double)M * N;
   ProfScope prof(epi_name(epi), stream, 2.0 * M * (double)N * K, bytes);
@@ -1289,12 +1357,12 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   int v = variant >= 0 ? variant : forced_tile();
   if (v < 0) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_SMALL;
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
-  if (v == GEMM_PP && (K % 32 != 0 || epi == EPI_LNF_GELU_F8)) v = GEMM_PIPE;
+  if (v == GEMM_PP && (K % 32 != 0 || epi >= EPI_LNF_GELU_F8)) v = GEMM_PIPE;
   if (fold && (v == GEMM_SMALL || v == GEMM_BIG)) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_PIPE;
   const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST || v == GEMM_PP) && !out32;
   SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
-  SR_CHECK(epi != EPI_LNF_GELU_F8 || v == GEMM_PIPE || v == GEMM_PIPE_PERSIST,
-           "gemm: the fp8-output epilogue runs on the pipelined kernels");
+  SR_CHECK(epi < EPI_LNF_GELU_F8 || v == GEMM_PIPE || v == GEMM_PIPE_PERSIST,
+           "gemm: the e4m3-output epilogues run on the pipelined kernels");
   const LnFold lfv = lf ? *lf : LnFold{};
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
@@ -1366,6 +1434,8 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
       SR_PIPE_CASE(EPI_RES16_STATS)
       SR_PIPE_CASE(EPI_LNR16_STATS)
       SR_PIPE_CASE(EPI_LNF_GELU_F8)
+      SR_PIPE_CASE(EPI_RES16_STATS_Y8)
+      SR_PIPE_CASE(EPI_LNR16_STATS_Y8)
       default: SR_CHECK(false, "gemm: unknown epilogue");
     }
 #undef SR_PIPE_CASE

@@ -25,11 +25,12 @@ enum Epilogue {
   // the same on OCP fp8-e4m3 operands e4m3(256 x) of unit vectors (block-scaled MFMA
   // v_mfma_scale_f32_16x16x128_f8f6f4, E8M0 block scales 2^-8 undo the factor)
   EPI_SCAN8 = 10,
-  // fp8 FFN (Encoder fp8_ffn mode): FFN1 = EPI_LNF_GELU_F16 storing OCP e4m3(2 GELU) bytes; FFN2 =
-  // EPI_LNR16_STATS on e4m3 activations x e4m3 weights (per-row power-of-two scales of the weight
-  // as the block-scaled MFMA's E8M0 A scales; launch_gemm_f8w)
+  // EPI_LNF_GELU_F16 storing OCP e4m3(2 GELU) bytes (the fp8 FFN1; its consumer runs fp8)
   EPI_LNF_GELU_F8 = 11,
-  EPI_LNR16_STATS_F8 = 12
+  // EPI_RES16_STATS / EPI_LNR16_STATS that also store an e4m3 copy of their fp16 output to
+  // LnFold.y8 (the next fp8 GEMM's A operand; separate codes keep the fp16 kernels' registers)
+  EPI_RES16_STATS_Y8 = 12,
+  EPI_LNR16_STATS_Y8 = 13
 };
 
 // Per-row statistics hand-over between GEMMs (Chan-combinable partials over 128-column spans):
@@ -42,6 +43,9 @@ struct LnFold {
   const float* gamma = nullptr;    // LNR: LayerNorm weight of the residual rows (its beta is
                                    //      pre-added to the GEMM bias)
   float* stat_out = nullptr;       // *_STATS: [M][N / 128] partials of the output rows
+  const uint8_t* wexp = nullptr;   // fp8 operands (launch_gemm_f8w): E8M0 exponent per weight row
+  uint8_t* y8 = nullptr;           // *_STATS: optional e4m3 copy of the fp16 output (row stride
+                                   //          ldy bytes), the next fp8 GEMM's A operand
   // EPI_SCAN(8) re-uses the fields (kernel-argument SGPRs are scarce in the persistent kernels):
   // stat_out = per-query candidate counts (int*), stat_ld = global row id of the chunk's first
   // row; bias = tau[B], R = live flags of the chunk, Y = candidate keys [B][cap] (ldy = cap).
@@ -60,11 +64,15 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
 void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 // K1 for large query blocks (B in (128, 256]) on the pipelined GEMM: rows [r0, r1) of the corpus
 // against B queries; non-dense threshold mode only (same contract as launch_cosine_scan).
-// Y = EPI_LNR16_STATS(X8 . W8^T) on OCP e4m3 operands: X8 [M][K] bytes (lda bytes), W8 [N][K] bytes
-// with per-row E8M0 exponents wexp[N] (W = W8 * 2^(wexp - 127)); K % 128 == 0, K >= 256.
-void launch_gemm_f8w(const uint8_t* X8, int64_t lda, const uint8_t* W8, const uint8_t* wexp,
-                     const float* bias, const void* R, int64_t ldr, void* Y, int64_t ldy, int M,
-                     int N, int K, hipStream_t stream, const LnFold* lf);
+// Y = epi(X8 . W8^T) on OCP e4m3 operands: X8 [M][K] bytes (lda bytes), W8 [N][K] bytes with
+// per-row E8M0 exponents lf->wexp[N] (W = W8 * 2^(wexp - 127)); K % 128 == 0, K >= 256;
+// epi in {EPI_LNF_F16, EPI_LNF_GELU_F8, EPI_RES16_STATS(_Y8), EPI_LNR16_STATS(_Y8)}.
+void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8, const float* bias,
+                     const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
+                     hipStream_t stream, const LnFold* lf);
+// colsum[n] = sum_k W8[n][k] * 2^(wexp[n] - 127) (the LN fold's column sums of an e4m3 weight)
+void launch_colsum_fp8(const uint8_t* W8, const uint8_t* wexp, int N, int K, float* colsum,
+                       hipStream_t s);
 // W [N][K] fp16 -> W8 [N][K] e4m3 of W * 2^e_n (largest power of two with max|W_n| 2^e_n <= 448),
 // wexp[n] = 127 - e_n
 void launch_quantize_rows_fp8(const half_t* W, int N, int K, uint8_t* W8, uint8_t* wexp,

@@ -133,9 +133,10 @@ class Encoder {
                     int mode, int pool, float* out);
 
   const sr_encoder_config& config() const { return cfg_; }
-  // fp8 FFN mode (LN-folded encoders): FFN1 stores e4m3(2 GELU), FFN2 runs the block-scaled fp8
-  // MFMA on it and an e4m3 copy of its weight (per-row power-of-two scales)
-  void set_fp8_ffn(bool on);
+  // fp8 modes (LN-folded encoders): 1 = FFN (FFN1 stores e4m3(2 GELU), FFN2 on the block-scaled
+  // fp8 MFMA with an e4m3 copy of its weight); 2 = also FFN1 and the QKV GEMMs of layers >= 1 on
+  // e4m3 copies of the residual sums written by the *_STATS epilogues; 0 = fp16
+  void set_fp8(int mode);
   int device() const { return device_; }
   std::mutex mu;
 
@@ -150,8 +151,9 @@ class Encoder {
     DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, w1, b1, w2, b2, ln2g, ln2b;
     // LayerNorm folding (fp16 residual stream): fp32 masters and the folded copies
     DevBuf wqkv32, w132, wqkv_f, cqkv, dqkv, w1_f, c1, d1, bo_f, b2_f, w2h;
-    // fp8 FFN mode: e4m3 copy of w2h and its per-row exponents
-    DevBuf w2_8, w2e;
+    // fp8 modes: e4m3 copies of w2h (FFN) and of the folded w1_f / wqkv_f (all), their per-row
+    // exponents and the folded column sums of the quantised weights
+    DevBuf w2_8, w2e, w1_8, w1e, c1_8, wqkv8, wqkve, cqkv8;
   };
   bool fold_enabled() const;
   void prepare_fold(hipStream_t s);
@@ -174,7 +176,8 @@ class Encoder {
   DevBuf ids_, mask_, types_, pos_, h16_, h32_, qkv_, ctx_, y32_, ffn_, clst_, hostio_;
   DevBuf statA_, statB_, mrA_, mrB_;  // per-row LayerNorm partials / (mu, rstd) (folded path)
   bool fold_ready_ = false;  // folded weights match the current weights
-  bool fp8_ffn_ = false;
+  int fp8_ = 0;
+  DevBuf u8_;  // e4m3 copy of the residual sums (fp8 mode 2)
   int64_t ws_tokens_ = 0;
 };
 

@@ -112,7 +112,7 @@ SIGNATURES = {
     "sr_cross_score": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "sr_cross_score_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                    c_void_p, c_void_p]),
-    "sr_encoder_set_fp8_ffn": (c_int, [c_void_p, c_int]),
+    "sr_encoder_set_fp8": (c_int, [c_void_p, c_int]),
     "sr_encoder_destroy": (None, [c_void_p]),
     "sr_build_pairs_dev": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,

@@ -188,10 +188,14 @@ class Encoder:
             N.call("sr_encoder_set_weight", self._h, name.encode(), N.ptr(a), a.size)
         N.call("sr_encoder_ready", self._h)
 
+    def set_fp8(self, mode: int) -> None:
+        """Opt-in fp8 precision mode (LN-folded fp16-residual encoders, e.g. cross-encoders):
+        1 = FFN (e4m3 FFN activations, FFN2 on the block-scaled fp8 MFMA), 2 = also FFN1 and QKV
+        of layers >= 1 on e4m3 copies of the residual sums, 0 = fp16 (sr_encoder_set_fp8)."""
+        N.call("sr_encoder_set_fp8", self._h, int(mode))
+
     def set_fp8_ffn(self, on: bool = True) -> None:
-        """Opt-in fp8 FFN precision mode (LN-folded fp16-residual encoders, e.g. cross-encoders):
-        FFN1 writes e4m3 activations, FFN2 runs the block-scaled fp8 MFMA (sr_encoder_set_fp8_ffn)."""
-        N.call("sr_encoder_set_fp8_ffn", self._h, 1 if on else 0)
+        self.set_fp8(1 if on else 0)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

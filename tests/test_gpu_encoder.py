@@ -246,6 +246,53 @@ def test_fp8_ffn_cross_encoder(S):
     np.testing.assert_array_equal(enc.cross_score(ids, mask), got16)
 
 
+@pytest.mark.parametrize("S", [16, 130])
+def test_fp8_mode2_cross_encoder(S):
+    # fp8 mode 2: FFN1 and the QKV of layers >= 1 also run the block-scaled fp8 MFMA, on e4m3
+    # copies of the pre-LN residual sums (written by the Wo / FFN2 epilogues) against e4m3 row
+    # copies of the LN-folded weights.  Against the oracle restating that quantisation
+    # (oracle/encoder_ref.py _fold8) the band is the fp8 FFN test's; against fp32 the fp8 rounding.
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("xlmr", d=256, H=4, F=512, L=3, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=34, style="test")
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 33, S, seed=S + 3)
+    got1 = (enc.set_fp8(1), enc.cross_score(ids, mask))[1]
+    enc.set_fp8(2)
+    got2 = enc.cross_score(ids, mask)
+    ref2 = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8=2)
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)
+    scale = 1.0 + np.abs(ref).max()
+    assert not np.array_equal(got2, got1)
+    assert np.abs(got2 - ref2).max() <= 8e-3 * scale
+    assert np.abs(got2 - ref).max() <= 5e-2 * scale
+    enc.set_fp8(1)
+    np.testing.assert_array_equal(enc.cross_score(ids, mask), got1)
+
+
+def test_fp8_mode2_persistent_tiles():
+    # 143k tokens: the persistent fp8 QKV / FFN1 / FFN2 kernels and the _Y8 epilogues
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("xlmr", d=256, H=4, F=512, L=2, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=35, style="test")
+    enc = Encoder(spec, weights=w, max_tokens=1 << 18)
+    enc.set_fp8(2)
+    ids, mask = _batch(spec, 1100, 130, seed=8, ragged=False)
+    got = enc.cross_score(ids, mask)
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8=2)
+    assert np.abs(got - ref).max() <= 8e-3 * (1.0 + np.abs(ref).max())
+
+
+def test_fp8_mode_rejects_unfolded_encoder():
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("bert", d=256, H=4, F=512, L=2)
+    enc = Encoder(spec, weights=random_weights(spec, seed=36, style="test"))
+    with pytest.raises(RuntimeError):
+        enc.set_fp8(2)
+    with pytest.raises(RuntimeError):
+        enc.set_fp8(3)
+
+
 def test_fp8_ffn_persistent_tiles():
     # enough rows (143k tokens) for the persistent fp8 FFN2 / e4m3-output FFN1 kernels
     from super_rag_amd.encoder import Encoder, random_weights

@@ -29,16 +29,20 @@ EPI_NAMES = {0: "gemm_f16_bias", 1: "gemm_f16_bias_gelu", 2: "gemm_f16_bias_resi
              8: "gemm_f16_lnres16_stats",
              9: "cosine_scan",    # K1 threshold chunks on the GEMM main loop (EPI_SCAN)
              10: "cosine_scan8",  # the fp8 scan (EPI_SCAN8)
-             11: "gemm_f16_lnfold_gelu_out8", 12: "gemm_f8_lnres16_stats"}
+             11: "gemm_f16_lnfold_gelu_out8", 12: "gemm_f16_residual16_stats_y8",
+             13: "gemm_f16_lnres16_stats_y8"}
 
 
 def logical(name):
     """Mangled HIP kernel name -> the library's logical kernel name (None for foreign kernels)."""
     if "_ZN2sr" not in name and not name.startswith("sr::"):
         return None
-    m = re.search(r"gemm_\w*?kernelILi(\d+)E", name)
+    m = re.search(r"gemm_\w*?kernelILi(\d+)E(\w*)", name)
     if m:
-        return EPI_NAMES.get(int(m.group(1)), f"gemm_epi{m.group(1)}")
+        base = EPI_NAMES.get(int(m.group(1)), f"gemm_epi{m.group(1)}")
+        if m.group(2).startswith("Lb") and m.group(2)[3:].startswith("Li0ELb1E"):  # F8IN variant
+            base = base.replace("gemm_f16_", "gemm_f8_")
+        return base
     m = re.search(r"\d+([a-z0-9_]+?)_kernel", name) or re.search(r"::(\w+?)_kernel", name)
     base = m.group(1) if m else name
     if base.startswith("attention"):
