@@ -176,13 +176,19 @@ __device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
   return __builtin_bit_cast(half4, v);
 }
 
-__global__ __launch_bounds__(256) void attention64_kernel(const half_t* __restrict__ qkv,
-                                                          const int32_t* __restrict__ mask,
-                                                          half_t* __restrict__ ctx, int S, int Sq,
-                                                          int d, float scale_log2) {
+// SPLIT (S_pad == 128, all four waves active): the Q fragments and the key mask are requested
+// first, then K (LDS-DMA), then V into registers; the score / softmax phase starts once Q and K
+// have landed (vmcnt(4): each wave's four V loads may still be in flight) and V is written to its
+// LDS image (same swizzle) only before the first P.V MFMA, so V's HBM latency overlaps QK^T +
+// softmax.  (V by LDS-DMA would make the compiler wait vmcnt(0) before every ds_read of K.)  amdgpu_waves_per_eu(3): 168
+// VGPRs, three workgroups per CU (two query tiles per wave stay interleaved for MFMA ILP).
+template <bool SPLIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attention64_kernel(
+    const half_t* __restrict__ qkv, const int32_t* __restrict__ mask, half_t* __restrict__ ctx,
+    int S, int Sq, int d, float scale_log2) {
   constexpr int DH = 64;
   extern __shared__ __attribute__((aligned(16))) char a2_smem[];
-  const int S_pad = (S + 31) & ~31;
+  const int S_pad = SPLIT ? 128 : (S + 31) & ~31;
   half_t* Ks = reinterpret_cast<half_t*>(a2_smem);
   half_t* Vs = Ks + S_pad * DH;
   float* kbias = reinterpret_cast<float*>(Vs + S_pad * DH);
@@ -193,34 +199,87 @@ __global__ __launch_bounds__(256) void attention64_kernel(const half_t* __restri
   const int64_t ld = 3 * (int64_t)d;
   const half_t* base = qkv + (int64_t)b * S * ld + h * DH;
 
-  // ---- stage K and V (rows >= S replicate row S-1; their keys are masked) ----
-  for (int piece = wave; piece < S_pad / 8; piece += 4) {
-    const int r = piece * 8 + (lane >> 3);
-    const int rr = r < S ? r : S - 1;
-    const half_t* rowp = base + (int64_t)rr * ld;
-    __builtin_amdgcn_global_load_lds((const void*)(rowp + d + a2_kswz(r, lane & 7) * 8),
-                                     SR_LDS(Ks + piece * 8 * DH), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(rowp + 2 * d + a2_vswz(r, lane & 7) * 8),
-                                     SR_LDS(Vs + piece * 8 * DH), 16, 0, 0);
-  }
-  for (int r = tid; r < S_pad; r += 256)
-    kbias[r] = (r < S && mask[(int64_t)b * S + r] != 0) ? 0.f : -INFINITY;
-
-  // ---- Q fragments (B operand of S^T): lane holds Q[q][8 (lane>>4) + 32 s .. +7] ----
   const int qw = blockIdx.x * A2_QB + wave * 32;  // first query row of this wave
   const bool active = qw < Sq;
   half8 qf[2][2];
+  half8 vreg[4];  // SPLIT: this wave's V pieces (written to the LDS image after the softmax)
+  if constexpr (SPLIT) {
+    // Q rows (this workgroup's 128), the key mask words and K by LDS-DMA, then V into registers:
+    // no register result is needed before the V loads issue, so one counted wait (vmcnt(4) = all
+    // but this wave's 4 V loads) publishes Q, mask and K.
+    half_t* Qs = reinterpret_cast<half_t*>(kbias + S_pad);  // 128 rows x 128 B, K's swizzle
+    int32_t* ms = reinterpret_cast<int32_t*>(kbias);
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    int qr = qw + 16 * u + (lane & 15);
-    qr = qr < S ? qr : S - 1;
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave + 4 * i;
+      const int r = piece * 8 + (lane >> 3);
+      const int rq = blockIdx.x * A2_QB + r;
+      __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(rq < S ? rq : S - 1) * ld +
+                                                     a2_kswz(r, lane & 7) * 8),
+                                       SR_LDS(Qs + piece * 8 * DH), 16, 0, 0);
+    }
+    if (wave < 2) {
+      const int r = wave * 64 + lane;
+      __builtin_amdgcn_global_load_lds((const void*)(mask + (int64_t)b * S + (r < S ? r : S - 1)),
+                                       SR_LDS(ms + wave * 64), 4, 0, 0);
+    }
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-      qf[u][s2] = *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + 8 * (lane >> 4) + 32 * s2);
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave + 4 * i;
+      const int r = piece * 8 + (lane >> 3);
+      __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(r < S ? r : S - 1) * ld + d +
+                                                     a2_kswz(r, lane & 7) * 8),
+                                       SR_LDS(Ks + piece * 8 * DH), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (wave + 4 * i) * 8 + (lane >> 3);
+      vreg[i] = *reinterpret_cast<const half8*>(base + (int64_t)(r < S ? r : S - 1) * ld + 2 * d +
+                                                a2_vswz(r, lane & 7) * 8);
+    }
+    SR_WAITCNT(4, 0);
+    __builtin_amdgcn_s_barrier();
+    // mask words -> additive key bias in place (keys >= S masked), then the Q fragments
+    if (wave < 2) {
+      const int r = wave * 64 + lane;
+      const int32_t m = ms[r];
+      kbias[r] = (r < S && m != 0) ? 0.f : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = wave * 32 + 16 * u + (lane & 15);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        qf[u][s2] = *reinterpret_cast<const half8*>(Qs + r * DH + a2_kswz(r, (lane >> 4) + 4 * s2) * 8);
+    }
+    SR_WAITCNT(4, 0);
+    __builtin_amdgcn_s_barrier();
+  } else {
+    // ---- Q fragments (B operand of S^T): lane holds Q[q][8 (lane>>4) + 32 s .. +7] ----
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int qr = qw + 16 * u + (lane & 15);
+      qr = qr < S ? qr : S - 1;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        qf[u][s2] = *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + 8 * (lane >> 4) + 32 * s2);
+    }
+    // ---- stage K and V (rows >= S replicate row S-1; their keys are masked) ----
+    for (int piece = wave; piece < S_pad / 8; piece += 4) {
+      const int r = piece * 8 + (lane >> 3);
+      const int rr = r < S ? r : S - 1;
+      const half_t* rowp = base + (int64_t)rr * ld;
+      __builtin_amdgcn_global_load_lds((const void*)(rowp + d + a2_kswz(r, lane & 7) * 8),
+                                       SR_LDS(Ks + piece * 8 * DH), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(rowp + 2 * d + a2_vswz(r, lane & 7) * 8),
+                                       SR_LDS(Vs + piece * 8 * DH), 16, 0, 0);
+    }
+    for (int r = tid; r < S_pad; r += 256)
+      kbias[r] = (r < S && mask[(int64_t)b * S + r] != 0) ? 0.f : -INFINITY;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (!active) return;  // no barrier follows
+  if (!SPLIT && !active) return;  // no barrier follows
 
   const int g = lane >> 4;
   float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
@@ -281,6 +340,13 @@ __global__ __launch_bounds__(256) void attention64_kernel(const half_t* __restri
     }
     // ---- O^T += V^T P^T over 32-key chunks (key order of the B operand: 32c + 4g + j, then
     //      32c + 16 + 4g + j; the transposed V reads use the same order) ----
+    if constexpr (SPLIT) {  // one key block: V lands in LDS here, once
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<half8*>(Vs + (wave + 4 * i) * 8 * DH + lane * 8) = vreg[i];
+      SR_WAITCNT(0, 0);
+      __builtin_amdgcn_s_barrier();
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       if (2 * c < nkt) {
@@ -358,10 +424,15 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
   const bool use_b = dh == 64 && S <= 512 && g_attn_variant != 0;
   if (use_b) {
     const int S_pad = (S + 31) & ~31;
-    const size_t shmem = (size_t)2 * S_pad * 64 * sizeof(half_t) + (size_t)S_pad * sizeof(float);
+    const bool split = S_pad == 128 && Sq > 96;  // K5b SPLIT: one key block, all waves active
+    const size_t shmem = (size_t)(split ? 3 : 2) * S_pad * 64 * sizeof(half_t) + (size_t)S_pad * sizeof(float);
     dim3 grid((unsigned)ceil_div(Sq, A2_QB), heads, B), block(256);
-    hipLaunchKernelGGL(attention64_kernel, grid, block, shmem, stream, qkv, mask, ctx, S, Sq, d,
-                       scale_log2);
+    if (split)
+      hipLaunchKernelGGL(attention64_kernel<true>, grid, block, shmem, stream, qkv, mask, ctx, S, Sq,
+                         d, scale_log2);
+    else
+      hipLaunchKernelGGL(attention64_kernel<false>, grid, block, shmem, stream, qkv, mask, ctx, S, Sq,
+                         d, scale_log2);
   } else {
     const int nw = (int)std::min<int64_t>(4, ceil_div(Sq, 16));
     dim3 grid((unsigned)ceil_div(Sq, 16 * nw), heads, B), block(64 * nw);

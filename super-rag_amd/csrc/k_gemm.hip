@@ -31,12 +31,6 @@ namespace {
 
 constexpr int GBK = 64;  // k per stage
 
-// s_waitcnt through the builtin (the compiler's own waitcnt pass then knows the counters are
-// satisfied; an asm waitcnt is invisible to it and it re-waits conservatively). gfx9 encoding:
-// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
-#define SR_WAITCNT(vm, lgkm) \
-  __builtin_amdgcn_s_waitcnt(((vm) & 15) | (7 << 4) | (((lgkm) & 15) << 8) | (((vm) >> 4) << 14))
-
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 // Issue NI glds wave-instructions of one tile: instruction i of this wave fills LDS rows

@@ -62,6 +62,12 @@ static inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b
 // Device pointer helpers for LDS address space.
 #define SR_LDS(p) ((__attribute__((address_space(3))) void*)(p))
 
+// s_waitcnt through the builtin (the compiler's own waitcnt pass then knows the counters are
+// satisfied; an asm waitcnt is invisible to it and it re-waits conservatively). gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
+#define SR_WAITCNT(vm, lgkm) \
+  __builtin_amdgcn_s_waitcnt(((vm) & 15) | (7 << 4) | (((lgkm) & 15) << 8) | (((vm) >> 4) << 14))
+
 // Order-preserving float -> uint32 (larger float -> larger uint).
 __device__ __forceinline__ uint32_t ordered_bits(float f) {
   uint32_t u = __float_as_uint(f);
