@@ -233,6 +233,21 @@ def main():
         hit = sum(len(set(rows[i].tolist()) & set(best_r[i].tolist())) for i in range(nq))
         recall = hit / (nq * a.k)
 
+    # ---- fp8 precision modes: final top-10 vs the fp16 reranker on the same candidates -----------
+    fp8_fidelity = None
+    if a.fp8 and world == 1:
+        r8 = pipe.run(*batches[0])
+        reranker.set_fp8(0)
+        r16 = pipe.run(*batches[0])
+        reranker.set_fp8(a.fp8)
+        f8, f16 = r8.rows.cpu(), r16.rows.cpu()
+        overlap = sum(len(set(f8[i].tolist()) & set(f16[i].tolist())) for i in range(f8.shape[0]))
+        l16 = r16.logits.float().cpu()
+        fp8_fidelity = {"top10_overlap_vs_f16": round(overlap / f8.numel(), 4),
+                        "top1_equal_vs_f16": round(float((f8[:, 0] == f16[:, 0]).float().mean()), 4),
+                        "final_logit_std_f16": round(float(l16.std()), 5),
+                        "queries": int(f8.shape[0])}
+
     # ---- roofline of the dominant kernel -------------------------------------------------------
     dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
@@ -299,6 +314,7 @@ def main():
                    "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
                    "parallelism": f"corpus row-shard x{world}, query DP x{world}"},
         "recall_at_10": recall,
+        **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
         "roofline": roof,
         "search_roofline": search_roof,
         "cpu_baseline": cpu,
