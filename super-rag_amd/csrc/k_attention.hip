@@ -182,8 +182,13 @@ __device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
 // LDS image (same swizzle) only before the first P.V MFMA, so V's HBM latency overlaps QK^T +
 // softmax.  (V by LDS-DMA would make the compiler wait vmcnt(0) before every ds_read of K.)  amdgpu_waves_per_eu(3): 168
 // VGPRs, three workgroups per CU (two query tiles per wave stay interleaved for MFMA ILP).
-template <bool SPLIT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attention64_kernel(
+// NW waves per workgroup (32 query rows each): 4, or 8 for S_pad > 256, where the whole-head K/V
+// image (up to 130 KiB at S_pad = 512) allows one workgroup per CU and is then shared by 256
+// queries: half the re-staging and two waves per SIMD (S = 512: 3.25 -> 2.04 ms per 1024 x 12
+// heads; 16 waves at 128 VGPRs spill and ran 2.73 ms).  SPLIT implies NW == 4.
+template <bool SPLIT, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 3, NW == 8 ? 2 : 3)))
+void attention64_kernel(
     const half_t* __restrict__ qkv, const int32_t* __restrict__ mask, half_t* __restrict__ ctx,
     int S, int Sq, int d, float scale_log2) {
   constexpr int DH = 64;
@@ -199,7 +204,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int64_t ld = 3 * (int64_t)d;
   const half_t* base = qkv + (int64_t)b * S * ld + h * DH;
 
-  const int qw = blockIdx.x * A2_QB + wave * 32;  // first query row of this wave
+  static_assert(!SPLIT || NW == 4, "SPLIT stages with four waves");
+  const int qw = blockIdx.x * (32 * NW) + wave * 32;  // first query row of this wave
   const bool active = qw < Sq;
   half8 qf[2][2];
   half8 vreg[4];  // SPLIT: this wave's V pieces (written to the LDS image after the softmax)
@@ -265,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         qf[u][s2] = *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + 8 * (lane >> 4) + 32 * s2);
     }
     // ---- stage K and V (rows >= S replicate row S-1; their keys are masked) ----
-    for (int piece = wave; piece < S_pad / 8; piece += 4) {
+    for (int piece = wave; piece < S_pad / 8; piece += NW) {
       const int r = piece * 8 + (lane >> 3);
       const int rr = r < S ? r : S - 1;
       const half_t* rowp = base + (int64_t)rr * ld;
@@ -274,7 +280,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       __builtin_amdgcn_global_load_lds((const void*)(rowp + 2 * d + a2_vswz(r, lane & 7) * 8),
                                        SR_LDS(Vs + piece * 8 * DH), 16, 0, 0);
     }
-    for (int r = tid; r < S_pad; r += 256)
+    for (int r = tid; r < S_pad; r += 64 * NW)
       kbias[r] = (r < S && mask[(int64_t)b * S + r] != 0) ? 0.f : -INFINITY;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
 }  // namespace
 
-static int g_attn_variant = -1;  // test hook: -1 auto, 0 = K5 (64-key tiles), 1 = K5b
+static int g_attn_variant = -1;  // test hook: -1 auto, 0 = K5 (64-key tiles), 1 = K5b (4 waves), 2 = K5b with 8 waves
 void attention_force_variant(int v) { g_attn_variant = v; }
 
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
@@ -425,14 +431,21 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
   if (use_b) {
     const int S_pad = (S + 31) & ~31;
     const bool split = S_pad == 128 && Sq > 96;  // K5b SPLIT: one key block, all waves active
-    const size_t shmem = (size_t)(split ? 3 : 2) * S_pad * 64 * sizeof(half_t) + (size_t)S_pad * sizeof(float);
-    dim3 grid((unsigned)ceil_div(Sq, A2_QB), heads, B), block(256);
-    if (split)
-      hipLaunchKernelGGL(attention64_kernel<true>, grid, block, shmem, stream, qkv, mask, ctx, S, Sq,
-                         d, scale_log2);
+    // long sequences: 8 waves (256 queries) per workgroup share one K/V image (auto: S_pad > 256)
+    const int nw = (g_attn_variant == 2 || (g_attn_variant < 0 && S_pad > 256)) ? 8 : 4;
+    // SPLIT also stages the workgroup's 128 Q rows (a third S_pad x 64 image)
+    const size_t shmem = (size_t)(split && nw == 4 ? 3 : 2) * S_pad * 64 * sizeof(half_t) +
+                         (size_t)S_pad * sizeof(float);
+    dim3 grid((unsigned)ceil_div(Sq, 32 * nw), heads, B), block(64 * nw);
+    if (split && nw == 4)
+      hipLaunchKernelGGL((attention64_kernel<true, 4>), grid, block, shmem, stream, qkv, mask, ctx, S,
+                         Sq, d, scale_log2);
+    else if (nw == 8)
+      hipLaunchKernelGGL((attention64_kernel<false, 8>), grid, block, shmem, stream, qkv, mask, ctx, S,
+                         Sq, d, scale_log2);
     else
-      hipLaunchKernelGGL(attention64_kernel<false>, grid, block, shmem, stream, qkv, mask, ctx, S, Sq,
-                         d, scale_log2);
+      hipLaunchKernelGGL((attention64_kernel<false, 4>), grid, block, shmem, stream, qkv, mask, ctx, S,
+                         Sq, d, scale_log2);
   } else {
     const int nw = (int)std::min<int64_t>(4, ceil_div(Sq, 16));
     dim3 grid((unsigned)ceil_div(Sq, 16 * nw), heads, B), block(64 * nw);

@@ -89,7 +89,7 @@ void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* l
 // sequence; ctx rows are laid out [B][Sq][d].
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
                       int d, int heads, hipStream_t stream);
-void attention_force_variant(int v);  // test hook: -1 auto, 0 = 64-key-tile kernel, 1 = K5b
+void attention_force_variant(int v);  // test hook: -1 auto, 0 = 64-key-tile kernel, 1 = K5b, 2 = K5b with 8 waves
 
 // k_encoder_misc.hip
 void launch_positions(const int32_t* ids, int32_t* pos, int B, int S, int offset, hipStream_t s);

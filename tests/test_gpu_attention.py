@@ -35,7 +35,7 @@ def _run(variant, B, S, Sq, heads, dh=64, seed=0, lens=None):
     return (ctx.float() - ref).abs().max().item()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("S,Sq", [(128, 128), (128, 1), (32, 32), (100, 100), (7, 7), (200, 200),
                                   (512, 512), (300, 1), (130, 130),
                                   # K5b SPLIT boundaries (S_pad == 128 and Sq > 96): first / last
@@ -50,6 +50,6 @@ def test_attention_vs_torch(variant, S, Sq):
 def test_attention_single_key_rows():
     import torch
     lens = torch.tensor([1, 1, 2, 128], device="cuda")
-    for variant in (0, 1):
+    for variant in (0, 1, 2):
         err = _run(variant, 4, 128, 128, heads=2, seed=3, lens=lens)
         assert err <= 4e-3, f"variant {variant}: max|err| {err:.3e}"

@@ -30,9 +30,9 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     byt = 2.0 * a.B * a.S * 3 * d + 2.0 * a.B * a.Sq * d
     fl = 4.0 * a.B * a.heads * a.Sq * a.S * 64
-    res = {0: [], 1: []}
+    res = {0: [], 1: [], 2: [], -1: []}
     for _ in range(3):
-        for v in (0, 1):
+        for v in (0, 1, 2, -1):
             N.call("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B, a.S,
                    a.Sq, d, a.heads, 0, st)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
