@@ -295,6 +295,10 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, int device,
                  void* stream);
 
+/* Diagnostic: device-to-device copy of `bytes` (multiple of 16) with 16-byte lanes, the HBM
+ * yardstick bench.py reports beside the spec peak (no reference counterpart). */
+int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream);
+
 /* Diagnostic: one attention launch (K5) on device pointers.  qkv: [B*S, 3d] fp16 (Q | K | V),
  * mask: [B, S] int32 (0 = padding key), ctx: [B*Sq, d] fp16 (first Sq query rows of every
  * sequence).  variant: -1 auto, 0 the 64-key-tile kernel, 1 the whole-head-in-LDS kernel with 4

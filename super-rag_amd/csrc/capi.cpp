@@ -667,6 +667,16 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
   SR_API_END
 }
 
+int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(src);
+  SR_NONNULL(dst);
+  SR_CHECK(bytes >= 0 && bytes % 16 == 0, "diag_copy: bytes must be a non-negative multiple of 16");
+  sr::DeviceGuard g(device);
+  sr::launch_copy16(src, dst, bytes, reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
 int sr_diag_attention(int variant, const void* qkv, const int32_t* mask, void* ctx, int B, int S,
                       int Sq, int d, int heads, int device, void* stream) {
   SR_API_BEGIN

@@ -447,6 +447,24 @@ void launch_scale_f16(const half_t* in, float scale, half_t* out, int64_t n, hip
   SR_LAUNCH_CHECK();
 }
 
+// Diagnostic HBM copy (measured-peak yardstick for bench.py): one 16-byte element per lane, one
+// pass (no grid-stride loop), the plain "float4 copy" form.
+__global__ __launch_bounds__(256) void copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                     int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+void launch_copy16(const void* src, void* dst, int64_t bytes, hipStream_t s) {
+  SR_CHECK(bytes % 16 == 0, "copy16: bytes must be a multiple of 16");
+  if (bytes <= 0) return;
+  const int64_t n = bytes / 16;
+  SR_CHECK(ceil_div(n, 256) < (1ll << 31), "copy16: too large");
+  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n);
+  SR_LAUNCH_CHECK();
+}
+
 void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(vec_add_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, a, b, out, n);

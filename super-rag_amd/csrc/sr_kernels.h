@@ -135,6 +135,7 @@ void launch_topk_select(uint64_t* cand, int* cnt, int cap, float* tau, int B, in
 void launch_topk_merge(const float* sims, const int64_t* rows, int P, int B, int k, int k_out,
                        float* out_sim, int64_t* out_rows, hipStream_t s);
 void launch_fill_int(int* p, int n, int v, hipStream_t s);
+void launch_copy16(const void* src, void* dst, int64_t bytes, hipStream_t s);  // diagnostic
 void launch_fill_float(float* p, int n, float v, hipStream_t s);
 void launch_build_pairs(const int32_t* q_tok, const int32_t* q_len, int lq_max,
                         const int32_t* p_tok, const int32_t* p_len, int lp_max,

@@ -124,6 +124,7 @@ SIGNATURES = {
                              c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
     "sr_diag_attention": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_void_p]),
+    "sr_diag_copy": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
 }
 
 _lib = None
