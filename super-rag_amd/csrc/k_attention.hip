@@ -176,6 +176,28 @@ __device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
   return __builtin_bit_cast(half4, v);
 }
 
+// The transposed V reads of one 32-key chunk (4 d-tiles x lo / hi rows) as ONE inline-asm block that
+// ends with its own lgkmcnt(0): the compiler cannot see them as LDS accesses, so it does not wait
+// for every in-flight LDS-DMA piece before them (it does before the builtin), and no use of the
+// results can be scheduled before the data has arrived (STREAM).
+__device__ __forceinline__ void tr_read_chunk_asm(const uint32_t (&addr)[8], uint2 (&v)[8]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %9\n\t"
+      "ds_read_b64_tr_b16 %2, %10\n\tds_read_b64_tr_b16 %3, %11\n\t"
+      "ds_read_b64_tr_b16 %4, %12\n\tds_read_b64_tr_b16 %5, %13\n\t"
+      "ds_read_b64_tr_b16 %6, %14\n\tds_read_b64_tr_b16 %7, %15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+        "=&v"(v[7])
+      : "v"(addr[0]), "v"(addr[1]), "v"(addr[2]), "v"(addr[3]), "v"(addr[4]), "v"(addr[5]),
+        "v"(addr[6]), "v"(addr[7])
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const half_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // SPLIT (S_pad == 128, all four waves active): the Q fragments and the key mask are requested
 // first, then K (LDS-DMA), then V into registers; the score / softmax phase starts once Q and K
 // have landed (vmcnt(4): each wave's four V loads may still be in flight) and V is written to its
@@ -186,14 +208,19 @@ __device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
 // image (up to 130 KiB at S_pad = 512) allows one workgroup per CU and is then shared by 256
 // queries: half the re-staging and two waves per SIMD (S = 512: 3.25 -> 2.04 ms per 1024 x 12
 // heads; 16 waves at 128 VGPRs spill and ran 2.73 ms).  SPLIT implies NW == 4.
-template <bool SPLIT, int NW>
+// STREAM (NW == 8, S_pad == 512, every wave active): K/V pieces are issued in key-block order and
+// each 128-key block is awaited only before it is used (counted vmcnt + barrier), so blocks 1..3
+// land while block 0.. are being processed; Q and the mask word are loaded right after block 0
+// and waited for with it (no plain load is outstanding afterwards, so the counted waits stay exact).
+template <bool SPLIT, int NW, bool STREAM = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 3, NW == 8 ? 2 : 3)))
 void attention64_kernel(
     const half_t* __restrict__ qkv, const int32_t* __restrict__ mask, half_t* __restrict__ ctx,
     int S, int Sq, int d, float scale_log2) {
   constexpr int DH = 64;
   extern __shared__ __attribute__((aligned(16))) char a2_smem[];
-  const int S_pad = SPLIT ? 128 : (S + 31) & ~31;
+  static_assert(!STREAM || (NW == 8 && !SPLIT), "STREAM runs the 8-wave non-split form");
+  const int S_pad = SPLIT ? 128 : STREAM ? 512 : (S + 31) & ~31;
   half_t* Ks = reinterpret_cast<half_t*>(a2_smem);
   half_t* Vs = Ks + S_pad * DH;
   float* kbias = reinterpret_cast<float*>(Vs + S_pad * DH);
@@ -260,6 +287,42 @@ void attention64_kernel(
     }
     SR_WAITCNT(4, 0);
     __builtin_amdgcn_s_barrier();
+  } else if constexpr (STREAM) {
+    auto stage_blk = [&](int blk) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int piece = blk * 16 + wave + 8 * i;
+        const int r = piece * 8 + (lane >> 3);
+        __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(r < S ? r : S - 1) * ld + d +
+                                                       a2_kswz(r, lane & 7) * 8),
+                                         SR_LDS(Ks + piece * 8 * DH), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int piece = blk * 16 + wave + 8 * i;
+        const int r = piece * 8 + (lane >> 3);
+        __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(r < S ? r : S - 1) * ld + 2 * d +
+                                                       a2_vswz(r, lane & 7) * 8),
+                                         SR_LDS(Vs + piece * 8 * DH), 16, 0, 0);
+      }
+    };
+    stage_blk(0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int qr = qw + 16 * u + (lane & 15);
+      qr = qr < S ? qr : S - 1;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        qf[u][s2] = *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + 8 * (lane >> 4) + 32 * s2);
+    }
+    const int32_t mk = mask[(int64_t)b * S + (tid < S ? tid : S - 1)];
+    SR_WAITCNT(0, 15);  // block 0, Q and the mask word
+    stage_blk(1);
+    stage_blk(2);
+    stage_blk(3);
+    kbias[tid] = (tid < S && mk != 0) ? 0.f : -INFINITY;  // 512 threads = S_pad keys
+    SR_WAITCNT(12, 0);
+    __builtin_amdgcn_s_barrier();
   } else {
     // ---- Q fragments (B operand of S^T): lane holds Q[q][8 (lane>>4) + 32 s .. +7] ----
 #pragma unroll
@@ -285,7 +348,7 @@ void attention64_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (!SPLIT && !active) return;  // no barrier follows
+  if (!SPLIT && !STREAM && !active) return;  // no barrier follows
 
   const int g = lane >> 4;
   float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
@@ -296,6 +359,14 @@ void attention64_kernel(
     for (int t = 0; t < 4; ++t) o[u][t] = float4v{0.f, 0.f, 0.f, 0.f};
 
   for (int k0 = 0; k0 < S_pad; k0 += 128) {
+    if constexpr (STREAM) {  // key block k0 / 128 (this wave's later blocks may still be in flight)
+      if (k0 > 0) {
+        if (k0 == 128) SR_WAITCNT(8, 15);
+        else if (k0 == 256) SR_WAITCNT(4, 15);
+        else SR_WAITCNT(0, 15);
+        __builtin_amdgcn_s_barrier();
+      }
+    }
     const int nkt = (S_pad - k0) >= 128 ? 8 : (S_pad - k0) / 16;  // 16-key tiles in this block
     float p[2][8][4];
     float tmax[2] = {-INFINITY, -INFINITY};
@@ -366,6 +437,27 @@ void attention64_kernel(
           }
         // lane 4q+p of group g: V row k0 + 32c + 16hh + 4g + q, dims 16t + 4p .. +3
         const int q = (lane >> 2) & 3, pp = lane & 3;
+        if constexpr (STREAM) {
+          uint32_t addr[8];
+          uint2 vv[8];
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const int r = k0 + 32 * c + 16 * hh + 4 * g + q;
+              addr[2 * t + hh] = lds_addr(Vs + r * DH + a2_vswz(r, 2 * t + (pp >> 1)) * 8 + 4 * (pp & 1));
+            }
+          tr_read_chunk_asm(addr, vv);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const half4 lo = __builtin_bit_cast(half4, vv[2 * t]), hi = __builtin_bit_cast(half4, vv[2 * t + 1]);
+            const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              o[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[u], o[u][t], 0, 0, 0);
+          }
+          continue;
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           half4 lo, hi;
@@ -440,6 +532,9 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
     if (split && nw == 4)
       hipLaunchKernelGGL((attention64_kernel<true, 4>), grid, block, shmem, stream, qkv, mask, ctx, S,
                          Sq, d, scale_log2);
+    else if (nw == 8 && S_pad == 512 && Sq > 480 && g_attn_variant != 2)  // every wave active
+      hipLaunchKernelGGL((attention64_kernel<false, 8, true>), grid, block, shmem, stream, qkv, mask, ctx,
+                         S, Sq, d, scale_log2);
     else if (nw == 8)
       hipLaunchKernelGGL((attention64_kernel<false, 8>), grid, block, shmem, stream, qkv, mask, ctx, S,
                          Sq, d, scale_log2);

@@ -3,7 +3,8 @@ a torch fp32 reference: ctx = softmax(Q K^T / sqrt(d_h) + key-padding mask) V pe
 first Sq query rows of each sequence.
 
 Covers both kernels (64-key tiles; whole head in LDS with transposed V reads, and its SPLIT
-staging at S_pad = 128), ragged masks,
+staging at S_pad = 128, the 8-wave form and its key-block STREAM staging at S_pad = 512; variant
+-1 = the automatic choice), ragged masks,
 S not a multiple of 16 / 32, S > 128 (online softmax across 128-key blocks), Sq = 1 (the CLS-only
 last layer), fully masked rows except the first key.  Tolerance: |ctx - ref| <= 4e-3 (fp16 P and
 output, fp32 statistics; |ref| <= max|V| ~ 1).
@@ -35,13 +36,15 @@ def _run(variant, B, S, Sq, heads, dh=64, seed=0, lens=None):
     return (ctx.float() - ref).abs().max().item()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, -1])
 @pytest.mark.parametrize("S,Sq", [(128, 128), (128, 1), (32, 32), (100, 100), (7, 7), (200, 200),
                                   (512, 512), (300, 1), (130, 130),
                                   # K5b SPLIT boundaries (S_pad == 128 and Sq > 96): first / last
                                   # S of the split range, the last query tile partly stored, and
                                   # Sq = 96 (non-split: wave 3 idle)
-                                  (97, 97), (128, 97), (128, 96), (120, 110)])
+                                  (97, 97), (128, 97), (128, 96), (120, 110),
+                                  # K5b STREAM (auto, 8 waves, S_pad = 512, Sq > 480)
+                                  (500, 500), (512, 481), (512, 480)])
 def test_attention_vs_torch(variant, S, Sq):
     err = _run(variant, 6, S, Sq, heads=3, seed=S * 7 + Sq)
     assert err <= 4e-3, f"variant {variant} S={S} Sq={Sq}: max|err| {err:.3e}"
@@ -50,6 +53,6 @@ def test_attention_vs_torch(variant, S, Sq):
 def test_attention_single_key_rows():
     import torch
     lens = torch.tensor([1, 1, 2, 128], device="cuda")
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, -1):
         err = _run(variant, 4, 128, 128, heads=2, seed=3, lens=lens)
         assert err <= 4e-3, f"variant {variant}: max|err| {err:.3e}"
