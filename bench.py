@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--embed-model", default="bge-base-en")
     ap.add_argument("--rerank-model", default="bge-reranker-base")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rerank-max-tokens", type=int, default=524288,
+                    help="cross-encoder tokens per chunk (workspace ~15 KB per token)")
     ap.add_argument("--cpu-queries", type=int, default=2)
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
@@ -138,7 +140,7 @@ def main():
     w_embed = random_weights(es, seed=11, style="hf")
     w_rerank = random_weights(rs, seed=12, style="hf")
     embedder = Encoder(es, device=local, weights=w_embed, max_tokens=a.batch * a.q_len)
-    reranker = Encoder(rs, device=local, weights=w_rerank, max_tokens=524288)
+    reranker = Encoder(rs, device=local, weights=w_rerank, max_tokens=a.rerank_max_tokens)
     if a.fp8_ffn:
         a.fp8 = max(a.fp8, 1)
     if a.fp8:
