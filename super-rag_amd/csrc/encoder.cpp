@@ -323,6 +323,18 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
           lq.wexp = L.wqkve.as<uint8_t>();
           launch_gemm_f8w(EPI_LNF_F16, u8, d, L.wqkv8.as<uint8_t>(), L.dqkv.as<float>(), nullptr, 0,
                           qkv, 3 * d, M, 3 * d, d, s, &lq);
+        } else if (last && d % 256 == 0) {  // CLS-only last layer: K, V for all rows, Q for CLS rows
+          LnFold lq;
+          lq.mr = mB;
+          lq.colsum = L.cqkv.as<float>() + d;
+          launch_gemm(EPI_LNF_F16, U, d, L.wqkv_f.as<half_t>() + (int64_t)d * d, L.dqkv.as<float>() + d,
+                      nullptr, 0, qkv + d, 3 * d, M, 2 * d, d, s, &lq);
+          LnFold lc;  // A = row b*S of each sequence (stride S*d), its statistics at row b*S
+          lc.mr = mB;
+          lc.stat_ld = S;
+          lc.colsum = L.cqkv.as<float>();
+          launch_gemm(EPI_LNF_F16, U, (int64_t)S * d, L.wqkv_f.as<half_t>(), L.dqkv.as<float>(), nullptr,
+                      0, qkv, (int64_t)S * 3 * d, nb, d, d, s, &lc);
         } else {  // A = u of the previous block, its LN2 folded into W'
           LnFold lq;
           lq.mr = mB;
