@@ -347,7 +347,8 @@ void launch_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* type
                      int max_pos, int type_vocab, half_t* h16, float* h32, hipStream_t s) {
   SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "embed_ln: hidden must be a multiple of 4, <= 2048");
   if (M <= 0) return;
-  ProfScope prof("embed_ln", s, 0.0, (double)M * d * (3 * 2 + 2 + 4));
+  // word + position + type rows in (fp16), h16 out, + h32 out for fp32-residual models
+  ProfScope prof("embed_ln", s, 0.0, (double)M * d * (3 * 2 + 2 + (h32 ? 4 : 0)));
   hipLaunchKernelGGL(embed_ln_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, ids, pos,
                      types, wemb, pemb, temb, gamma, beta, eps, M, d, vocab, max_pos, type_vocab,
                      h16, h32);
