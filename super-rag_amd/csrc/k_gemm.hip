@@ -510,7 +510,20 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     }
   }
   if (t >= t_end || t_step <= 0) return;
-  int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  // tile walk: n fastest, or groups of lf.group_m m-panels with m fastest inside a group (a window
+  // of concurrent tiles then shares fewer W column tiles in the XCD's L2)
+  const int gm = lf.group_m, tiles_m = (M + BM - 1) / BM;
+  auto tile_m = [&](int tt) __attribute__((always_inline)) {
+    if (gm <= 1) return tt / tiles_n;
+    const int first = (tt / (gm * tiles_n)) * gm, gsz = min(gm, tiles_m - first);
+    return first + (tt - first * tiles_n) % gsz;
+  };
+  auto tile_n = [&](int tt) __attribute__((always_inline)) {
+    if (gm <= 1) return tt % tiles_n;
+    const int first = (tt / (gm * tiles_n)) * gm, gsz = min(gm, tiles_m - first);
+    return (tt - first * tiles_n) / gsz;
+  };
+  int m0 = tile_m(t) * BM, n0 = tile_n(t) * BN;
 
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -746,7 +759,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 
     const int t_next = t + t_step;
     const bool more = PERSIST && t_next < t_end && nk > 1;
-    const int m0n = (t_next / tiles_n) * BM, n0n = (t_next % tiles_n) * BN;
+    const int m0n = tile_m(t_next) * BM, n0n = tile_n(t_next) * BN;
     int kt = 0;
     bool lenient = stores_pending;
     for (; kt + 2 < nk; ++kt) {
@@ -1357,7 +1370,12 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
   SR_CHECK(epi < EPI_LNF_GELU_F8 || v == GEMM_PIPE || v == GEMM_PIPE_PERSIST,
            "gemm: the e4m3-output epilogues run on the pipelined kernels");
-  const LnFold lfv = lf ? *lf : LnFold{};
+  LnFold lfv = lf ? *lf : LnFold{};
+  // Short-K GEMMs (K <= 1024: QKV, FFN1, O-proj) walk groups of 8 (N >= 2048) or 4 m-panels;
+  // FFN2 (K = 3072) stays n fastest.  Same-box A/B of the full bench: 422.8 / 424.0 -> 429.8 /
+  // 431.0 q/s (profiles/r01_gemm_group_m.log).  SR_GEMM_GROUP_M overrides (diagnostic).
+  lfv.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;
+  if (const char* e = std::getenv("SR_GEMM_GROUP_M")) lfv.group_m = std::atoi(e);
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
                                        ldr, Y, ldy, M, N, K);

@@ -46,6 +46,8 @@ struct LnFold {
   const uint8_t* wexp = nullptr;   // fp8 operands (launch_gemm_f8w): E8M0 exponent per weight row
   uint8_t* y8 = nullptr;           // *_STATS: optional e4m3 copy of the fp16 output (row stride
                                    //          ldy bytes), the next fp8 GEMM's A operand
+  int group_m = 0;                 // pipelined kernels: tile t walks groups of group_m m-panels
+                                   // (m fastest inside a group); 0 / 1 = n fastest
   // EPI_SCAN(8) re-uses the fields (kernel-argument SGPRs are scarce in the persistent kernels):
   // stat_out = per-query candidate counts (int*), stat_ld = global row id of the chunk's first
   // row; bias = tau[B], R = live flags of the chunk, Y = candidate keys [B][cap] (ldy = cap).
