@@ -7,14 +7,18 @@ recall@10".  One step = one batch of B synthetic queries per rank through the wh
   100 candidates per query at S_pair=128  ->  top-10.
 Weights are seeded random (no checkpoints offline), inputs synthetic.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
-(one rank per GPU, RCCL).  Rank 0 prints one JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W].  Under torch.distributed.run (WORLD_SIZE
+set) every process is one rank on one GPU (RCCL); run directly with --gpus N > 1 the script
+starts the N ranks itself through torch.distributed.run before anything touches the GPU, waits for
+them and exits with the first non-zero rank status.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,7 +37,8 @@ PEAK_F8_TFLOPS = 5000.0     # dense fp8 MFMA spec (no sparsity)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE the script launches them itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--corpus-rows", type=int, default=10_000_000)
@@ -49,8 +54,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rerank-max-tokens", type=int, default=524288,
                     help="cross-encoder tokens per chunk (workspace ~15 KB per token)")
-    ap.add_argument("--cpu-queries", type=int, default=2)
-    ap.add_argument("--cpu-rows", type=int, default=200_000)
+    ap.add_argument("--cpu-queries", type=int, default=32,
+                    help="cpu_baseline: queries embedded and reranked (100 pairs each) on the host")
+    ap.add_argument("--cpu-search-rows", type=int, default=0,
+                    help="cpu_baseline: corpus rows scanned by the host search (0 = the whole corpus)")
     ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
     ap.add_argument("--workload", default="config4", choices=["config4", "config5"],
                     help="config4 (default, the BASELINE metric) or config5: bge-m3 embed, 6.25M x "
@@ -113,11 +120,32 @@ def gen_corpus_chunk(r0, r1, dim, centers, dev):
     return out
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, script: str | None = None, env=None) -> int:
+    """Start n ranks of `script` (default: this file) with torch.distributed.run on 127.0.0.1 and
+    wait for them.  Called before any GPU call in this process (the parent never initialises HIP;
+    the ranks are child processes, not an exec).  Returns 0 or the first failing rank's status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           script or os.path.abspath(__file__), *argv]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus is not None and a.gpus != world:
+        sys.exit(f"bench: --gpus {a.gpus} but the launcher started {world} rank(s)")
     if a.dist_backend == "gloo":  # rehearsal mode: ranks may share the visible GPUs
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -128,6 +156,12 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        ver = torch.cuda.nccl.version() if a.dist_backend != "gloo" else None
+        print(f"[bench] rank {rank}/{world}: backend {dist.get_backend()} reports world_size "
+              f"{dist.get_world_size()}" + (f", RCCL {ver}" if ver else "") + f", device {dev}",
+              file=sys.stderr, flush=True)
+        if dist.get_world_size() != world:
+            sys.exit(f"bench: backend world_size {dist.get_world_size()} != WORLD_SIZE {world}")
 
     from super_rag_amd import _native as N
     from super_rag_amd.encoder import MODELS, Encoder, random_weights
@@ -295,7 +329,8 @@ def main():
     # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) ----------------------------
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a, es, rs, w_embed, w_rerank, centers.cpu(), batches[0], p_tok, N_total)
+        cpu = cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batches[0], p_tok, N_total,
+                           embedder, dev)
 
     workload = ("config4: bge-base-en embed (S=32) + exact cosine top-100 over "
                 f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
@@ -403,45 +438,107 @@ def pmc_traffic(kernel):
                             f"{k['write_B']} B per launch (mean over {k['launches']} launches)")
 
 
-def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total):
-    """Oracle (oracle/*, the CPU restatement) timed on host cores on a bounded sample."""
+def cpu_cores() -> int:
+    """CPUs this process may use: its affinity set, capped by the cgroup CPU quota (the GPU box
+    grants 16 CPUs per GPU: cpu.max = 1600000 100000 while os.cpu_count() shows the machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return "unknown"
+
+
+def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total, embedder, dev):
+    """The oracle (oracle/*, the CPU restatement) timed on the host cores,
+    stage by stage, with no extrapolation:
+      embed   a.cpu_queries queries (S = q_len) through the fp32 torch-CPU encoder;
+      search  the full batch of queries (this rank's B) against the whole corpus as a batched
+              fp32 torch matmul + topk, streamed in 1M-row chunks (each chunk is generated and
+              L2-normalised on the GPU and copied to pinned host memory outside the timed part);
+      rerank  a.cpu_queries queries x k_cand (query, passage) pairs at S_pair through the fp32
+              cross-encoder, one query's pairs per call.
+    End-to-end q/s = 1 / (embed + search + rerank seconds per query)."""
     from oracle import encoder_ref as R
-    from oracle.cosine_topk import cosine_topk
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_cores()
     torch.set_num_threads(threads)
-    nq = a.cpu_queries
     cfg = lambda s: R.RefConfig(s.vocab_size, s.hidden, s.layers, s.heads, s.intermediate,
                                 s.max_position, s.type_vocab, s.ln_eps, s.position_offset,
                                 s.classifier, s.num_labels)
-    ids, mask, qtok, qlen = (t[:nq].cpu().numpy() for t in batch)
+    log = lambda m: print(f"[cpu_baseline] {m}", file=sys.stderr, flush=True)
+    nq = min(a.cpu_queries, a.batch)
+    ids, mask, qtok, qlen = batch
     wt_e = {k: torch.from_numpy(v) for k, v in w_embed.items()}
     wt_r = {k: torch.from_numpy(v) for k, v in w_rerank.items()}
+    # ---- (i) embed -----------------------------------------------------------------------------
+    ids_h, mask_h = ids[:nq].cpu().numpy(), mask[:nq].cpu().numpy()
     t0 = time.perf_counter()
-    q = R.embed(cfg(es), wt_e, ids, mask)
+    R.embed(cfg(es), wt_e, ids_h, mask_h)
     t_embed = time.perf_counter() - t0
-    g = torch.Generator().manual_seed(1)
-    rows = a.cpu_rows
-    x = (centers[torch.arange(rows) % centers.shape[0]]
-         + 0.5 * torch.randn((rows, a.dim), generator=g)).numpy()
-    t0 = time.perf_counter()
-    _, cand = cosine_topk(x, q, a.k_cand)
-    t_search = (time.perf_counter() - t0) * (N_total / rows)
-    pt = p_tok[torch.from_numpy(np.clip(cand, 0, None).reshape(-1)).to(p_tok.device)].view(nq, a.k_cand, -1).cpu().numpy()
-    pids, pmask, _ = R.pack_pairs(qtok, qlen, pt.reshape(nq * a.k_cand, -1),
-                                  np.full(nq * a.k_cand, pt.shape[-1]),
+    log(f"embed {nq} queries: {t_embed:.2f} s ({threads} threads)")
+    # ---- (ii) exact fp32 cosine top-k over the whole corpus, batched ---------------------------
+    q = embedder.embed_dev(ids, mask, fp16=False).cpu()      # [B, d] unit queries (inputs)
+    rows_total = a.cpu_search_rows or N_total
+    step = 1 << 20
+    host = torch.empty((step, a.dim), dtype=torch.float32).pin_memory()
+    best_s = torch.full((q.shape[0], 0), -2.0)
+    best_r = torch.zeros((q.shape[0], 0), dtype=torch.int64)
+    t_search = 0.0
+    for c0 in range(0, rows_total, step):
+        c1 = min(rows_total, c0 + step)
+        x = torch.nn.functional.normalize(gen_corpus_chunk(c0, c1, a.dim, centers, dev), dim=1)
+        host[: c1 - c0].copy_(x)
+        del x
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s = q @ host[: c1 - c0].T
+        v, i = s.topk(a.k_cand, dim=1)
+        best_s = torch.cat([best_s, v], 1)
+        best_r = torch.cat([best_r, i + c0], 1)
+        top = best_s.topk(a.k_cand, dim=1)
+        best_s, best_r = top.values, best_r.gather(1, top.indices)
+        t_search += time.perf_counter() - t0
+    del host
+    log(f"search {q.shape[0]} queries x {rows_total} rows: {t_search:.2f} s")
+    # ---- (iii) cross-encoder rerank of k_cand pairs per query -----------------------------------
+    cand = best_r[:nq]
+    pt = p_tok[cand.reshape(-1).to(p_tok.device)].view(nq, a.k_cand, -1).cpu().numpy()
+    pids, pmask, _ = R.pack_pairs(qtok[:nq].cpu().numpy(), qlen[:nq].cpu().numpy(),
+                                  pt.reshape(nq * a.k_cand, -1), np.full(nq * a.k_cand, pt.shape[-1]),
                                   np.arange(nq * a.k_cand).reshape(nq, a.k_cand), a.pair_len, 0,
                                   rs.bos_id, rs.eos_id, rs.pad_id)
-    t0 = time.perf_counter()
-    R.cross_logits(cfg(rs), wt_r, pids, pmask)
-    t_rerank = time.perf_counter() - t0
-    per_q = (t_embed + t_search + t_rerank) / nq
-    return {"value": round(1.0 / per_q, 4), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": (f"{nq} queries end-to-end through the oracle (torch-CPU fp32 encoders, "
-                       f"numpy fp64 exact cosine top-{a.k_cand}); search timed over {rows} rows and "
-                       f"scaled x{N_total / rows:.0f} to {N_total} rows"),
-            "stage_s_per_query": {"embed": round(t_embed / nq, 4),
-                                  "search_10M": round(t_search / nq, 3),
-                                  "rerank": round(t_rerank / nq, 3)}}
+    t_rerank = 0.0
+    for i in range(nq):
+        sl = slice(i * a.k_cand, (i + 1) * a.k_cand)
+        t0 = time.perf_counter()
+        R.cross_logits(cfg(rs), wt_r, pids[sl], pmask[sl])
+        t_rerank += time.perf_counter() - t0
+        if i % 4 == 3 or i == nq - 1:
+            log(f"rerank {i + 1}/{nq} queries: {t_rerank:.1f} s")
+    per_q = {"embed": t_embed / nq, "search": t_search / q.shape[0], "rerank": t_rerank / nq}
+    total = sum(per_q.values())
+    return {"value": round(1.0 / total, 4), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle (torch-CPU fp32) on {threads} threads, no extrapolation: embed "
+                       f"{nq} queries (S={a.q_len}); exact cosine top-{a.k_cand} of {q.shape[0]} "
+                       f"queries over all {rows_total} x {a.dim} rows as a batched fp32 matmul + "
+                       f"topk in 1M-row chunks; rerank {nq} queries x {a.k_cand} pairs "
+                       f"(S={a.pair_len}); end to end = 1 / sum of per-query stage times"),
+            "cpu_model": cpu_model(), "machine_cpus": os.cpu_count(),
+            "stage_s_per_query": {k: round(v, 5) for k, v in per_q.items()},
+            "stage_qps": {k: round(1.0 / v, 3) for k, v in per_q.items()},
+            "stage_s_total": {"embed": round(t_embed, 3), "search": round(t_search, 3),
+                              "rerank": round(t_rerank, 3)}}
 
 
 if __name__ == "__main__":

@@ -413,13 +413,15 @@ void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* 
 }
 
 // Snapshot format (little endian): "SRMISTO1", int32 dim, int64 n_rows, n_rows x dim fp16
-// (normalised rows, unpadded), n_rows bytes of live flags.
+// (normalised rows, unpadded), n_rows bytes of live flags.  Written to "<path>.tmp" and renamed
+// over <path>, so a crash mid-save leaves the previous snapshot intact.
 void Store::save(const char* path) {
   DeviceGuard g(device_);
   begin(stream_);
   SR_HIP(hipStreamSynchronize(stream_));
-  std::ofstream f(path, std::ios::binary);
-  if (!f) throw Error(SR_ERR_IO, std::string("store.save: cannot open ") + path);
+  const std::string tmp = std::string(path) + ".tmp";
+  std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+  if (!f) throw Error(SR_ERR_IO, std::string("store.save: cannot open ") + tmp);
   f.write("SRMISTO1", 8);
   const int32_t d = dim_;
   f.write(reinterpret_cast<const char*>(&d), 4);
@@ -435,7 +437,11 @@ void Store::save(const char* path) {
     f.write(reinterpret_cast<const char*>(buf.data()), (std::streamsize)(buf.size() * sizeof(half_t)));
   }
   f.write(reinterpret_cast<const char*>(live_host_.data()), (std::streamsize)n_rows_);
-  if (!f) throw Error(SR_ERR_IO, std::string("store.save: write failed for ") + path);
+  f.flush();
+  if (!f) throw Error(SR_ERR_IO, std::string("store.save: write failed for ") + tmp);
+  f.close();
+  if (std::rename(tmp.c_str(), path) != 0)
+    throw Error(SR_ERR_IO, std::string("store.save: cannot rename ") + tmp + " to " + path);
 }
 
 Store* Store::load(const char* path, int device) {

@@ -138,9 +138,14 @@ def get_collection_embedding_service_sync(collection, device: Optional[int] = No
     model = emb.get("model")
     if not model:
         raise InvalidConfigurationError("embedding.model", model, "Model name cannot be empty")
+    provider = emb.get("custom_llm_provider") or "mi355x"
     try:
-        svc = EmbeddingService(emb.get("custom_llm_provider") or "mi355x", model, "", "",
-                               emb.get("max_chunks", 10), device=device)
-    except KeyError as e:
-        raise EmbeddingError(f"Failed to create embedding model: {e}", {"model": model}) from e
+        svc = EmbeddingService(provider, model, "", "", emb.get("max_chunks", 10), device=device)
+    except EmbeddingError:
+        raise
+    except Exception as e:  # noqa: BLE001 - unknown model, missing checkpoint / tokenizer, device
+        # base_embedding.py:114-121: every creation failure surfaces as EmbeddingError
+        logger.error("Failed to create embedding model %s/%s: %s", provider, model, e)
+        raise EmbeddingError(f"Failed to create embedding model: {e}",
+                             {"provider": provider, "model": model}) from e
     return svc, svc.dimension

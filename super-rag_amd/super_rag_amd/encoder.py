@@ -2,19 +2,45 @@
 
 Model shapes follow the public model cards of the models the reference calls remotely
 (super_rag/migration/sql/model_configs_init.sql seeds BAAI/bge-m3 for embedding and
-BAAI/bge-reranker-v2-m3 for rerank).  No checkpoints exist offline: weights come from a
-safetensors file when one is provided (``SUPER_RAG_AMD_WEIGHTS`` directory / explicit path),
-otherwise from a seeded random initialisation of identical shape (documented in DESIGN.md).
+BAAI/bge-reranker-v2-m3 for rerank).  Weights come from a Hugging Face model directory
+``$SUPER_RAG_AMD_WEIGHTS/<model>/`` (``model.safetensors``; a ``config.json`` there also defines
+models not in MODELS) or an explicit ``checkpoint=`` path.  A missing checkpoint is an error:
+seeded random weights of identical shape (benchmarks, tests) need the explicit opt-in
+``SUPER_RAG_AMD_SYNTHETIC=1`` or ``weights=random_weights(...)``, so a misconfigured deployment
+cannot serve meaningless embeddings silently.
 """
 from __future__ import annotations
 
 import ctypes
+import json
+import logging
 import os
-from dataclasses import dataclass, field, replace
+from dataclasses import dataclass
 
 import numpy as np
 
 from . import _native as N
+
+logger = logging.getLogger(__name__)
+
+
+class ModelAssetsError(FileNotFoundError):
+    """A model's checkpoint / config / tokenizer is missing or unusable."""
+
+
+def synthetic_allowed() -> bool:
+    """Explicit opt-in for seeded random weights and the hashing tokenizer (tests, benchmarks)."""
+    return os.environ.get("SUPER_RAG_AMD_SYNTHETIC", "") not in ("", "0", "false", "False")
+
+
+def weights_root() -> str | None:
+    return os.environ.get("SUPER_RAG_AMD_WEIGHTS") or None
+
+
+def model_dir(name: str) -> str | None:
+    """$SUPER_RAG_AMD_WEIGHTS/<name> (the org prefix of "BAAI/bge-m3" is dropped), if set."""
+    root = weights_root()
+    return os.path.join(root, name.split("/")[-1]) if root else None
 
 
 @dataclass(frozen=True)
@@ -68,15 +94,78 @@ MODELS = {
 }
 
 
-def resolve_spec(model: str) -> ModelSpec:
-    """Map a reference model name (e.g. "BAAI/bge-m3", "bge-base-en-v1.5") to a ModelSpec."""
+def _key(model: str) -> str:
     key = model.split("/")[-1].lower()
     for suffix in ("-v1.5", "-v1"):
         if key.endswith(suffix):
             key = key[: -len(suffix)]
+    return key
+
+
+def spec_from_dir(path: str, name: str | None = None) -> ModelSpec:
+    """ModelSpec of a Hugging Face BERT / XLM-R model directory: config.json (shapes, head),
+    tokenizer.json (special-token ids), 1_Pooling/config.json (sentence-transformers pooling)."""
+    cfg_path = os.path.join(path, "config.json")
+    try:
+        with open(cfg_path, encoding="utf-8") as f:
+            cfg = json.load(f)
+    except OSError as e:
+        raise ModelAssetsError(f"model config not found: {cfg_path}") from e
+    mt = cfg.get("model_type", "")
+    if mt == "bert":
+        arch = "bert"
+    elif mt in ("xlm-roberta", "roberta"):
+        arch = "xlmr"
+    else:
+        raise ModelAssetsError(f"{cfg_path}: unsupported model_type '{mt}' (bert, xlm-roberta)")
+    if cfg.get("hidden_act", "gelu") != "gelu":
+        raise ModelAssetsError(f"{cfg_path}: unsupported hidden_act '{cfg.get('hidden_act')}'")
+    classifier = int(any("SequenceClassification" in a for a in cfg.get("architectures", [])))
+    num_labels = max(1, len(cfg.get("id2label", {}))) if classifier else 1
+    pool = "cls"
+    pcfg = os.path.join(path, "1_Pooling", "config.json")
+    if os.path.exists(pcfg):
+        with open(pcfg, encoding="utf-8") as f:
+            pc = json.load(f)
+        if pc.get("pooling_mode_mean_tokens") and not pc.get("pooling_mode_cls_token"):
+            pool = "mean"
+    pad = int(cfg.get("pad_token_id", 0 if arch == "bert" else 1))
+    if arch == "bert":
+        bos, eos = 101, 102
+        special = ("[CLS]", "[SEP]", "[PAD]")
+    else:
+        bos, eos = int(cfg.get("bos_token_id", 0)), int(cfg.get("eos_token_id", 2))
+        special = ("<s>", "</s>", "<pad>")
+    tok = os.path.join(path, "tokenizer.json")
+    if os.path.exists(tok):
+        from tokenizers import Tokenizer as HFTokenizer
+        t = HFTokenizer.from_file(tok)
+        ids = [t.token_to_id(s) for s in special]
+        bos, eos = ids[0] if ids[0] is not None else bos, ids[1] if ids[1] is not None else eos
+        pad = ids[2] if ids[2] is not None else pad
+    max_pos = int(cfg["max_position_embeddings"])
+    off = pad if arch == "xlmr" else 0
+    return ModelSpec(name or os.path.basename(os.path.normpath(path)), arch, int(cfg["vocab_size"]),
+                     int(cfg["hidden_size"]), int(cfg["num_hidden_layers"]),
+                     int(cfg["num_attention_heads"]), int(cfg["intermediate_size"]), max_pos,
+                     int(cfg.get("type_vocab_size", 2 if arch == "bert" else 1)),
+                     float(cfg.get("layer_norm_eps", 1e-12 if arch == "bert" else 1e-5)), off,
+                     pool=pool, classifier=classifier, num_labels=num_labels, bos_id=bos,
+                     eos_id=eos, pad_id=pad, max_length=max_pos - off - (1 if off else 0),
+                     residual_fp16=bool(classifier))
+
+
+def resolve_spec(model: str) -> ModelSpec:
+    """Map a reference model name (e.g. "BAAI/bge-m3", "bge-base-en-v1.5") to a ModelSpec: the
+    built-in shapes of MODELS, else the config.json of $SUPER_RAG_AMD_WEIGHTS/<model>."""
+    key = _key(model)
     if key in MODELS:
         return MODELS[key]
-    raise KeyError(f"unknown encoder model '{model}' (known: {sorted(MODELS)})")
+    d = model_dir(model)
+    if d and os.path.exists(os.path.join(d, "config.json")):
+        return spec_from_dir(d, key)
+    raise KeyError(f"unknown encoder model '{model}' (known: {sorted(MODELS)}; or a model "
+                   f"directory with config.json under SUPER_RAG_AMD_WEIGHTS)")
 
 
 def weight_shapes(spec: ModelSpec) -> dict:
@@ -152,18 +241,44 @@ def load_safetensors(path: str) -> dict:
 
 
 def find_checkpoint(spec: ModelSpec) -> str | None:
-    root = os.environ.get("SUPER_RAG_AMD_WEIGHTS")
-    if not root:
+    """$SUPER_RAG_AMD_WEIGHTS/<model>/model.safetensors, or None when the variable is unset.
+    Raises ModelAssetsError when the variable is set but the file is missing (misconfiguration)."""
+    d = model_dir(spec.name)
+    if d is None:
         return None
-    p = os.path.join(root, spec.name, "model.safetensors")
-    return p if os.path.exists(p) else None
+    p = os.path.join(d, "model.safetensors")
+    if not os.path.exists(p):
+        raise ModelAssetsError(f"checkpoint for {spec.name} not found: {p}")
+    return p
+
+
+def model_weights(spec: ModelSpec, checkpoint: str | None = None, seed: int = 0,
+                  init_style: str = "hf") -> dict:
+    """The weights an Encoder loads when none are passed: the explicit or configured
+    checkpoint, else seeded random weights under the explicit synthetic opt-in, else an error."""
+    ckpt = checkpoint or find_checkpoint(spec)
+    if ckpt:
+        if not os.path.exists(ckpt):
+            raise ModelAssetsError(f"checkpoint for {spec.name} not found: {ckpt}")
+        return load_safetensors(ckpt)
+    if synthetic_allowed():
+        logger.warning("%s: no checkpoint, using seeded random weights (SUPER_RAG_AMD_SYNTHETIC)",
+                       spec.name)
+        return random_weights(spec, seed, init_style)
+    raise ModelAssetsError(
+        f"no weights for {spec.name}: set SUPER_RAG_AMD_WEIGHTS to a directory holding "
+        f"{spec.name}/model.safetensors (or pass checkpoint=); seeded random weights need the "
+        f"explicit opt-in SUPER_RAG_AMD_SYNTHETIC=1")
 
 
 class Encoder:
     """One encoder instance resident on one device (sr_encoder_* in the C-ABI)."""
 
     def __init__(self, spec: ModelSpec, device: int = 0, weights: dict | None = None,
-                 seed: int = 0, max_tokens: int = 0, init_style: str = "hf"):
+                 seed: int = 0, max_tokens: int = 0, init_style: str = "hf",
+                 checkpoint: str | None = None):
+        if weights is None:   # resolve first: a missing checkpoint fails before any device work
+            weights = model_weights(spec, checkpoint, seed, init_style)
         N.require_gpu()
         self.spec = spec
         self.device = int(device)
@@ -174,9 +289,6 @@ class Encoder:
         h = ctypes.c_void_p()
         N.call("sr_encoder_create", ctypes.byref(cfg), self.device, ctypes.byref(h))
         self._h = h
-        if weights is None:
-            ckpt = find_checkpoint(spec)
-            weights = load_safetensors(ckpt) if ckpt else random_weights(spec, seed, init_style)
         self.load_weights(weights)
 
     def load_weights(self, weights: dict) -> None:

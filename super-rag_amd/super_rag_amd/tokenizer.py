@@ -1,14 +1,15 @@
 """Host-side tokenisation for the in-process encoders.
 
 The reference never tokenises: text goes to remote servers (embedding_service.py:168-175,
-rerank_service.py:95-104).  In-process we need token ids.  With a Hugging Face ``tokenizer.json``
-(``SUPER_RAG_AMD_WEIGHTS/<model>/tokenizer.json`` or an explicit path) the real WordPiece /
-SentencePiece vocabulary is used through the ``tokenizers`` library.  No vocabulary ships
-offline, so otherwise a deterministic hashing tokenizer of the same id range is used (documented
-in DESIGN.md as synthetic: embeddings are then only self-consistent, not BGE-compatible).
+rerank_service.py:95-104).  In-process we need token ids: the model's Hugging Face ``tokenizer.json``
+(``$SUPER_RAG_AMD_WEIGHTS/<model>/tokenizer.json`` or an explicit path) through the
+``tokenizers`` library.  A missing vocabulary is an error; the deterministic hashing tokenizer of
+the same id range (synthetic: embeddings only self-consistent, not BGE-compatible) needs the
+explicit opt-in ``SUPER_RAG_AMD_SYNTHETIC=1`` (tests, benchmarks) or ``synthetic=True``.
 """
 from __future__ import annotations
 
+import logging
 import os
 import re
 from typing import List, Sequence, Tuple
@@ -18,6 +19,7 @@ import numpy as np
 _WORD = re.compile(r"[぀-ヿ㐀-䶿一-鿿가-힯]|\w+|[^\w\s]",
                    re.UNICODE)
 _FIRST_ID = 1000  # ids below are reserved for specials / control tokens
+logger = logging.getLogger(__name__)
 
 
 def _fnv1a(s: str) -> int:
@@ -46,17 +48,28 @@ def longest_first(a: int, b: int, budget: int):
 
 
 class Tokenizer:
-    def __init__(self, spec, path: str | None = None):
+    def __init__(self, spec, path: str | None = None, synthetic: bool | None = None):
+        from .encoder import ModelAssetsError, model_dir, synthetic_allowed
         self.spec = spec
         self.max_length = spec.max_length
         self._hf = None
-        if path is None:
-            root = os.environ.get("SUPER_RAG_AMD_WEIGHTS")
-            cand = os.path.join(root, spec.name, "tokenizer.json") if root else None
-            path = cand if cand and os.path.exists(cand) else None
+        if path is None and not synthetic:
+            d = model_dir(spec.name)
+            if d is not None:
+                path = os.path.join(d, "tokenizer.json")
         if path:
+            if not os.path.exists(path):
+                raise ModelAssetsError(f"tokenizer for {spec.name} not found: {path}")
             from tokenizers import Tokenizer as HFTokenizer
             self._hf = HFTokenizer.from_file(path)
+        elif synthetic or (synthetic is None and synthetic_allowed()):
+            logger.warning("%s: hashing tokenizer (synthetic opt-in), not the model vocabulary",
+                           spec.name)
+        else:
+            raise ModelAssetsError(
+                f"no tokenizer for {spec.name}: set SUPER_RAG_AMD_WEIGHTS to a directory holding "
+                f"{spec.name}/tokenizer.json (or pass path=); the hashing tokenizer needs the "
+                f"explicit opt-in SUPER_RAG_AMD_SYNTHETIC=1")
         self.synthetic = self._hf is None
 
     # -- content tokens (no specials) -------------------------------------------------------------

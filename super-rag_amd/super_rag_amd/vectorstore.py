@@ -93,6 +93,7 @@ class _Collection:
         self.masks: Dict[str, tuple] = {}   # filter -> (version, mask_key, allow mask)
         self.lex = None         # BM25 index over the same rows (ctx "fulltext"), lexical.py
         self.vocab = None
+        self.journal = None     # persist.Journal with ctx["snapshot_dir"]
 
     def ensure_lex(self) -> None:
         """Create the lexical index, back-filling the rows added before it existed."""
@@ -108,35 +109,83 @@ class _Collection:
                 lex.remove(np.asarray(dead, dtype=np.int64))
         self.lex, self.vocab = lex, vocab
 
-    def snapshot(self, directory: str) -> None:
-        os.makedirs(directory, exist_ok=True)
-        base = os.path.join(directory, self.name)
-        self.store.save(base + ".srmi")
-        meta = {"dim": self.dim, "ids": self.ids, "texts": self.texts,
-                "metadatas": self.metadatas}
-        if self.lex is not None:
-            self.lex.save(base + ".srlex")
-            meta["lex_vocab"] = self.vocab.terms
-        with open(base + ".json.tmp", "w", encoding="utf-8") as f:
-            json.dump(meta, f)
-        os.replace(base + ".json.tmp", base + ".json")
+    # -- checkpoint / resume (persist.py) ----------------------------------------------------------
+    def persist_add(self, first_row: int, vecs, ids, texts, metadatas) -> None:
+        if self.journal is None:
+            return
+        if self.journal.gen is None:
+            self.journal.checkpoint(self)          # first base of a new collection
+        else:
+            self.journal.append_add(first_row, vecs, ids, texts, metadatas)
+
+    def persist_delete(self, rows, compacted: bool) -> None:
+        if self.journal is None:
+            return
+        if compacted or self.journal.gen is None:
+            self.journal.checkpoint(self)          # rows were renumbered: new base
+        else:
+            self.journal.append_delete(rows)
+
+    def maybe_checkpoint(self, ratio: float) -> None:
+        j = self.journal
+        if j is not None and j.gen is not None and \
+                j.journal_bytes() > ratio * j.base_bytes() + (64 << 20):
+            j.checkpoint(self)
+
+    def _replay(self, rec: dict) -> None:
+        if rec["op"] == "add":
+            vecs = self.journal.vectors(rec, self.dim)
+            rows = self.store.add(vecs)
+            if int(rows[0]) != int(rec["row"]) or len(rows) != len(rec["ids"]):
+                raise IOError(f"{self.journal.log_path}: add replays at row {int(rows[0])}, "
+                              f"journaled at {rec['row']}")
+            if self.lex is not None:
+                from .lexical import analyze
+                self.lex.add([self.vocab.doc_ids(analyze(t)) for t in rec["texts"]])
+            for u, t, m in zip(rec["ids"], rec["texts"], rec["metadatas"]):
+                self.row_of[u] = len(self.ids)
+                self.ids.append(u)
+                self.texts.append(t)
+                self.metadatas.append(m)
+        elif rec["op"] == "del":
+            rows = np.asarray(rec["rows"], dtype=np.int64)
+            self.store.remove(rows)
+            if self.lex is not None:
+                self.lex.remove(rows)
+            for r in rows.tolist():
+                self.row_of.pop(self.ids[r], None)
+                self.ids[r] = self.texts[r] = self.metadatas[r] = None
+        else:
+            raise IOError(f"{self.journal.log_path}: unknown journal op {rec['op']!r}")
 
     @classmethod
     def restore(cls, name: str, directory: str, device: int) -> Optional["_Collection"]:
-        base = os.path.join(directory, name)
-        if not (os.path.exists(base + ".srmi") and os.path.exists(base + ".json")):
+        from .persist import Journal
+        j = Journal(directory, name)
+        meta = j.read_meta()
+        if meta is None:
             return None
-        with open(base + ".json", encoding="utf-8") as f:
-            meta = json.load(f)
-        c = cls(name, int(meta["dim"]), device, store=_store_loader(base + ".srmi", device))
+        gen = meta.get("gen")            # None: the round-1 layout (<name>.srmi, no journal)
+        store = _store_loader(j.store_path(gen), device)
+        n_rows, _ = store.count()
+        if n_rows != meta.get("n_rows", len(meta["ids"])) or n_rows != len(meta["ids"]):
+            raise IOError(f"snapshot of {name} is inconsistent: {n_rows} stored rows, metadata "
+                          f"for {len(meta['ids'])} (generation {gen})")
+        c = cls(name, int(meta["dim"]), device, store=store)
         c.ids = meta["ids"]
         c.texts = meta["texts"]
         c.metadatas = meta["metadatas"]
         c.row_of = {u: i for i, u in enumerate(c.ids) if u is not None}
-        if "lex_vocab" in meta and os.path.exists(base + ".srlex"):
+        if "lex_vocab" in meta and os.path.exists(j.lex_path(gen)):
             from .lexical import Vocab
-            c.lex = _lex_loader(base + ".srlex", device)
+            c.lex = _lex_loader(j.lex_path(gen), device)
             c.vocab = Vocab(meta["lex_vocab"])
+        j.gen = gen
+        c.journal = j
+        for rec in j.records(gen):
+            c._replay(rec)
+        if gen is None:
+            j.checkpoint(c)              # migrate to the journaled layout
         return c
 
 
@@ -173,6 +222,7 @@ class MI355XVectorStoreConnector:
         self.hybrid_k_each = ctx.get("hybrid_k_each")
         self.rrf_rank_const = int(ctx.get("rrf_rank_const", 1))
         self.scan_dtype = str(ctx.get("scan_dtype", "fp16"))   # "fp8": e4m3 scan + fp16 re-score
+        self.checkpoint_ratio = float(ctx.get("checkpoint_ratio", 1.0))
         self.store = self
         if self.snapshot_dir and _get(self.collection_name) is None:
             c = _Collection.restore(self.collection_name, self.snapshot_dir, self.device)
@@ -195,6 +245,9 @@ class MI355XVectorStoreConnector:
             c = _collections.get(self.collection_name)
             if c is None:
                 c = _Collection(self.collection_name, int(dim), self.device)
+                if self.snapshot_dir:
+                    from .persist import Journal
+                    c.journal = Journal(self.snapshot_dir, self.collection_name)
                 _collections[self.collection_name] = c
         self._apply_scan_dtype(c)
         return c
@@ -212,14 +265,8 @@ class MI355XVectorStoreConnector:
         if c is not None and hasattr(c.store, "close"):
             c.store.close()
         if self.snapshot_dir:
-            for ext in (".srmi", ".json", ".srlex"):
-                p = os.path.join(self.snapshot_dir, self.collection_name + ext)
-                if os.path.exists(p):
-                    os.remove(p)
-
-    def _persist(self, c: _Collection) -> None:
-        if self.snapshot_dir:
-            c.snapshot(self.snapshot_dir)
+            from .persist import Journal
+            Journal(self.snapshot_dir, self.collection_name).remove_all()
 
     # -- mutation ---------------------------------------------------------------------------------
     def add(self, nodes) -> List[str]:
@@ -240,6 +287,7 @@ class MI355XVectorStoreConnector:
                 from .lexical import analyze
                 first = c.lex.add([c.vocab.doc_ids(analyze(n.text)) for n in nodes])
                 assert first == int(rows[0]), "lexical index out of step with the store"
+            first = len(c.ids)
             for u, r, n in zip(ids, rows, nodes):
                 assert int(r) == len(c.ids)
                 c.ids.append(u)
@@ -247,7 +295,8 @@ class MI355XVectorStoreConnector:
                 c.texts.append(n.text)
                 c.metadatas.append(copy.deepcopy(n.metadata) if n.metadata is not None else None)
             c.version += 1
-            self._persist(c)
+            c.persist_add(first, vecs, ids, c.texts[first:], c.metadatas[first:])
+            c.maybe_checkpoint(self.checkpoint_ratio)
         logger.debug("Added %d documents to collection %s", len(ids), self.collection_name)
         return ids
 
@@ -269,10 +318,12 @@ class MI355XVectorStoreConnector:
                     c.texts[r] = None
                     c.metadatas[r] = None
                 n_rows, n_live = c.store.count()
-                if n_rows and n_live < (1.0 - self.compact_ratio) * n_rows:
+                compacted = bool(n_rows and n_live < (1.0 - self.compact_ratio) * n_rows)
+                if compacted:
                     self._compact(c)
                 c.version += 1
-            self._persist(c)
+                c.persist_delete(rows, compacted)
+                c.maybe_checkpoint(self.checkpoint_ratio)
 
     def _compact(self, c: _Collection) -> None:
         remap = c.store.compact()

@@ -9,3 +9,7 @@ for p in (ROOT, os.path.join(ROOT, "super-rag_amd")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+
+# Seeded random weights and the hashing tokenizer are an explicit opt-in of tests and benchmarks
+# (encoder.synthetic_allowed); tests of the product-path refusal delete the variable.
+os.environ.setdefault("SUPER_RAG_AMD_SYNTHETIC", "1")
