@@ -290,7 +290,8 @@ int sr_profile_read(sr_kernel_stat* out, int max, int* n);
  * ldy (fp16 for epi 0/1/4, fp32 for 2/3).  epi: 0 bias, 1 bias+GELU, 2 bias+residual fp32,
  * 3 bias+tanh (fp32 out), 4 bias+residual fp16.  variant: -1 auto, 0 128x128, 1 256x256 (8 waves,
  * 2-stage), 4 pipelined 256x256, 5 persistent pipelined 256x256 (6 / 7: timing-only diagnostics
- * with wrong results). */
+ * with wrong results); variant | 0x100 = split weights: W is [hi | lo] (N x K) over an X of K / 2
+ * columns (the embedders' precision mode). */
 int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, int device,
                  void* stream);

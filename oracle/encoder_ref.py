@@ -37,7 +37,7 @@ class RefConfig:
 
 def position_ids(ids: torch.Tensor, offset: int) -> torch.Tensor:
     if offset == 0:
-        return torch.arange(ids.shape[1]).unsqueeze(0).expand_as(ids)
+        return torch.arange(ids.shape[1], device=ids.device).unsqueeze(0).expand_as(ids)
     m = (ids != offset).long()
     return torch.cumsum(m, dim=1) * m + offset
 
@@ -85,10 +85,14 @@ def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
     fp8_rows(fp16(W2 / 2)); 2 = also FFN1 and the QKV of layers >= 1 as _fold8 on the pre-LN
     residual sums."""
     fp8 = max(fp8, 1 if fp8_ffn else 0)
-    ids = torch.as_tensor(np.asarray(ids), dtype=torch.long)
-    mask = torch.as_tensor(np.asarray(mask), dtype=torch.float32)
+    # weights given as torch tensors on a device (e.g. fp32 on the GPU for the long-sequence
+    # checks) run the same restatement there; numpy weights run on the CPU
+    dev = _t(w, "embeddings.word_embeddings.weight").device
+    ids = torch.as_tensor(np.asarray(ids), dtype=torch.long, device=dev)
+    mask = torch.as_tensor(np.asarray(mask), dtype=torch.float32, device=dev)
     B, S = ids.shape
-    tt = torch.zeros_like(ids) if type_ids is None else torch.as_tensor(np.asarray(type_ids), dtype=torch.long)
+    tt = torch.zeros_like(ids) if type_ids is None else \
+        torch.as_tensor(np.asarray(type_ids), dtype=torch.long, device=dev)
     pos = position_ids(ids, cfg.position_offset)
     x = (_t(w, "embeddings.word_embeddings.weight")[ids]
          + _t(w, "embeddings.position_embeddings.weight")[pos]
@@ -136,14 +140,14 @@ def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
 def embed(cfg: RefConfig, w: dict, ids, mask, type_ids=None, pool: str = "cls") -> np.ndarray:
     """Sentence embeddings [B, d], pooled then L2-normalised (fp32)."""
     h = encode_hidden(cfg, w, ids, mask, type_ids)
-    m = torch.as_tensor(np.asarray(mask), dtype=torch.float32)
+    m = torch.as_tensor(np.asarray(mask), dtype=torch.float32, device=h.device)
     if pool == "cls":
         e = h[:, 0]
     else:
         e = (h * m[..., None]).sum(1) / m.sum(1, keepdim=True).clamp_min(1e-30)
     n = e.norm(dim=-1, keepdim=True)
     e = torch.where(n > 0, e / n, torch.zeros_like(e))
-    return e.numpy()
+    return e.cpu().numpy()
 
 
 @torch.no_grad()
@@ -152,7 +156,7 @@ def cross_logits(cfg: RefConfig, w: dict, ids, mask, type_ids=None, fp8_ffn: boo
     """RoBERTa classification head on the first token: [P, num_labels] raw logits."""
     h = encode_hidden(cfg, w, ids, mask, type_ids, fp8_ffn, fp8)[:, 0]
     t = torch.tanh(h @ _t(w, "classifier.dense.weight").T + _t(w, "classifier.dense.bias"))
-    return (t @ _t(w, "classifier.out_proj.weight").T + _t(w, "classifier.out_proj.bias")).numpy()
+    return (t @ _t(w, "classifier.out_proj.weight").T + _t(w, "classifier.out_proj.bias")).cpu().numpy()
 
 
 def longest_first(a: int, b: int, budget: int):

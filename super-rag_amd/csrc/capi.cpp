@@ -661,9 +661,15 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
   SR_CHECK(epi >= 0 && epi <= 4, "diag_gemm: epi must be 0..4");
   SR_CHECK((epi != 2 && epi != 4) || R, "diag_gemm: residual epilogue needs R");
   sr::DeviceGuard g(device);
+  sr::LnFold lf;  // variant | 0x100: split weights, W = [hi | lo] with K = 2 x_k
+  if (variant >= 0 && (variant & 0x100)) {
+    SR_CHECK(K % 128 == 0, "diag_gemm: split weights need K % 128 == 0");
+    lf.x_k = K / 2;
+    variant &= 0xff;
+  }
   sr::launch_gemm_variant(variant, epi, reinterpret_cast<const sr::half_t*>(X), lda,
                           reinterpret_cast<const sr::half_t*>(W), bias, R, ldr, Y, ldy, M, N, K,
-                          reinterpret_cast<hipStream_t>(stream));
+                          reinterpret_cast<hipStream_t>(stream), &lf);
   SR_API_END
 }
 

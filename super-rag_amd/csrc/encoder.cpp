@@ -42,6 +42,11 @@ Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(
   SR_HIP(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
 
   const int64_t D = d, F = cfg.intermediate;
+  {
+    const char* e = std::getenv("SR_WEIGHT_SPLIT");  // A/B of the precision mode (default on)
+    split_ = !cfg.residual_fp16 && !(e && e[0] == '0');
+  }
+  const int64_t sk = split_ ? D : 0, skf = split_ ? F : 0;
   register_target("embeddings.word_embeddings.weight", wemb_, (int64_t)cfg.vocab_size * D, true);
   register_target("embeddings.position_embeddings.weight", pemb_, (int64_t)cfg.max_position * D, true);
   register_target("embeddings.token_type_embeddings.weight", temb_, (int64_t)cfg.type_vocab * D, true);
@@ -51,19 +56,19 @@ Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(
   for (int l = 0; l < cfg.layers; ++l) {
     Layer& L = layers_[l];
     const std::string p = "encoder.layer." + std::to_string(l) + ".";
-    register_target(p + "attention.self.query.weight", L.wqkv, D * D, true, 0, 3 * D * D);
-    register_target(p + "attention.self.key.weight", L.wqkv, D * D, true, D * D, 3 * D * D);
-    register_target(p + "attention.self.value.weight", L.wqkv, D * D, true, 2 * D * D, 3 * D * D);
+    register_target(p + "attention.self.query.weight", L.wqkv, D * D, true, 0, 3 * D * D, sk);
+    register_target(p + "attention.self.key.weight", L.wqkv, D * D, true, D * D, 3 * D * D, sk);
+    register_target(p + "attention.self.value.weight", L.wqkv, D * D, true, 2 * D * D, 3 * D * D, sk);
     register_target(p + "attention.self.query.bias", L.bqkv, D, false, 0, 3 * D);
     register_target(p + "attention.self.key.bias", L.bqkv, D, false, D, 3 * D);
     register_target(p + "attention.self.value.bias", L.bqkv, D, false, 2 * D, 3 * D);
-    register_target(p + "attention.output.dense.weight", L.wo, D * D, true);
+    register_target(p + "attention.output.dense.weight", L.wo, D * D, true, 0, -1, sk);
     register_target(p + "attention.output.dense.bias", L.bo, D, false);
     register_target(p + "attention.output.LayerNorm.weight", L.ln1g, D, false);
     register_target(p + "attention.output.LayerNorm.bias", L.ln1b, D, false);
-    register_target(p + "intermediate.dense.weight", L.w1, F * D, true);
+    register_target(p + "intermediate.dense.weight", L.w1, F * D, true, 0, -1, sk);
     register_target(p + "intermediate.dense.bias", L.b1, F, false);
-    register_target(p + "output.dense.weight", L.w2, D * F, true);
+    register_target(p + "output.dense.weight", L.w2, D * F, true, 0, -1, skf);
     register_target(p + "output.dense.bias", L.b2, D, false);
     register_target(p + "output.LayerNorm.weight", L.ln2g, D, false);
     register_target(p + "output.LayerNorm.bias", L.ln2b, D, false);
@@ -102,14 +107,17 @@ Encoder::~Encoder() {
 }
 
 void Encoder::register_target(const std::string& name, DevBuf& buf, int64_t numel, bool f16,
-                              int64_t offset_elems, int64_t total_elems) {
+                              int64_t offset_elems, int64_t total_elems, int64_t split_k) {
   const int64_t total = total_elems < 0 ? numel : total_elems;
   const size_t esz = f16 ? sizeof(half_t) : sizeof(float);
+  const int64_t rep = split_k > 0 ? 2 : 1;  // split: hi and lo halves of every row
   if (buf.p == nullptr) {
-    buf.reserve((size_t)total * esz);
-    SR_HIP(hipMemset(buf.p, 0, (size_t)total * esz));
+    buf.reserve((size_t)total * rep * esz);
+    SR_HIP(hipMemset(buf.p, 0, (size_t)total * rep * esz));
   }
-  targets_[name] = Target{reinterpret_cast<char*>(buf.p) + offset_elems * esz, numel, f16};
+  Target t{reinterpret_cast<char*>(buf.p) + offset_elems * rep * esz, numel, f16};
+  t.split_k = split_k;
+  targets_[name] = t;
   is_set_[name] = false;
 }
 
@@ -123,7 +131,19 @@ void Encoder::set_weight(const std::string& name, const float* data, int64_t num
   DeviceGuard g(device_);
   begin(stream_);
   SR_HIP(hipStreamSynchronize(stream_));
-  if (t.f16) {
+  if (t.f16 && t.split_k > 0) {  // row r -> [fp16(w) | fp16(w - fp16(w))], 2 split_k halfs
+    const int64_t K = t.split_k;
+    SR_CHECK(numel % K == 0, "encoder: split weight '" + name + "' is not whole rows");
+    std::vector<half_t> h((size_t)numel * 2);
+    for (int64_t r = 0; r < numel / K; ++r)
+      for (int64_t j = 0; j < K; ++j) {
+        const float v = data[r * K + j];
+        const half_t hi = (half_t)v;
+        h[(size_t)(r * 2 * K + j)] = hi;
+        h[(size_t)(r * 2 * K + K + j)] = (half_t)(v - (float)hi);
+      }
+    SR_HIP(hipMemcpy(t.ptr, h.data(), h.size() * sizeof(half_t), hipMemcpyHostToDevice));
+  } else if (t.f16) {
     std::vector<half_t> h((size_t)numel);
     for (int64_t i = 0; i < numel; ++i) h[i] = (half_t)data[i];
     SR_HIP(hipMemcpy(t.ptr, h.data(), (size_t)numel * sizeof(half_t), hipMemcpyHostToDevice));
@@ -390,21 +410,29 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       launch_ln_apply(cls_only ? Uc : U, d, mB, Lz.ln2g.as<float>(), Lz.ln2b.as<float>(),
                       cls_only ? nb : M, d, h16, s);
     }
+    // split weights: W = [hi | lo] (N x 2K), the GEMM's K is 2K over the repeated activation
+    const int kr = split_ ? 2 : 1;
+    auto lin = [&](int epi, const half_t* X, int64_t lda, const half_t* W, const float* b,
+                   const void* R, int64_t ldr, void* Y, int64_t ldy, int Mm, int Nn, int Kx) {
+      LnFold lx;
+      lx.x_k = split_ ? Kx : 0;
+      launch_gemm(epi, X, lda, W, b, R, ldr, Y, ldy, Mm, Nn, kr * Kx, s, &lx);
+    };
     for (size_t l = 0; l < (fold ? 0 : layers_.size()); ++l) {
       const Layer& L = layers_[l];
       const bool last = cls_only && l + 1 == layers_.size();
-      launch_gemm(EPI_BIAS_F16, h16, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
-                  3 * d, M, 3 * d, d, s);
+      lin(EPI_BIAS_F16, h16, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv, 3 * d, M,
+          3 * d, d);
       // rows of the rest of the block: all M tokens, or the nb CLS rows (compact) in the last layer
       const int Mr = last ? nb : M;
       launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
-      launch_gemm(epi_res, ctx, d, L.wo.as<half_t>(), L.bo.as<float>(), hres,
-                  last ? (int64_t)S * d : d, y, d, Mr, d, d, s);
+      lin(epi_res, ctx, d, L.wo.as<half_t>(), L.bo.as<float>(), hres, last ? (int64_t)S * d : d, y,
+          d, Mr, d, d);
       launch_layernorm(y, res16, L.ln1g.as<float>(), L.ln1b.as<float>(), cfg_.ln_eps, Mr, d, h16,
                        h32w, s);
-      launch_gemm(EPI_BIAS_GELU_F16, h16, d, L.w1.as<half_t>(), L.b1.as<float>(), nullptr, 0, ffn,
-                  F, Mr, F, d, s);
-      launch_gemm(epi_res, ffn, F, L.w2.as<half_t>(), L.b2.as<float>(), hres, d, y, d, Mr, d, F, s);
+      lin(EPI_BIAS_GELU_F16, h16, d, L.w1.as<half_t>(), L.b1.as<float>(), nullptr, 0, ffn, F, Mr, F,
+          d);
+      lin(epi_res, ffn, F, L.w2.as<half_t>(), L.b2.as<float>(), hres, d, y, d, Mr, d, F);
       launch_layernorm(y, res16, L.ln2g.as<float>(), L.ln2b.as<float>(), cfg_.ln_eps, Mr, d, h16,
                        h32w, s);
     }

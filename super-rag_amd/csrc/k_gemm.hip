@@ -513,14 +513,15 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // tile walk: n fastest, or groups of lf.group_m m-panels with m fastest inside a group (a window
   // of concurrent tiles then shares fewer W column tiles in the XCD's L2)
   const int gm = lf.group_m, tiles_m = (M + BM - 1) / BM;
+  // (only called for tt < nwg; gsz is clamped to >= 1 so no argument can divide by zero)
   auto tile_m = [&](int tt) __attribute__((always_inline)) {
     if (gm <= 1) return tt / tiles_n;
-    const int first = (tt / (gm * tiles_n)) * gm, gsz = min(gm, tiles_m - first);
+    const int first = (tt / (gm * tiles_n)) * gm, gsz = max(1, min(gm, tiles_m - first));
     return first + (tt - first * tiles_n) % gsz;
   };
   auto tile_n = [&](int tt) __attribute__((always_inline)) {
     if (gm <= 1) return tt % tiles_n;
-    const int first = (tt / (gm * tiles_n)) * gm, gsz = min(gm, tiles_m - first);
+    const int first = (tt / (gm * tiles_n)) * gm, gsz = max(1, min(gm, tiles_m - first));
     return (tt - first * tiles_n) / gsz;
   };
   int m0 = tile_m(t) * BM, n0 = tile_n(t) * BN;
@@ -530,6 +531,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wm = wave & 3;
   const int nk = K / GBK;
+  const int kxs = lf.x_k > 0 ? lf.x_k / GBK : nk;  // K-steps of the X operand (split weights)
+  (void)kxs;
   const int arow = wn * 128 + (lane & 15), brow = wm * 64 + (lane & 15), c0 = lane >> 4;
 
   // LDS-DMA staging is split by K-step parity: the 4 waves of group (s & 1) issue all 64 pieces
@@ -555,7 +558,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     const auto rx = panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2);
     // row-group offsets advanced in place (an opaque running value: precomputed per piece and
     // hoisted, the 32 soffsets would exhaust the SGPRs)
-    int sw = w4 * 8 * 16 * K + kt * GBK * 2, sx = w4 * 8 * 16 * (int)lda + kt * GBK * 2;
+    const int kx = kt >= kxs ? kt - kxs : kt;   // split weights: X's K-steps repeat
+    int sw = w4 * 8 * 16 * K + kt * GBK * 2, sx = w4 * 8 * 16 * (int)lda + kx * GBK * 2;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       asm volatile("" : "+s"(sw));
@@ -759,7 +763,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 
     const int t_next = t + t_step;
     const bool more = PERSIST && t_next < t_end && nk > 1;
-    const int m0n = tile_m(t_next) * BM, n0n = tile_n(t_next) * BN;
+    const int t_walk = more ? t_next : t;   // the next tile's coordinates only when it exists
+    const int m0n = tile_m(t_walk) * BM, n0n = tile_n(t_walk) * BN;
     int kt = 0;
     bool lenient = stores_pending;
     for (; kt + 2 < nk; ++kt) {
@@ -1017,7 +1022,7 @@ template <int EPI, int BN, int BM, int WN, int WM, bool PERSIST>
 __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) void gemm_f16_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
-    void* __restrict__ Y, int64_t ldy, int M, int N, int K) {
+    void* __restrict__ Y, int64_t ldy, int M, int N, int K, int kxs) {
   constexpr int WAVES = WN * WM;
   constexpr int FN = BN / WN / 16, FM = BM / WM / 16;  // 16x16 tiles per wave
   constexpr int NIA = BN / 8 / WAVES, NIB = BM / 8 / WAVES;
@@ -1070,8 +1075,9 @@ __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) vo
     const half_t* Bs = As + BN * GBK;
     if (kt + 1 < nk) {
       half_t* An = lds + (cur ^ 1) * STAGE;
+      const int kx = kt + 1 >= kxs ? kt + 1 - kxs : kt + 1;   // split weights: X repeats
       stage_tile<NIA>(W, K, n0, N, (kt + 1) * GBK, An, wave, lane);
-      stage_tile<NIB>(X, lda, m0, M, (kt + 1) * GBK, An + BN * GBK, wave, lane);
+      stage_tile<NIB>(X, lda, m0, M, kx * GBK, An + BN * GBK, wave, lane);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1114,12 +1120,12 @@ __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) vo
 template <int BN, int BM, int WN, int WM, bool PERSIST>
 void launch_tile(int epi, dim3 grid, hipStream_t stream, const half_t* X, int64_t lda,
                  const half_t* W, const float* bias, const void* R, int64_t ldr, void* Y,
-                 int64_t ldy, int M, int N, int K) {
+                 int64_t ldy, int M, int N, int K, int kxs) {
   const dim3 block(64 * WN * WM);
 #define SR_GEMM_CASE(E)                                                                        \
   case E:                                                                                      \
     hipLaunchKernelGGL((gemm_f16_kernel<E, BN, BM, WN, WM, PERSIST>), grid, block, 0, stream, \
-                       X, lda, W, bias, R, ldr, Y, ldy, M, N, K);                              \
+                       X, lda, W, bias, R, ldr, Y, ldy, M, N, K, kxs);                         \
     break;
   switch (epi) {
     SR_GEMM_CASE(EPI_BIAS_F16)
@@ -1350,6 +1356,9 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   SR_CHECK(!(epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS || epi == EPI_RES16_STATS_Y8 ||
              epi == EPI_LNR16_STATS_Y8) || lf->stat_out,
            "gemm: *_STATS epilogue needs stat_out");
+  const int x_k = lf && lf->x_k > 0 ? lf->x_k : K;
+  SR_CHECK(x_k == K || (K == 2 * x_k && x_k % GBK == 0 && epi < EPI_LNF_GELU_F8),
+           "gemm: split weights need K == 2 x_k (x_k % 64 == 0, fp16 operands)");
   if (M <= 0) return;
   const bool out32 = epi == EPI_BIAS_RES_F32 || epi == EPI_BIAS_TANH_F32;
   const double out_b = out32 ? 4.0 : epi == EPI_LNF_GELU_F8 ? 1.0 : 2.0;
@@ -1357,14 +1366,15 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
                        : (epi == EPI_BIAS_RES_F16 || epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS ||
                           epi == EPI_RES16_STATS_Y8 || epi == EPI_LNR16_STATS_Y8) ? 2.0
                                                                                                      : 0.0;
-  const double bytes = 2.0 * ((double)M * K + (double)N * K) + (out_b + res_b) * (double)M * N;
+  const double bytes = 2.0 * ((double)M * x_k + (double)N * K) + (out_b + res_b) * (double)M * N;
   ProfScope prof(epi_name(epi), stream, 2.0 * M * (double)N * K, bytes);
   const int64_t big_tiles = (N % 256 == 0) ? (int64_t)(N / 256) * ceil_div(M, 256) : 0;
   SR_CHECK(big_tiles < (1ll << 31), "gemm: too many tiles");
   int v = variant >= 0 ? variant : forced_tile();
   if (v < 0) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_SMALL;
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
-  if (v == GEMM_PP && (K % 32 != 0 || epi >= EPI_LNF_GELU_F8)) v = GEMM_PIPE;
+  if (v == GEMM_PP && (K % 32 != 0 || epi >= EPI_LNF_GELU_F8 || x_k != K)) v = GEMM_PIPE;
+  if (x_k != K && v >= GEMM_DIAG_NOLOAD && v != GEMM_PP) v = GEMM_PIPE;  // diagnostics: plain K
   if (fold && (v == GEMM_SMALL || v == GEMM_BIG)) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_PIPE;
   const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST || v == GEMM_PP) && !out32;
   SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
@@ -1374,11 +1384,15 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   // Short-K GEMMs (K <= 1024: QKV, FFN1, O-proj) walk groups of 8 (N >= 2048) or 4 m-panels;
   // FFN2 (K = 3072) stays n fastest.  Same-box A/B of the full bench: 422.8 / 424.0 -> 429.8 /
   // 431.0 q/s (profiles/r01_gemm_group_m.log).  SR_GEMM_GROUP_M overrides (diagnostic).
-  lfv.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;
-  if (const char* e = std::getenv("SR_GEMM_GROUP_M")) lfv.group_m = std::atoi(e);
+  static const int group_m_env = [] {
+    const char* e = std::getenv("SR_GEMM_GROUP_M");
+    return e ? std::atoi(e) : -1;
+  }();
+  lfv.group_m = group_m_env >= 0 ? group_m_env : (K <= 1024 ? (N >= 2048 ? 8 : 4) : 0);
+  lfv.x_k = x_k == K ? 0 : x_k;
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
-                                       ldr, Y, ldy, M, N, K);
+                                       ldr, Y, ldy, M, N, K, x_k / GBK);
   } else if (v >= GEMM_DIAG_P_NOEPI && v <= GEMM_DIAG_P_STOREONLY) {
     const int64_t g = 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8));
     const dim3 grid((unsigned)g), block(512);
@@ -1455,7 +1469,7 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
     const int64_t tiles = (int64_t)(N / 128) * ceil_div(M, 128);
     SR_CHECK(tiles < (1ll << 31), "gemm: too many tiles");
     launch_tile<128, 128, 2, 2, false>(epi, dim3((unsigned)tiles), stream, X, lda, W, bias, R,
-                                       ldr, Y, ldy, M, N, K);
+                                       ldr, Y, ldy, M, N, K, x_k / GBK);
   }
   SR_LAUNCH_CHECK();
 }

@@ -146,6 +146,7 @@ class Encoder {
     int64_t numel;
     bool f16;
     float* master = nullptr;  // fp32 copy kept for LayerNorm folding (QKV / FFN1 weights)
+    int64_t split_k = 0;      // split weights: rows of split_k fp32 -> [fp16 hi | fp16 lo]
   };
   struct Layer {
     DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, w1, b1, w2, b2, ln2g, ln2b;
@@ -160,7 +161,7 @@ class Encoder {
   void begin(hipStream_t s) { SR_HIP(hipStreamWaitEvent(s, done_, 0)); }
   void end(hipStream_t s) { SR_HIP(hipEventRecord(done_, s)); }
   void register_target(const std::string& name, DevBuf& buf, int64_t numel, bool f16,
-                       int64_t offset_elems = 0, int64_t total_elems = -1);
+                       int64_t offset_elems = 0, int64_t total_elems = -1, int64_t split_k = 0);
   void ensure_ws(int64_t tokens, int B);
 
   sr_encoder_config cfg_;
@@ -177,6 +178,10 @@ class Encoder {
   DevBuf statA_, statB_, mrA_, mrB_;  // per-row LayerNorm partials / (mu, rstd) (folded path)
   bool fold_ready_ = false;  // folded weights match the current weights
   int fp8_ = 0;
+  // split weights (fp32-residual encoders, i.e. the embedders): each layer matrix W is held as
+  // [fp16(W) | fp16(W - fp16(W))] and the GEMMs run K = 2 K_x over the repeated activation, which
+  // removes the fp16 weight rounding (~9e-4 of the 1.1e-3 embedding error of 24-layer bge-m3)
+  bool split_ = false;
   DevBuf u8_;  // e4m3 copy of the residual sums (fp8 mode 2)
   int64_t ws_tokens_ = 0;
 };

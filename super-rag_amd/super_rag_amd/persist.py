@@ -89,10 +89,18 @@ class Journal:
         for p in (self.log_path, self.vlog_path):
             if os.path.exists(p):
                 os.remove(p)
-        for p in (self.store_path(old), self.lex_path(old)) if old is not None else \
-                (self.store_path(None), self.lex_path(None)):
-            if os.path.exists(p):
-                os.remove(p)
+        self._remove_generation(old)
+
+    def _pattern(self, gen_re: str) -> "re.Pattern":
+        n = re.escape(self.name)
+        return re.compile(n + gen_re + r"\.(srmi|srlex)(\.s\d+|\.rows(\.tmp)?\.npz)?(\.tmp)?")
+
+    def _remove_generation(self, gen: Optional[int]) -> None:
+        """Files of one base generation (store, shard stores and tables, lexical index)."""
+        pat = self._pattern("" if gen is None else re.escape(f".g{gen}"))
+        for fn in os.listdir(self.dir):
+            if pat.fullmatch(fn):
+                os.remove(os.path.join(self.dir, fn))
 
     # -- journal --------------------------------------------------------------------------------------
     def _append(self, rec: dict) -> None:
@@ -145,9 +153,8 @@ class Journal:
         """Delete every file of this collection (and only this collection's)."""
         if not os.path.isdir(self.dir):
             return
-        pat = re.compile(re.escape(self.name) +
-                         r"(\.g\d+)?\.(srmi|srlex)(\.tmp)?$|" + re.escape(self.name) +
-                         r"\.(json|json\.tmp|log|vlog)$")
+        base = self._pattern(r"(\.g\d+)?")
+        own = re.compile(re.escape(self.name) + r"\.(json|json\.tmp|log|vlog)")
         for fn in os.listdir(self.dir):
-            if pat.fullmatch(fn):
+            if base.fullmatch(fn) or own.fullmatch(fn):
                 os.remove(os.path.join(self.dir, fn))

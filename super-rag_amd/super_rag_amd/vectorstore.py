@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import copy
 import json
+from collections import OrderedDict
 import logging
 import os
 import threading
@@ -35,6 +36,7 @@ from .models import DocumentWithScore, QueryResult
 logger = logging.getLogger(__name__)
 
 VECTOR_DB_TYPE = "mi355x"
+MASK_CACHE_SIZE = 8      # filter masks kept per collection (n_rows bytes each)
 
 
 def _native_store(dim: int, device: int):
@@ -77,12 +79,31 @@ def set_lex_backend(factory: Callable, loader: Callable | None = None) -> None:
     _lex_loader = loader or _native_lex_load
 
 
+def _make_store(dim: int, device: int, devices: Optional[List[int]]):
+    """One store on `device`, or a ShardedStore over ctx["devices"] (one shard per entry)."""
+    if devices and len(devices) > 1:
+        from .store import ShardedStore
+        return ShardedStore(dim, devices, factory=lambda d, dev: _store_factory(d, dev))
+    return _store_factory(dim, devices[0] if devices else device)
+
+
+def _load_store(path: str, device: int, devices: Optional[List[int]]):
+    from .store import ShardedStore
+    if ShardedStore.is_manifest(path):
+        return ShardedStore.load(path, devices or [device], loader=_store_loader)
+    if devices and len(devices) > 1:
+        raise IOError(f"{path}: a single-device collection cannot load on devices {devices}")
+    return _store_loader(path, devices[0] if devices else device)
+
+
 class _Collection:
-    def __init__(self, name: str, dim: int, device: int, store=None):
+    def __init__(self, name: str, dim: int, device: int, store=None,
+                 devices: Optional[List[int]] = None):
         self.name = name
         self.dim = dim
         self.device = device
-        self.store = store if store is not None else _store_factory(dim, device)
+        self.devices = devices
+        self.store = store if store is not None else _make_store(dim, device, devices)
         self.ids: List[Optional[str]] = []       # row -> uuid (None once deleted)
         self.row_of: Dict[str, int] = {}
         self.texts: List[Optional[str]] = []
@@ -90,7 +111,8 @@ class _Collection:
         self.lock = threading.RLock()
         self.coalescer = None   # created on first coalesced search (coalesce.py)
         self.version = 0        # bumped on every add / delete / compaction
-        self.masks: Dict[str, tuple] = {}   # filter -> (version, mask_key, allow mask)
+        # filter -> (version, mask_key, allow mask): a small LRU (each mask is n_rows bytes)
+        self.masks: "OrderedDict[str, tuple]" = OrderedDict()
         self.lex = None         # BM25 index over the same rows (ctx "fulltext"), lexical.py
         self.vocab = None
         self.journal = None     # persist.Journal with ctx["snapshot_dir"]
@@ -159,19 +181,20 @@ class _Collection:
             raise IOError(f"{self.journal.log_path}: unknown journal op {rec['op']!r}")
 
     @classmethod
-    def restore(cls, name: str, directory: str, device: int) -> Optional["_Collection"]:
+    def restore(cls, name: str, directory: str, device: int,
+                devices: Optional[List[int]] = None) -> Optional["_Collection"]:
         from .persist import Journal
         j = Journal(directory, name)
         meta = j.read_meta()
         if meta is None:
             return None
         gen = meta.get("gen")            # None: the round-1 layout (<name>.srmi, no journal)
-        store = _store_loader(j.store_path(gen), device)
+        store = _load_store(j.store_path(gen), device, devices)
         n_rows, _ = store.count()
         if n_rows != meta.get("n_rows", len(meta["ids"])) or n_rows != len(meta["ids"]):
             raise IOError(f"snapshot of {name} is inconsistent: {n_rows} stored rows, metadata "
                           f"for {len(meta['ids'])} (generation {gen})")
-        c = cls(name, int(meta["dim"]), device, store=store)
+        c = cls(name, int(meta["dim"]), device, store=store, devices=devices)
         c.ids = meta["ids"]
         c.texts = meta["texts"]
         c.metadatas = meta["metadatas"]
@@ -208,6 +231,11 @@ class MI355XVectorStoreConnector:
         if self.distance != "cosine":
             raise ValueError(f"unsupported distance '{self.distance}' (only cosine)")
         self.device = int(ctx.get("device", os.environ.get("SUPER_RAG_AMD_DEVICE", 0)))
+        # ctx "devices": shard the collection's rows over several GPUs (store.ShardedStore)
+        devs = ctx.get("devices")
+        self.devices = [int(d) for d in devs] if devs else None
+        if self.devices and len(self.devices) > 1 and (ctx.get("fulltext") or ctx.get("hybrid")):
+            raise ValueError("fulltext / hybrid collections are single-device (ctx 'devices')")
         self.snapshot_dir = ctx.get("snapshot_dir")
         self.coalesce = bool(ctx.get("coalesce", True))
         self.max_batch = int(ctx.get("max_batch", 256))
@@ -225,7 +253,8 @@ class MI355XVectorStoreConnector:
         self.checkpoint_ratio = float(ctx.get("checkpoint_ratio", 1.0))
         self.store = self
         if self.snapshot_dir and _get(self.collection_name) is None:
-            c = _Collection.restore(self.collection_name, self.snapshot_dir, self.device)
+            c = _Collection.restore(self.collection_name, self.snapshot_dir, self.device,
+                                    self.devices)
             if c is not None:
                 with _registry_lock:
                     _collections.setdefault(self.collection_name, c)
@@ -244,7 +273,8 @@ class MI355XVectorStoreConnector:
         with _registry_lock:
             c = _collections.get(self.collection_name)
             if c is None:
-                c = _Collection(self.collection_name, int(dim), self.device)
+                c = _Collection(self.collection_name, int(dim), self.device,
+                                devices=self.devices)
                 if self.snapshot_dir:
                     from .persist import Journal
                     c.journal = Journal(self.snapshot_dir, self.collection_name)
@@ -371,6 +401,7 @@ class MI355XVectorStoreConnector:
         key = canonical(flt)
         hit = c.masks.get(key)
         if hit is not None and hit[0] == c.version:
+            c.masks.move_to_end(key)
             return hit[1], hit[2]
         allow = np.fromiter((u is not None and matches(flt, md)
                              for u, md in zip(c.ids, c.metadatas)), dtype=np.uint8, count=len(c.ids))
@@ -379,6 +410,11 @@ class MI355XVectorStoreConnector:
             _mask_serial += 1
             mkey = _mask_serial
         c.masks[key] = (c.version, mkey, allow)
+        c.masks.move_to_end(key)
+        for k in [k for k, v in c.masks.items() if v[0] != c.version]:
+            del c.masks[k]                      # stale: the rows changed since
+        while len(c.masks) > MASK_CACHE_SIZE:
+            c.masks.popitem(last=False)
         return mkey, allow
 
     @staticmethod

@@ -88,3 +88,22 @@ def test_filters_are_ignored_by_default_like_the_reference(conn_factory):
     cm = ContextManager("flt", None, "mi355x", {"collection": "flt"})
     hits = cm.query("q", score_threshold=0.99, topk=3, vector=[1.0, 0.0], chat_id="c1")
     assert len(hits) == 3   # neither the chat_id filter nor the threshold is applied
+
+
+def test_filter_mask_cache_is_bounded(conn_factory):
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.models import QueryWithEmbedding, TextNode
+    conn = conn_factory(honor_filter=True, coalesce=False)
+    conn.store.add([TextNode(text=f"t{i}", metadata={"chat_id": f"c{i % 20}"},
+                             embedding=[1.0, float(i)]) for i in range(40)])
+    q = QueryWithEmbedding(query="q", top_k=3, embedding=[1.0, 0.0])
+    for c in range(20):                           # 20 distinct filters
+        hits = conn.search(q, filter={"chat_id": c and f"c{c}" or "c0"}).results
+        assert all(h.metadata["chat_id"] == f"c{c}" for h in hits)
+    masks = V._get("flt").masks
+    assert len(masks) == V.MASK_CACHE_SIZE
+    conn.search(q, filter={"chat_id": "c19"})     # a hit refreshes its entry
+    assert next(reversed(masks)).find("c19") >= 0
+    conn.store.add([TextNode(text="new", metadata={"chat_id": "c1"}, embedding=[0.0, 1.0])])
+    conn.search(q, filter={"chat_id": "c1"})      # version changed: stale masks are dropped
+    assert len(masks) == 1

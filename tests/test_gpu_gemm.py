@@ -60,3 +60,48 @@ def test_gemm_persistent_multi_tile(epi):
     assert err <= tol, f"persistent epi{epi}: max|err| {err:.3e} > {tol:.1e}"
     err, tol = _run(VARIANTS["pipe_persist"], epi, 96 * 256, 2304, 128, seed=11 + epi)
     assert err <= tol, f"persistent K=128 epi{epi}: max|err| {err:.3e} > {tol:.1e}"
+
+
+@pytest.mark.parametrize("M,N", [(13 * 256 - 5, 768), (37 * 256 - 100, 3072), (9 * 256, 768)])
+def test_gemm_persistent_grouped_walk_ragged_last_group(M, N):
+    # the grouped tile walk (K <= 1024: groups of 4 m-panels for N < 2048, 8 for N >= 2048) with a
+    # partial last group (13 % 4, 37 % 8 m-tiles) and tiles_n > 1; 9 m-tiles: tiles_m % gm == 1
+    for epi in (0, 4):
+        err, tol = _run(VARIANTS["pipe_persist"], epi, M, N, 768, seed=M + N + epi)
+        assert err <= tol, f"grouped walk {M}x{N} epi{epi}: max|err| {err:.3e} > {tol:.1e}"
+
+
+@pytest.mark.parametrize("variant", ["small", "big", "pipe", "pipe_persist"])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_split_weights_match_fp32_weights(variant, epi):
+    """Split weights (the embedders' precision mode): W = [fp16(W) | fp16(W - fp16(W))] over a
+    repeated X gives X . W^T with the fp32 weights, not their fp16 rounding."""
+    import torch
+    from super_rag_amd import _native as NT
+    dev = torch.device("cuda", 0)
+    M, N, K = 2300, 768, 1024
+    g = torch.Generator(device=dev).manual_seed(epi)
+    X = (torch.randn(M, K, device=dev, generator=g) * 0.5).half()
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    hi = W.half()
+    lo = (W - hi.float()).half()
+    W2 = torch.cat([hi, lo], 1).contiguous()
+    b = torch.randn(N, device=dev, generator=g) * 0.1
+    R = torch.randn(M, N, device=dev, generator=g) if epi == 2 else None
+    Y = torch.full((M, N), float("nan"), device=dev, dtype=torch.float32 if epi == 2 else torch.float16)
+    NT.call("sr_diag_gemm", VARIANTS[variant] | 0x100, epi, X.data_ptr(), X.stride(0), W2.data_ptr(),
+            b.data_ptr(), R.data_ptr() if R is not None else None, R.stride(0) if R is not None else 0,
+            Y.data_ptr(), Y.stride(0), M, N, 2 * K, 0, torch.cuda.current_stream().cuda_stream)
+    ref = X.double() @ W.double().T + b.double()
+    ref_h = X.double() @ hi.double().T + b.double()          # what unsplit fp16 weights give
+    if epi == 1:
+        ref, ref_h = torch.nn.functional.gelu(ref), torch.nn.functional.gelu(ref_h)
+    elif epi == 2:
+        ref, ref_h = ref + R.double(), ref_h + R.double()
+    torch.cuda.synchronize()
+    err = (Y.double() - ref).abs().max().item()
+    err_h = (ref_h - ref).abs().max().item()
+    out_round = (2 ** -11 if epi != 2 else 2 ** -23) * ref.abs().max().item()
+    assert err <= out_round + 2e-5, f"{variant} epi{epi}: {err:.3e}"
+    if epi == 2:   # fp32 output: the split is visibly more exact than fp16 weights
+        assert err < 0.1 * err_h, (err, err_h)

@@ -209,3 +209,22 @@ def test_two_rank_sharded_pipeline_equals_single_process():
         np.testing.assert_allclose(got[r]["cand_sims"], full[r]["cand_sims"], atol=1e-6)
         np.testing.assert_array_equal(got[r]["rows"], full[r]["rows"])
         np.testing.assert_allclose(got[r]["logits"], full[r]["logits"], atol=1e-5)
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` (no torch.distributed.run) starts both ranks itself; gloo lets
+    them share the box's one GPU.  The JSON line reports the world the backend formed."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--corpus-rows", "200000", "--batch", "32",
+                        "--steps", "1", "--warmup", "1", "--batches", "1", "--no-cpu-baseline",
+                        "--rerank-max-tokens", "65536"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 64
+    assert "reports world_size 2" in r.stderr

@@ -1,0 +1,79 @@
+"""GPU: a collection sharded over several stores (ctx "devices") returns exactly one store's results.
+
+Two shards on the box's one GPU exercise the same code as one shard per GPU: per-shard K1 + K2,
+local -> global rows on the device, K2 topk_merge (sr_topk_merge_dev) on the first device; filtered
+searches through the per-shard masked search and the host merge.  Reference surface:
+MI355XVectorStoreConnector.search == SeekDBVectorStoreConnector.search (seekdb_connector.py:98-155),
+configured from VECTOR_DB_CONTEXT (config.py:65-67).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, dim, seed):
+    rng = np.random.default_rng(seed)
+    c = rng.standard_normal((64, dim)).astype(np.float32)
+    return c[np.arange(n) % 64] + 0.5 * rng.standard_normal((n, dim)).astype(np.float32)
+
+
+def test_sharded_store_equals_single_store():
+    from super_rag_amd.store import NativeStore, ShardedStore
+    dim = 768
+    x = _data(60_000, dim, 1)
+    one, sh = NativeStore(dim), ShardedStore(dim, [0, 0])
+    for s in range(0, 60_000, 7_000):                    # batches alternate between the shards
+        assert one.add(x[s:s + 7000]).tolist() == sh.add(x[s:s + 7000]).tolist()
+    dup = np.repeat(x[3:4], 3, 0)
+    one.add(dup)
+    sh.add(dup)                                          # exact ties in both shards
+    q = _data(33, dim, 2)
+    q[0] = x[3]
+    for k in (1, 10, 100):
+        d1, r1 = one.search(q, k)
+        d2, r2 = sh.search(q, k)                         # device path + topk_merge_dev
+        assert np.array_equal(r1, r2)
+        assert np.array_equal(d1, d2)
+    dead = np.arange(0, 60_003, 5)
+    one.remove(dead)
+    sh.remove(dead)
+    allow = (np.arange(60_003) % 3 != 0).astype(np.uint8)
+    d1, r1 = one.search(q, 50, allow=allow, mask_key=7)
+    d2, r2 = sh.search(q, 50, allow=allow, mask_key=7)   # per-shard masked search, host merge
+    assert np.array_equal(r1, r2) and np.array_equal(d1, d2)
+    assert np.array_equal(one.compact(), sh.compact())
+    d1, r1 = one.search(q, 100)
+    d2, r2 = sh.search(q, 100)
+    assert np.array_equal(r1, r2) and np.array_equal(d1, d2)
+    np.testing.assert_array_equal(one.get(np.arange(100)), sh.get(np.arange(100)))
+    one.close()
+    sh.close()
+
+
+def test_connector_devices_ctx_matches_single_device(tmp_path):
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.models import QueryWithEmbedding, TextNode
+    V._collections.clear()
+    x = _data(5000, 384, 3)
+    single = V.MI355XVectorStoreConnector({"collection": "s1", "device": 0})
+    multi = V.MI355XVectorStoreConnector({"collection": "s2", "devices": [0, 0],
+                                          "snapshot_dir": str(tmp_path)})
+    for con in (single, multi):
+        ids = []
+        for s in range(0, 5000, 600):
+            ids += con.add([TextNode(text=f"doc {i}", metadata={"i": i}, embedding=x[i].tolist())
+                            for i in range(s, min(5000, s + 600))])
+        con.delete(ids=ids[100:160])
+    qs = [QueryWithEmbedding(query="q", top_k=k, embedding=v.tolist())
+          for k, v in zip((1, 8, 64), _data(3, 384, 4))]
+    dump = lambda con: [[(d.text, d.score) for d in con.search(q).results] for q in qs]
+    want = dump(single)
+    assert dump(multi) == want
+    V._collections.clear()
+    again = V.MI355XVectorStoreConnector({"collection": "s2", "devices": [0, 0],
+                                          "snapshot_dir": str(tmp_path)})
+    assert dump(again) == want
+    again.delete_collection()
+    single.delete_collection()
+    V._collections.clear()

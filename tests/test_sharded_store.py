@@ -1,0 +1,98 @@
+"""CPU: a collection row-sharded over several stores (VECTOR_DB_CONTEXT "devices": [...]).
+
+Global row ids follow insertion order across shards, so a sharded collection must return exactly
+what one store returns — same rows, same (distance asc, row asc) order — through adds, deletes,
+compaction, filters and a snapshot round trip (the reference's connector is configured from
+VECTOR_DB_CONTEXT: super_rag/config.py:65-67, vectorstore/connector.py:4-15).  The shards here are
+the NumpyStore doubles (host merge path); tests/test_gpu_store_sharded.py runs the device path.
+"""
+import numpy as np
+import pytest
+
+from doubles import NumpyStore
+
+
+def _pair(P=3, dim=6):
+    from super_rag_amd.store import ShardedStore
+    return NumpyStore(dim), ShardedStore(dim, list(range(P)), factory=lambda d, dev: NumpyStore(d))
+
+
+def test_sharded_equals_single_through_mutations():
+    rng = np.random.default_rng(0)
+    one, sh = _pair()
+    for n in (5, 17, 1, 40, 9, 30):
+        x = rng.standard_normal((n, 6)).astype(np.float32)
+        assert one.add(x).tolist() == sh.add(x).tolist()
+    x = rng.standard_normal((4, 6)).astype(np.float32)
+    one.add(np.repeat(x[:1], 4, 0))          # exact ties across shards: order by global row
+    sh.add(np.repeat(x[:1], 4, 0))
+    assert {int(s) for s in sh.shard_of} == {0, 1, 2}
+    q = rng.standard_normal((7, 6)).astype(np.float32)
+    q[0] = x[0]
+    for k in (1, 5, 30, 200):
+        d1, r1 = one.search(q, k)
+        d2, r2 = sh.search(q, k)
+        assert np.array_equal(r1, r2)
+        np.testing.assert_allclose(d1[r1 >= 0], d2[r2 >= 0], atol=1e-12)
+    dead = np.arange(0, 100, 3)
+    one.remove(dead)
+    sh.remove(dead)
+    assert one.count() == sh.count()
+    allow = (np.arange(106) % 4 != 1).astype(np.uint8)
+    for a in (None, allow):
+        d1, r1 = one.search(q, 12, allow=a) if a is not None else one.search(q, 12)
+        d2, r2 = sh.search(q, 12, allow=a) if a is not None else sh.search(q, 12)
+        assert np.array_equal(r1, r2)
+    m1, m2 = one.compact(), sh.compact()
+    assert np.array_equal(m1, m2)
+    assert np.array_equal(one.search(q, 20)[1], sh.search(q, 20)[1])
+    np.testing.assert_array_equal(one.get(np.arange(10)), sh.get(np.arange(10)))
+
+
+def test_connector_with_devices_matches_one_device_and_restores(tmp_path):
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.models import QueryWithEmbedding, TextNode
+    V.set_store_backend(lambda dim, dev: NumpyStore(dim, dev), NumpyStore.load)
+    V._collections.clear()
+    try:
+        rng = np.random.default_rng(1)
+        vecs = rng.standard_normal((60, 8))
+        one = V.MI355XVectorStoreConnector({"collection": "one"})
+        many = V.MI355XVectorStoreConnector({"collection": "many", "devices": [0, 0, 0],
+                                             "snapshot_dir": str(tmp_path)})
+        ids_m = []
+        for c in (one, many):
+            ids = []
+            for s in range(0, 60, 7):
+                ids += c.add([TextNode(text=f"t{i}", metadata={"i": i}, embedding=vecs[i].tolist())
+                              for i in range(s, min(60, s + 7))])
+            c.delete(ids=ids[5:9])
+            ids_m.append(ids)
+        qs = [QueryWithEmbedding(query="q", top_k=k, embedding=rng.standard_normal(8).tolist())
+              for k in (1, 6, 25)]
+        dump = lambda con: [[(d.text, d.score) for d in con.search(q).results] for q in qs]
+        want = dump(one)
+        assert dump(many) == want
+        V._collections.clear()                                   # restart: sharded snapshot
+        again = V.MI355XVectorStoreConnector({"collection": "many", "devices": [0, 0, 0],
+                                              "snapshot_dir": str(tmp_path)})
+        assert dump(again) == want
+        assert type(V._get("many").store).__name__ == "ShardedStore"
+        V._collections.clear()
+        with pytest.raises(IOError, match="3-shard"):
+            V.MI355XVectorStoreConnector({"collection": "many", "devices": [0, 0],
+                                          "snapshot_dir": str(tmp_path)})
+        V._collections.clear()
+        again = V.MI355XVectorStoreConnector({"collection": "many", "devices": [0, 0, 0],
+                                              "snapshot_dir": str(tmp_path)})
+        again.delete_collection()
+        assert list(tmp_path.iterdir()) == []
+    finally:
+        V._collections.clear()
+        V.set_store_backend(V._native_store, V._native_load)
+
+
+def test_multi_device_fulltext_is_refused():
+    from super_rag_amd import vectorstore as V
+    with pytest.raises(ValueError, match="single-device"):
+        V.MI355XVectorStoreConnector({"collection": "x", "devices": [0, 1], "hybrid": True})
