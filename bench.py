@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--embed-model", default="bge-base-en")
     ap.add_argument("--rerank-model", default="bge-reranker-base")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip recall@10 and the measured peaks (A/B timing runs only)")
     ap.add_argument("--rerank-max-tokens", type=int, default=524288,
                     help="cross-encoder tokens per chunk (workspace ~15 KB per token)")
     ap.add_argument("--cpu-queries", type=int, default=32,
@@ -252,7 +254,7 @@ def main():
 
     # ---- recall@10 of the search stage vs exact fp32 (outside the timed region) -----------------
     recall = None
-    if world == 1:
+    if world == 1 and not a.no_extras:
         ids, mask, _, _ = batches[0]
         nq = min(32, a.batch)
         q16 = embedder.embed_dev(ids[:nq], mask[:nq], fp16=False)
@@ -269,7 +271,7 @@ def main():
         hit = sum(len(set(rows[i].tolist()) & set(best_r[i].tolist())) for i in range(nq))
         recall = hit / (nq * a.k)
 
-    peaks = measured_peaks(dev) if rank == 0 else None
+    peaks = measured_peaks(dev) if rank == 0 and not a.no_extras else None
 
     # ---- fp8 precision modes: final top-10 vs the fp16 reranker on the same candidates -----------
     fp8_fidelity = None

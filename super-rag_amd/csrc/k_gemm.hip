@@ -25,6 +25,10 @@
 #include "sr_common.h"
 #include "sr_kernels.h"
 
+#ifndef SR_GEMM_LINE_STORE
+#define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
+#endif
+
 namespace sr {
 
 namespace {
@@ -104,6 +108,53 @@ __device__ __forceinline__ float gelu2_erf(float x) {
   p *= t;
   const float w = __builtin_amdgcn_exp2f(x * (x * -0.72134752044448170f));  // exp(-x^2 / 2)
   return fmaf(ax, fmaf(-p, w, 1.0f), x);
+}
+
+// The lane id re-read by an asm the compiler may not hoist: epilogue addresses derived from it are
+// recomputed where used instead of being hoisted out of the persistent tile loop (at 256 VGPRs
+// hoisted lane-dependent offsets spill).
+__device__ __forceinline__ int lane_id_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0" : "=v"(l));
+  asm volatile("v_mbcnt_hi_u32_b32 %0, -1, %0" : "+v"(l));
+  return l;
+}
+
+// Packed-fp32 forms of the epilogue math for the wide (8-column) layout: every FMA / MUL / ADD of
+// two neighbouring columns is ONE v_pk_*_f32 (2 lanes of math per issue; the scalar forms issue at
+// half that rate), only the transcendentals stay per element.  Same operations in the same order
+// as gelu_erf / gelu2_erf, so the outputs are bit-identical to the scalar epilogue's.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v splat2(float x) { return f2v{x, x}; }
+
+__device__ __forceinline__ f2v gelu2_erf2(f2v x) {
+  const f2v ax = __builtin_elementwise_abs(x);
+  const f2v d = pk_fma(splat2(0.3275911f * 0.70710678118654752f), ax, splat2(1.0f));
+  const f2v t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f2v p = pk_fma(splat2(1.061405429f), t, splat2(-1.453152027f));
+  p = pk_fma(p, t, splat2(1.421413741f));
+  p = pk_fma(p, t, splat2(-0.284496736f));
+  p = pk_fma(p, t, splat2(0.254829592f));
+  p *= t;
+  const f2v e = x * (x * splat2(-0.72134752044448170f));
+  const f2v w = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  return pk_fma(ax, pk_fma(-p, w, splat2(1.0f)), x);
+}
+
+__device__ __forceinline__ f2v gelu_erf2(f2v x) {
+  const f2v z = __builtin_elementwise_abs(x) * splat2(0.70710678118654752f);
+  const f2v d = pk_fma(splat2(0.3275911f), z, splat2(1.0f));
+  const f2v t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f2v p = pk_fma(splat2(1.061405429f), t, splat2(-1.453152027f));
+  p = pk_fma(p, t, splat2(1.421413741f));
+  p = pk_fma(p, t, splat2(-0.284496736f));
+  p = pk_fma(p, t, splat2(0.254829592f));
+  p *= t;
+  const f2v zz = -z * z;
+  const f2v e = splat2(1.0f) - p * f2v{__expf(zz.x), __expf(zz.y)};
+  const f2v s = {copysignf(e.x, x.x), copysignf(e.y, x.y)};
+  return splat2(0.5f) * x * (splat2(1.0f) + s);
 }
 
 // Epilogue: lane owns D[n = nw0 + 16i + 4(lane>>4) + r][m = mw0 + 16j + (lane&15)] of the wave's
@@ -219,12 +270,12 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
 // from mr (launch_ln_stats_finalize of the producer's partials).  The *_STATS epilogues write the
 // Chan partials of their own fp16-rounded outputs: per 128-column wave span the sum over the 4
 // lane groups (xor-shuffles 16 / 32), then M2 around that span's mean.
-template <int EPI, bool CHECK>
+template <int EPI, bool CHECK, bool LINE_ST = false>
 __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, int mw0, int lane,
                                                 int M, int N, const float* __restrict__ bias,
                                                 const void* __restrict__ R, int64_t ldr,
                                                 void* __restrict__ Y, int64_t ldy,
-                                                const LnFold& lf) {
+                                                const LnFold& lf, half_t* __restrict__ scr = nullptr) {
   constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;  // e4m3 bytes instead of fp16
   constexpr bool Y8 = EPI == EPI_RES16_STATS_Y8 || EPI == EPI_LNR16_STATS_Y8;  // + e4m3 copy
   constexpr bool LNF = EPI == EPI_LNF_F16 || EPI == EPI_LNF_GELU_F16 || OUT8;
@@ -233,6 +284,15 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   constexpr bool STATS = (RESN && EPI != EPI_BIAS_RES_F16) || LNR;
   constexpr bool GELU = EPI == EPI_BIAS_GELU_F16;
   constexpr bool GELU2 = EPI == EPI_LNF_GELU_F16 || OUT8;  // stores 2 * GELU (consumer weight halved)
+  // packed fp32 math (f2v) for the LN-folded / GELU epilogues; the residual + statistics
+  // epilogues keep the scalar form (packing them raised EPI_LNR16_STATS's spills 12 -> 112 B)
+  constexpr bool PACK = !(RESN || LNR);
+  // LINE: the fp16 rows of a 16-row group go through the wave's 4 KiB LDS scratch `scr` and leave
+  // as whole 256-B row segments (4 rows x 256 B per store instruction) instead of 16 rows x 64 B:
+  // 71 vs 19 B/clk of store throughput per CU (tools/diag/store_rate.hip)
+  // (not for the GELU epilogues: there the exchange measured slower, FFN1 932 -> 881 TF/s, while
+  // QKV gained 1005 -> 1044 and the residual + statistics GEMMs 1072 -> 1078, ab_line3)
+  constexpr bool LINE = LINE_ST && !OUT8 && !Y8 && !GELU && !GELU2;
   static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
@@ -263,10 +323,22 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int m = mw0 + j * 16 + (lane & 15);
-    if (CHECK && m >= M) continue;
+    const int m_row = mw0 + j * 16 + (lane & 15);
+    // LINE: every lane takes part in the scratch exchange; rows past M compute on row M - 1's
+    // operands and are never stored
+    if (!LINE && CHECK && m_row >= M) continue;
+    const int m = (LINE && CHECK && m_row >= M) ? M - 1 : m_row;
     half8 r16[(RESN || LNR) ? 4 : 1];
-    if constexpr (RESN || LNR) {
+    if constexpr ((RESN || LNR) && LINE) {
+      // residual row segments at offsets re-derived from the lane id where used (no hoisted
+      // per-lane 64-bit addresses: they spill at 256 VGPRs); m is clamped to row M - 1
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int ln = lane_id_here(), gl = ln >> 4;
+        r16[p] = *reinterpret_cast<const half8*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr +
+                                                 nw0 + 16 * (gl & 1) + 4 * (gl & 2) + 32 * p);
+      }
+    } else if constexpr (RESN || LNR) {
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         r16[p] = *reinterpret_cast<const half8*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr + nlane + 32 * p);
@@ -277,6 +349,79 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       rstd = mrj[j].y;
     }
     half8 hv[4];
+    if constexpr (PACK) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // columns nb .. nb+7 as 4 packed pairs: x[q] = (col 2q, col 2q + 1)
+      f2v x[4];
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const auto s0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                         __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r + 1]),
+                                                         __float_as_uint(acc[2 * p + 1][j][r + 1]), false, false);
+        x[r / 2] = f2v{__uint_as_float(s0[0]), __uint_as_float(s1[0])};
+        x[2 + r / 2] = f2v{__uint_as_float(s0[1]), __uint_as_float(s1[1])};
+      }
+      const f2v bb[4] = {b0[p].xy, b0[p].zw, b1[p].xy, b1[p].zw};
+      if constexpr (LNF) {
+        const f2v cc[4] = {c0[p].xy, c0[p].zw, c1[p].xy, c1[p].zw};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          x[q] = pk_fma(splat2(rstd), pk_fma(splat2(-mu), cc[q], x[q]), bb[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] += bb[q];
+      }
+      if constexpr (RESN) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] += f2v{(float)r16[p][2 * q], (float)r16[p][2 * q + 1]};
+      }
+      if constexpr (LNR) {
+        const f2v cc[4] = {c0[p].xy, c0[p].zw, c1[p].xy, c1[p].zw};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f2v rn = (f2v{(float)r16[p][2 * q], (float)r16[p][2 * q + 1]} - splat2(mu)) * splat2(rstd);
+          x[q] = pk_fma(rn, cc[q], x[q]);
+        }
+      }
+      if constexpr (GELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = gelu_erf2(x[q]);
+      }
+      if constexpr (GELU2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = gelu2_erf2(x[q]);
+      }
+      if constexpr (OUT8) {
+        uint2 q8;
+        q8.x = e4m3x4(x[0].x, x[0].y, x[1].x, x[1].y);
+        q8.y = e4m3x4(x[2].x, x[2].y, x[3].x, x[3].y);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          hv[p][2 * q] = (half_t)x[q].x;
+          hv[p][2 * q + 1] = (half_t)x[q].y;
+        }
+        if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
+          const int ln = lane_id_here(), gl = ln >> 4;
+          *reinterpret_cast<half8*>(scr + (ln & 15) * 128 +
+                                    (((4 * p + 2 * (gl & 1) + ((gl >> 1) & 1)) ^ (ln & 15)) << 3)) = hv[p];
+        }
+        else
+          *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
+        if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+          {
+            uint2 q8;
+            q8.x = e4m3x4((float)hv[p][0], (float)hv[p][1], (float)hv[p][2], (float)hv[p][3]);
+            q8.y = e4m3x4((float)hv[p][4], (float)hv[p][5], (float)hv[p][6], (float)hv[p][7]);
+            *reinterpret_cast<uint2*>(lf.y8 + (int64_t)m * ldy + nlane + 32 * p) = q8;
+          }
+        }
+      }
+    }
+    } else {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       float v[8];
@@ -327,7 +472,13 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
-        *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
+        if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
+          const int ln = lane_id_here(), gl = ln >> 4;
+          *reinterpret_cast<half8*>(scr + (ln & 15) * 128 +
+                                    (((4 * p + 2 * (gl & 1) + ((gl >> 1) & 1)) ^ (ln & 15)) << 3)) = hv[p];
+        }
+        else
+          *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
         if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
           {
             uint2 q8;
@@ -336,6 +487,20 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
             *reinterpret_cast<uint2*>(lf.y8 + (int64_t)m * ldy + nlane + 32 * p) = q8;
           }
         }
+      }
+    }
+    }
+    if constexpr (LINE) {
+      // the row group's 16 x 128 columns were written to the scratch (chunk c of row r at
+      // c ^ r: conflict-free b128 writes and reads); read back as rows 4q + (lane >> 4), chunk
+      // lane & 15, so each store instruction writes 4 whole 256-B row segments
+      half_t* const yw = reinterpret_cast<half_t*>(Y) + (int64_t)(mw0 + j * 16) * ldy + nw0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ln = lane_id_here(), c = ln & 15, rr = 4 * q + (ln >> 4);
+        const half8 o = *reinterpret_cast<const half8*>(scr + rr * 128 + ((c ^ rr) << 3));
+        if (!CHECK || mw0 + j * 16 + rr < M)
+          *reinterpret_cast<half8*>(yw + (int64_t)rr * ldy + c * 8) = o;
       }
     }
     if constexpr (STATS) {
@@ -358,7 +523,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         }
       m2 += __shfl_xor(m2, 16, 64);
       m2 += __shfl_xor(m2, 32, 64);
-      if (g == 0) {
+      if (g == 0 && (!CHECK || m_row < M)) {
         float2 st;
         st.x = sum;
         st.y = m2;
@@ -375,13 +540,14 @@ template <int EPI>
 struct PipeEpi {
   static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
   static constexpr int NSTORE = WIDE ? 16 : 32;
-  template <bool CHECK>
+  template <bool CHECK, bool LINE = false>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
                                              int N, const float* __restrict__ bias,
                                              const void* __restrict__ R, int64_t ldr,
-                                             void* __restrict__ Y, int64_t ldy, const LnFold& lf) {
+                                             void* __restrict__ Y, int64_t ldy, const LnFold& lf,
+                                             half_t* __restrict__ scr = nullptr) {
     if constexpr (WIDE)
-      store_tile_wide<EPI, CHECK>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf);
+      store_tile_wide<EPI, CHECK, LINE>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr);
     else
       store_tile_fast<EPI, CHECK, 8, 4>(acc, nw0, mw0, lane, M, bias, R, ldr, Y, ldy);
   }
@@ -492,7 +658,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr bool F8 = EPI == EPI_SCAN8 || F8W;
   constexpr bool SCAN = EPI == EPI_SCAN || EPI == EPI_SCAN8;
   constexpr int EPI_OUT = EPI;
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE];
+  // whole-line epilogue stores: a 4 KiB LDS scratch per wave after the two 64 KiB stages (one
+  // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
+  constexpr bool LINE = SR_GEMM_LINE_STORE && PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 &&
+                        EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16;
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0)];
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -530,6 +700,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wm = wave & 3;
+#ifdef SR_GEMM_PRIO_HALF  // experiment: static priority for the second-dispatched half
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   const int nk = K / GBK;
   const int kxs = lf.x_k > 0 ? lf.x_k / GBK : nk;  // K-steps of the X operand (split weights)
   (void)kxs;
@@ -584,6 +757,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
   for (int i = 0; i < 8; ++i) sa[i] = 119;  // the scan: 2^-8 on both operands
 
+  if (PERSIST && lf.stagger > 0) {  // de-phase the walkers of an XCD (their store bursts)
+    const int n_sleep = ((blockIdx.x >> 3) & 7) * lf.stagger;
+    for (int i = 0; i < n_sleep; ++i) __builtin_amdgcn_s_sleep(8);
+  }
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
     stage(0, lds, m0, n0);
@@ -831,11 +1008,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       scan_epilogue(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                     reinterpret_cast<const uint8_t*>(R), reinterpret_cast<uint64_t*>(Y), (int)ldy, lf);
     } else if (full) {
-      PipeEpi<EPI_OUT>::template run<false>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R,
-                                            ldr, Y, ldy, lf);
+      PipeEpi<EPI_OUT>::template run<false, LINE>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                  R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048);
     } else {
-      PipeEpi<EPI_OUT>::template run<true>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R,
-                                           ldr, Y, ldy, lf);
+      PipeEpi<EPI_OUT>::template run<true, LINE>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                 R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048);
     }
     if (!more) break;
     // next tile: K-step 0 (group 0's 16 glds) landed; younger: the epilogue's NSTORE stores
@@ -1390,6 +1567,13 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   }();
   lfv.group_m = group_m_env >= 0 ? group_m_env : (K <= 1024 ? (N >= 2048 ? 8 : 4) : 0);
   lfv.x_k = x_k == K ? 0 : x_k;
+  // de-phasing of the persistent walkers: phase step ~1/16 of a tile (K / 96 x 512 cycles);
+  // SR_GEMM_STAGGER = units of 512 cycles per phase (0 = off)
+  static const int stagger_env = [] {
+    const char* e = std::getenv("SR_GEMM_STAGGER");
+    return e ? std::atoi(e) : -1;
+  }();
+  lfv.stagger = stagger_env >= 0 ? (stagger_env > 0 ? std::max(1, stagger_env * K / 768) : 0) : 0;
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
                                        ldr, Y, ldy, M, N, K, x_k / GBK);
