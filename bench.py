@@ -273,6 +273,11 @@ def main():
 
     peaks = measured_peaks(dev) if rank == 0 and not a.no_extras else None
 
+    # ---- search-only at B = 32 (config 2's query block) on this rank's shard: fp16 and fp8 -----
+    search32 = None
+    if rank == 0 and not a.no_extras and a.workload == "config4":
+        search32 = search_b32(store, centers, N_total, r0, r1, a.dim, dev)
+
     # ---- fp8 precision modes: final top-10 vs the fp16 reranker on the same candidates -----------
     fp8_fidelity = None
     if a.fp8 and world == 1:
@@ -358,6 +363,7 @@ def main():
         **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
         "roofline": roof,
         "search_roofline": search_roof,
+        "search_b32": search32,
         "measured_peaks": peaks,
         "cpu_baseline": cpu,
         "kernels": kern,
@@ -367,6 +373,49 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
+    """K1 + K2 alone for a block of 32 search-only queries (corpus rows + 0.3 noise, seed 3; SURVEY
+    section 8(d)) over this rank's rows: the config-2 query block, HBM-bound.  Reported per scan
+    dtype with the scan kernels' algorithmic HBM rate (rows x row bytes per query block) against
+    the 8 TB/s spec; the fp8 scan reads e4m3 rows (1 B per element) and re-scores exactly in fp16."""
+    from super_rag_amd import _native as N
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    idx = torch.randint(r0, r1, (32,), generator=g, device=dev)
+    q = torch.cat([gen_corpus_chunk(int(i), int(i) + 1, dim, centers, dev) for i in idx.tolist()])
+    q = q + 0.3 * torch.randn(q.shape, generator=g, device=dev)
+    out = {"queries": 32, "k": 10, "rows": r1 - r0, "dim": dim}
+    ref_rows = None
+    for mode in ("fp16", "fp8"):
+        store.set_scan_dtype(mode)
+        _, rows = store.search_dev(q, 10)
+        torch.cuda.synchronize()
+        N.profile_enable(True)
+        N.profile_read()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            store.search_dev(q, 10)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        N.profile_enable(False)
+        prof = N.profile_read()
+        scan = {k: v for k, v in prof.items() if k.startswith("cosine_scan")}
+        sb, sm = sum(v["bytes"] for v in scan.values()), sum(v["total_ms"] for v in scan.values())
+        gbs = sb / (sm * 1e-3) / 1e9
+        out[mode] = {"ms_per_batch": round(dt * 1e3, 3), "qps": round(32 / dt, 1),
+                     "scan_ms": round(sm / reps, 3), "scan_GBps": round(gbs, 1),
+                     "frac": round(gbs / PEAK_HBM_GBS, 4)}
+        if mode == "fp16":
+            ref_rows = rows.cpu()
+        else:
+            r8 = rows.cpu()
+            out["fp8_recall_at_10_vs_fp16"] = round(
+                sum(len(set(r8[i].tolist()) & set(ref_rows[i].tolist())) for i in range(32)) / 320, 4)
+    store.set_scan_dtype("fp16")
+    out["fp8_speedup"] = round(out["fp16"]["ms_per_batch"] / out["fp8"]["ms_per_batch"], 3)
+    return out
 
 
 def measured_peaks(dev):

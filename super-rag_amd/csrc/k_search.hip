@@ -46,7 +46,21 @@ __device__ __forceinline__ half8 lds_frag(const half_t* tile, int row, int chunk
   return *reinterpret_cast<const half8*>(tile + row * SBK + swz_chunk(row, chunk) * 8);
 }
 
-template <int QT, bool DENSE>
+typedef int i8v __attribute__((ext_vector_type(8)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+// fp8 fragment of a 128-byte K-step row (128 e4m3 elements): the lane's chunks c and c + 4 as one
+// 32-byte operand of the block-scaled MFMA (the pairing k_gemm.hip's read_frag8 uses; A and B
+// share the slot -> k map, so the products pair up exactly)
+__device__ __forceinline__ i8v lds_frag8(const half_t* tile, int row, int chunk) {
+  const i4v lo = __builtin_bit_cast(i4v, lds_frag(tile, row, chunk));
+  const i4v hi = __builtin_bit_cast(i4v, lds_frag(tile, row, chunk + 4));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// F8: the rows and queries are OCP e4m3 of 256 x (unit vectors; ldc counts 2-byte units, so a
+// K-step still moves 128-byte rows, now 128 elements); E8M0 block scales 2^-8 on both operands
+// undo the staging factor inside v_mfma_scale_f32_16x16x128_f8f6f4: sims are plain cosines.
+template <int QT, bool DENSE, bool F8 = false>
 __global__ __launch_bounds__(STHREADS, 1) void cosine_scan_kernel(
     const half_t* __restrict__ corpus, int64_t ldc, const uint8_t* __restrict__ live, int64_t r0,
     int64_t r1, const half_t* __restrict__ Q, int B, const float* __restrict__ tau,
@@ -86,6 +100,20 @@ __global__ __launch_bounds__(STHREADS, 1) void cosine_scan_kernel(
     if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
     const half_t* C = lds + cur * STAGE;
     const half_t* Qs = C + SROWS * SBK;
+    if constexpr (F8) {
+      const int c0 = lane >> 4;
+      i8v a[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) a[rt] = lds_frag8(C, wave * 32 + rt * 16 + (lane & 15), c0);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const i8v b = lds_frag8(Qs, qt * 16 + (lane & 15), c0);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          acc[rt][qt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[rt], b, acc[rt][qt], 0, 0,
+                                                                           0, 119, 0, 119);
+      }
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int chunk = (lane >> 4) + 4 * s;
@@ -99,6 +127,7 @@ __global__ __launch_bounds__(STHREADS, 1) void cosine_scan_kernel(
         for (int rt = 0; rt < 2; ++rt)
           acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], b, acc[rt][qt], 0, 0, 0);
       }
+    }
     }
     __syncthreads();
   }
@@ -288,15 +317,15 @@ __global__ __launch_bounds__(256) void rerank_select_kernel(const float* __restr
 // ------------------------------------------------------------------------------------------------
 // Host launchers
 
-template <int QT>
+template <int QT, bool F8 = false>
 static void scan_qt(bool dense, dim3 grid, hipStream_t s, const half_t* corpus, int64_t ldc,
                     const uint8_t* live, int64_t r0, int64_t r1, const half_t* Q, int B,
                     const float* tau, uint64_t* cand, int* cnt, int cap) {
   if (dense)
-    hipLaunchKernelGGL((cosine_scan_kernel<QT, true>), grid, dim3(STHREADS), 0, s, corpus, ldc,
+    hipLaunchKernelGGL((cosine_scan_kernel<QT, true, F8>), grid, dim3(STHREADS), 0, s, corpus, ldc,
                        live, r0, r1, Q, B, tau, cand, cnt, cap);
   else
-    hipLaunchKernelGGL((cosine_scan_kernel<QT, false>), grid, dim3(STHREADS), 0, s, corpus, ldc,
+    hipLaunchKernelGGL((cosine_scan_kernel<QT, false, F8>), grid, dim3(STHREADS), 0, s, corpus, ldc,
                        live, r0, r1, Q, B, tau, cand, cnt, cap);
 }
 
@@ -333,6 +362,32 @@ void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uin
     case 4: scan_qt<4>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
     case 8: scan_qt<8>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
     default: scan_qt<16>(dense, grid, s, corpus, ldc, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+  }
+  SR_LAUNCH_CHECK();
+}
+
+// fp8 K1 for up to 64 queries: the small-block kernel above on e4m3 rows (the 256 x 256 GEMM
+// main loop, launch_cosine_scan_gemm8, computes 256 query columns whatever B is: at B = 32 seven
+// eighths of its MFMA work were padding).  ld8 = row bytes (multiple of 128); same contract as
+// launch_cosine_scan (dense: every row's key at position row - r0, no atomics).
+void launch_cosine_scan8(bool dense, const uint8_t* corpus8, int64_t ld8, const uint8_t* live,
+                         int64_t r0, int64_t r1, const uint8_t* Q8, int B, const float* tau,
+                         uint64_t* cand, int* cnt, int cap, hipStream_t s) {
+  SR_CHECK(B > 0 && B <= 64, "cosine_scan8: 1..64 queries per launch");
+  SR_CHECK(ld8 % 128 == 0, "cosine_scan8: row bytes must be a multiple of 128");
+  if (r1 <= r0) return;
+  SR_CHECK(!dense || r1 - r0 <= cap, "cosine_scan8: dense chunk larger than the candidate list");
+  const dim3 grid((unsigned)ceil_div(r1 - r0, SROWS));
+  const double rows = (double)(r1 - r0);
+  ProfScope prof(dense ? "cosine_scan8_dense" : "cosine_scan8", s, 2.0 * rows * ld8 * B,
+                 rows * ld8 + (double)B * ld8 + (dense ? rows * B * 8.0 : 0.0));
+  const half_t* C = reinterpret_cast<const half_t*>(corpus8);
+  const half_t* Q = reinterpret_cast<const half_t*>(Q8);
+  const int64_t ld = ld8 / 2;  // staging in 2-byte units: 64 per 128-byte K-step
+  switch (scan_query_tiles(B)) {
+    case 1: scan_qt<1, true>(dense, grid, s, C, ld, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+    case 2: scan_qt<2, true>(dense, grid, s, C, ld, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
+    default: scan_qt<4, true>(dense, grid, s, C, ld, live, r0, r1, Q, B, tau, cand, cnt, cap); break;
   }
   SR_LAUNCH_CHECK();
 }

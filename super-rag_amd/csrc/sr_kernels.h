@@ -89,6 +89,10 @@ void launch_quantize_rows_fp8(const half_t* W, int N, int K, uint8_t* W8, uint8_
 void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t* live, int64_t r0,
                               int64_t r1, const uint8_t* Q8, int B, const float* tau, uint64_t* cand,
                               int* cnt, int cap, hipStream_t s);
+// fp8 K1 for B <= 64 (k_search.hip): the small-block scan kernel on e4m3 rows (ld8 bytes each)
+void launch_cosine_scan8(bool dense, const uint8_t* corpus8, int64_t ld8, const uint8_t* live,
+                         int64_t r0, int64_t r1, const uint8_t* Q8, int B, const float* tau,
+                         uint64_t* cand, int* cnt, int cap, hipStream_t s);
 void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* live, int64_t r0,
                              int64_t r1, const half_t* Q, int B, const float* tau, uint64_t* cand,
                              int* cnt, int cap, hipStream_t s);

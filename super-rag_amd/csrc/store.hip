@@ -281,17 +281,30 @@ void Store::search_block8(const half_t* qn, int B, int k, float* out_sim, int64_
   if (n == 0) {
     launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, true, asim, arow, 0, s, live);
   } else {
+    // B <= 128: the small-block fp8 kernel (dense first chunk, then threshold chunks); larger
+    // blocks: the 256 x 256 fp8 GEMM main loop (its first chunk in threshold mode at tau = -inf)
+    const bool small = B <= 64;   // (at 128 queries the GEMM main loop is faster: 4.4 ms vs ~3.7)
     const int64_t dense = std::min<int64_t>(n, safe ? (int64_t)(cap - kk) : kDenseRows);
-    launch_cosine_scan_gemm8(corpus8_.as<uint8_t>(), ld8(), live, 0, dense, q8, B, tau, cand, cnt,
-                             cap, s);
+    if (small) {
+      launch_cosine_scan8(true, corpus8_.as<uint8_t>(), ld8(), live, 0, dense, q8, B, tau, cand,
+                          cnt, cap, s);
+      launch_fill_int(cnt, B, (int)dense, s);
+    } else {
+      launch_cosine_scan_gemm8(corpus8_.as<uint8_t>(), ld8(), live, 0, dense, q8, B, tau, cand, cnt,
+                               cap, s);
+    }
     launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, dense == n, asim, arow, 0, s, live);
     const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(8, (cap - kk) / (2 * kk)));
     int64_t r = dense;
     while (r < n) {
       const int64_t step = safe ? (int64_t)(cap - kk) : std::max<int64_t>(r * growth, kDenseRows);
       const int64_t next = std::min(n, r + step);
-      launch_cosine_scan_gemm8(corpus8_.as<uint8_t>(), ld8(), live, r, next, q8, B, tau, cand, cnt,
-                               cap, s);
+      if (small)
+        launch_cosine_scan8(false, corpus8_.as<uint8_t>(), ld8(), live, r, next, q8, B, tau, cand,
+                            cnt, cap, s);
+      else
+        launch_cosine_scan_gemm8(corpus8_.as<uint8_t>(), ld8(), live, r, next, q8, B, tau, cand, cnt,
+                                 cap, s);
       launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, next == n, asim, arow, 0, s, live);
       r = next;
     }

@@ -241,7 +241,8 @@ def test_masked_search_k_best_eligible_rows():
         s.search(q, 10, allow=allow[:-1])
 
 
-@pytest.mark.parametrize("dim,B,k", [(768, 256, 10), (1024, 64, 100), (100, 7, 5), (64, 300, 1)])
+@pytest.mark.parametrize("dim,B,k", [(768, 256, 10), (1024, 64, 100), (100, 7, 5), (64, 300, 1),
+                                     (768, 32, 10), (384, 128, 20), (1024, 16, 1)])
 def test_fp8_scan_rescored_matches_fp16(dim, B, k):
     # fp8 scan (block-scaled MFMA on e4m3 rows) + exact fp16 re-scoring of its top max(2k, k+32):
     # the returned rows are the fp16 store's top k (recall), their distances exact fp16 scores.
