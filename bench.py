@@ -578,6 +578,14 @@ def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total, e
         if i % 4 == 3 or i == nq - 1:
             log(f"rerank {i + 1}/{nq} queries: {t_rerank:.1f} s")
     per_q = {"embed": t_embed / nq, "search": t_search / q.shape[0], "rerank": t_rerank / nq}
+    # (iv) the reference flow's own host-side orchestration per query (NodeflowEngine + runners,
+    # constant-time stub backends), measured in the build container by tools/ref_orchestration.py
+    orch = None
+    orch_path = os.path.join(ROOT, "profiles", "r02_reference_orchestration.json")
+    if os.path.exists(orch_path):
+        with open(orch_path) as f:
+            orch = json.load(f)
+        per_q["orchestration"] = float(orch["value"])
     total = sum(per_q.values())
     return {"value": round(1.0 / total, 4), "unit": "queries/s", "cores": threads, "kind": "port",
             "sample": (f"oracle (torch-CPU fp32) on {threads} threads, no extrapolation: embed "
@@ -589,7 +597,9 @@ def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total, e
             "stage_s_per_query": {k: round(v, 5) for k, v in per_q.items()},
             "stage_qps": {k: round(1.0 / v, 3) for k, v in per_q.items()},
             "stage_s_total": {"embed": round(t_embed, 3), "search": round(t_search, 3),
-                              "rerank": round(t_rerank, 3)}}
+                              "rerank": round(t_rerank, 3)},
+            "orchestration_source": (f"{os.path.relpath(orch_path, ROOT)} ({orch['method']}; "
+                                     f"{orch['note']})") if orch else None}
 
 
 if __name__ == "__main__":
