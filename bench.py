@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip recall@10 and the measured peaks (A/B timing runs only)")
-    ap.add_argument("--rerank-max-tokens", type=int, default=524288,
-                    help="cross-encoder tokens per chunk (workspace ~15 KB per token)")
+    ap.add_argument("--rerank-max-tokens", type=int, default=1638400,
+                    help="cross-encoder tokens per chunk (workspace ~15 KB per token; 1,638,400 = "
+                         "2 chunks per step: +0.8 %% over 524,288, profiles/r02_ab_chunks.log)")
     ap.add_argument("--cpu-queries", type=int, default=32,
                     help="cpu_baseline: queries embedded and reranked (100 pairs each) on the host")
     ap.add_argument("--cpu-search-rows", type=int, default=0,
