@@ -727,6 +727,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // buffer-resource type through its signature: hipcc then drops the host stubs of this template)
   auto stage = [&](int kt, half_t* s, int mm, int nn) {
 #if defined(__HIP_DEVICE_COMPILE__)
+#ifdef SR_GEMM_DIAG_L2ONLY  // experiment: the no-epilogue diagnostic stages tile (0, 0) only
+    if (DIAG == 2) mm = nn = 0;
+#endif
     const auto rw = panel_rsrc(W + (int64_t)nn * K, (int64_t)(N - nn < BN ? N - nn : BN) * K * 2);
     const auto rx = panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2);
     // row-group offsets advanced in place (an opaque running value: precomputed per piece and
