@@ -20,6 +20,8 @@
 // Workgroups are remapped so each XCD owns a contiguous range of tiles, n fastest: the X panel
 // of an m-tile is read from HBM once per XCD and re-served from that XCD's L2.
 #include <cstdlib>
+#include <string>
+#include <vector>
 #include <type_traits>
 
 #include "sr_common.h"
@@ -1564,11 +1566,29 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   // Short-K GEMMs (K <= 1024: QKV, FFN1, O-proj) walk groups of 8 (N >= 2048) or 4 m-panels;
   // FFN2 (K = 3072) stays n fastest.  Same-box A/B of the full bench: 422.8 / 424.0 -> 429.8 /
   // 431.0 q/s (profiles/r01_gemm_group_m.log).  SR_GEMM_GROUP_M overrides (diagnostic).
-  static const int group_m_env = [] {
+  // (diagnostic) SR_GEMM_GROUP_M = "G" for every shape, or "N:G,N:G,..." per output width N
+  static const std::vector<std::pair<int, int>> group_m_env = [] {
+    std::vector<std::pair<int, int>> v;
     const char* e = std::getenv("SR_GEMM_GROUP_M");
-    return e ? std::atoi(e) : -1;
+    if (!e) return v;
+    std::string str(e);
+    if (str.find(':') == std::string::npos) {
+      v.emplace_back(-1, std::atoi(e));
+      return v;
+    }
+    size_t pos = 0;
+    while (pos < str.size()) {
+      const size_t end = std::min(str.find(',', pos), str.size());
+      const std::string item = str.substr(pos, end - pos);
+      const size_t c = item.find(':');
+      if (c != std::string::npos) v.emplace_back(std::atoi(item.c_str()), std::atoi(item.c_str() + c + 1));
+      pos = end + 1;
+    }
+    return v;
   }();
-  lfv.group_m = group_m_env >= 0 ? group_m_env : (K <= 1024 ? (N >= 2048 ? 8 : 4) : 0);
+  lfv.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;
+  for (const auto& [n_env, g_env] : group_m_env)
+    if (n_env < 0 || n_env == N) lfv.group_m = g_env;
   lfv.x_k = x_k == K ? 0 : x_k;
   // de-phasing of the persistent walkers: phase step ~1/16 of a tile (K / 96 x 512 cycles);
   // SR_GEMM_STAGGER = units of 512 cycles per phase (0 = off)

@@ -40,7 +40,7 @@ class SearchPipeline:
                  passage_tok: torch.Tensor, passage_len: torch.Tensor, k_candidates: int = 100,
                  k_final: int = 10, pair_len: int = 128, shard_offset: int = 0, group=None,
                  merge_fn=topk_merge_dev, lexical=None, k_each: int | None = None,
-                 rank_const: int = 1):
+                 rank_const: int = 1, force_exchange: bool = False):
         self.embedder = embedder
         self.reranker = reranker
         self.store = store
@@ -58,6 +58,9 @@ class SearchPipeline:
         import torch.distributed as dist
         self.world = dist.get_world_size(group) if (group is not None or
                                                      (dist.is_available() and dist.is_initialized())) else 1
+        # force_exchange: run the collectives even in a world of one (the RCCL calls of the
+        # sharded path exercised on a one-GPU box)
+        self.exchange = self.world > 1 or bool(force_exchange)
 
     def embed(self, q_ids: torch.Tensor, q_mask: torch.Tensor) -> torch.Tensor:
         return self.embedder.embed_dev(q_ids, q_mask, fp16=True)
@@ -65,7 +68,7 @@ class SearchPipeline:
     def retrieve(self, q_emb: torch.Tensor):
         """[B, d] fp16 unit queries of this rank -> merged global top-K (sims, rows) [B, K]."""
         B = q_emb.shape[0]
-        if self.world == 1:
+        if not self.exchange:
             return self.store.search_dev(q_emb, self.K, row_offset=self.offset)
         import torch.distributed as dist
         # RCCL moves device tensors; the gloo backend (CPU tests, rehearsals of several ranks on
@@ -100,7 +103,7 @@ class SearchPipeline:
         B = q_emb.shape[0]
         dev = q_emb.device
         ke = self.k_each
-        if self.world == 1:
+        if not self.exchange:
             allq, toks, lens = q_emb, q_tok, q_len
         else:
             import torch.distributed as dist
@@ -117,7 +120,7 @@ class SearchPipeline:
         queries = [t_np[i, :l_np[i]] for i in range(t_np.shape[0])]
         qoff, qterms = query_arrays(queries)
         stats = None
-        if self.world > 1:
+        if self.exchange:
             import torch.distributed as dist
             host = dist.get_backend(self.group) == "gloo"
             terms = np.unique(qterms[: qoff[-1]]).astype(np.int32)
@@ -130,7 +133,7 @@ class SearchPipeline:
         sims, rows = self.store.search_dev(allq, ke, row_offset=self.offset)
         lsc, lrows = self.lexical.search_dev(qoff, qterms, ke, global_stats=stats,
                                              row_offset=self.offset)
-        if self.world > 1:
+        if self.exchange:
             import torch.distributed as dist
             host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda
             sims, rows = self._exchange(sims, rows, B, ke, host, dev)

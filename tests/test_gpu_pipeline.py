@@ -133,7 +133,44 @@ def _sharded_worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-def _run_pipeline(rank, world, sharded=True, hybrid=False):
+def _rccl_worker(port, out_q):
+    # a world of one over the nccl backend (RCCL) with the exchange forced on: the all_gather /
+    # all_to_all / all_reduce calls of the sharded path run on device tensors
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "super-rag_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        res = _run_pipeline(0, 1, force_exchange=True)
+        res_h = _run_pipeline(0, 1, hybrid=True, force_exchange=True)
+        out_q.put((res, res_h))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_world_one_equals_plain_path():
+    import os
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(29500 + os.getpid() % 150, q))
+    p.start()
+    res, res_h = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    plain, plain_h = _run_pipeline(0, 1), _run_pipeline(0, 1, hybrid=True)
+    for got, want in ((res, plain), (res_h, plain_h)):
+        for f in ("rows", "cand_rows", "cand_sims", "logits"):
+            np.testing.assert_array_equal(got[f], want[f])
+
+
+def _run_pipeline(rank, world, sharded=True, hybrid=False, force_exchange=False):
     # rank's B queries; sharded: over rows [r0, r1) of the corpus (shard_offset r0) inside a
     # world-size process group, else over the whole corpus in a single process
     import torch
@@ -168,7 +205,8 @@ def _run_pipeline(rank, world, sharded=True, hybrid=False):
         lex.add([(p_tok[i, :p_len[i]] % 97 + 5).tolist() for i in range(r0, r1)])
         q_tok = q_tok % 97 + 5
     pipe = SearchPipeline(emb, rer, store, t(p_tok), t(p_len), k_candidates=K, k_final=k,
-                          pair_len=S, shard_offset=r0, lexical=lex, k_each=16 if hybrid else None)
+                          pair_len=S, shard_offset=r0, lexical=lex, k_each=16 if hybrid else None,
+                          force_exchange=force_exchange)
     mine = slice(rank * B, (rank + 1) * B)
     res = pipe.run(t(q_ids[mine]), t(np.ones_like(q_ids[mine])), t(q_tok[mine]), t(q_len[mine]))
     torch.cuda.synchronize()
