@@ -168,6 +168,14 @@ bool Encoder::fold_enabled() const {
   return !(e && e[0] == '0');
 }
 
+// K5c (fused QKV projection + attention) for the folded layers at S == 128: opt-in
+// (SR_FUSED_QKV_ATTN=1).  Bit-exact with the QKV GEMM + K5b pair but 2 % slower end to end: its
+// attention phase runs at two waves per SIMD with nothing to overlap.
+static bool fused_qkv_attention_enabled() {
+  const char* e = std::getenv("SR_FUSED_QKV_ATTN");
+  return e && e[0] == '1';
+}
+
 void Encoder::set_fp8(int mode) {
   SR_CHECK(mode >= 0 && mode <= 2, "encoder: fp8 mode must be 0, 1 or 2");
   if (mode) {
@@ -329,11 +337,23 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       float* mA = mrA_.as<float>();
       float* mB = mrB_.as<float>();
       uint8_t* u8 = u8_.as<uint8_t>();
+      // K5c: QKV projection + attention in one kernel (the QKV activation stays in LDS)
+      const bool fuse_qa = fused_qkv_attention_enabled() && fp8_ < 2 && qkv_attention_supported(S, d, H);
       for (size_t l = 0; l < layers_.size(); ++l) {
         const Layer& L = layers_[l];
         const bool last = cls_only && l + 1 == layers_.size();
         const Layer* P = l > 0 ? &layers_[l - 1] : nullptr;
-        if (l == 0) {
+        if (fuse_qa && !last) {
+          LnFold lq;
+          lq.mr = mB;
+          lq.colsum = L.cqkv.as<float>();
+          if (l == 0)
+            launch_qkv_attention(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr,
+                                 cmask, ctx, nb, S, d, H, s);
+          else
+            launch_qkv_attention(EPI_LNF_F16, U, d, L.wqkv_f.as<half_t>(), L.dqkv.as<float>(), &lq,
+                                 cmask, ctx, nb, S, d, H, s);
+        } else if (l == 0) {
           launch_gemm(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
                       3 * d, M, 3 * d, d, s);
         } else if (fp8_ >= 2) {  // A = e4m3 copy of u (written by the previous FFN2)
@@ -363,7 +383,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
                       3 * d, M, 3 * d, d, s, &lq);
         }
         const int Mr = last ? nb : M;
-        launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
+        if (!(fuse_qa && !last)) launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
         // O-projection + residual LN2(l-1)(u) -> u1 (in place, or compact rows) + partials sA
         half_t* Uo = last ? Uc : U;
         LnFold lo;

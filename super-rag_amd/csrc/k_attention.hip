@@ -12,6 +12,8 @@
 // P.V product (O^T = V^T P^T) with a permuted k order (keys 32c+4g+j and 32c+16+4g+j for lane
 // group g), so P never leaves the registers; V is stored transposed in LDS to match.
 // Accumulation and softmax statistics are fp32; P is rounded to fp16 for the MFMA.
+#include <cstdlib>
+
 #include "sr_common.h"
 #include "sr_kernels.h"
 
@@ -504,6 +506,323 @@ void attention64_kernel(
   }
 }
 
+
+// ---- K5c: fused QKV projection + attention (S == 128, d_h == 64; the cross-encoder layers) ------
+// One workgroup per (256-token panel = two sequences, head h): the 256 x 192 tile
+// [Q_h | K_h | V_h] = epi(X . W_h^T) over K = d runs K4's pipelined main loop (LDS-DMA double
+// buffer, XOR-swizzled 128-B rows, four MFMA phases per K-step, the K-step-parity wave group issuing
+// the staging burst); its epilogue (bias, or the LayerNorm fold rstd (acc - mu c) + b') writes the
+// fp16 Q, K, V of the panel into LDS images laid out as K5b's (K / Q: kswz, V: vswz) instead of
+// HBM, and the same 8 waves then run K5b's attention on them (waves 4s .. 4s+3: sequence s,
+// 32 queries each).  The QKV activation never touches HBM: per token 4.6 KB of writes and reads
+// disappear.  Numerics equal the unfused pair bit for bit (same MFMA order per accumulator, same
+// epilogue FMAs, same fp16 rounding, same attention code order).
+constexpr int QA_BM = 256;              // tokens per panel
+constexpr int QA_BN = 192;              // Q_h, K_h, V_h rows of W
+constexpr int QA_STAGE = (QA_BM + QA_BN) * 64;  // halfs per K-step buffer (56 KiB)
+
+__device__ __forceinline__ half8 qa_frag(const half_t* t, int row, int chunk) {
+  return *reinterpret_cast<const half8*>(t + row * 64 + a2_kswz(row, chunk) * 8);
+}
+
+// 12-MFMA phase: R fragment reads spread among the first MFMAs
+#define SR_QA_INTERLEAVE(R)                                                \
+  do {                                                                     \
+    _Pragma("unroll") for (int _r = 0; _r < (R); ++_r) {                   \
+      __builtin_amdgcn_sched_group_barrier(0x008, (R) >= 8 ? 1 : 2, 0);    \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                   \
+    }                                                                      \
+    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);                    \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+  } while (0)
+
+// DIAG (timing experiments only, wrong results): 1 = no K-loop (epilogue + attention on zero
+// accumulators), 2 = no attention (the K-loop and the LDS epilogue only)
+template <bool LNF, int DIAG = 0>
+__global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
+    const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ colsum, const float* __restrict__ mr,
+    const int32_t* __restrict__ mask, half_t* __restrict__ ctx, int M, int d, int heads,
+    float scale_log2) {
+  constexpr int DH = 64;
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * QA_STAGE];
+  __shared__ float kbias[QA_BM];
+  // tile t = (panel, head), head fastest; every XCD walks a contiguous range of tiles so the
+  // 12 heads of a panel share its X rows in that XCD's L2 (and W stays L2-resident)
+  const int panels = (M + QA_BM - 1) / QA_BM, nwg = panels * heads;
+  int t;
+  {
+    const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
+    const int lo = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+    const int hi = lo + q + (xcd < rem ? 1 : 0);
+    t = lo + (blockIdx.x >> 3);
+    if (t >= hi) return;
+  }
+  const int h = t % heads, m0 = (t / heads) * QA_BM;
+  const int K = d, nk = K / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 2, wm = wave & 3, grp = wave >> 2, w4 = wave & 3;
+  const int arow = wn * 96 + (lane & 15), brow = wm * 64 + (lane & 15), c0 = lane >> 4;
+  (void)w4;
+
+  // staging: the 4 waves of group (kt & 1) issue K-step kt: 6 W pieces (8 rows of one of the
+  // Q / K / V segments) + 8 X pieces each
+  uint32_t vbw[2], vbx[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int ch = (lane & 7) ^ ((lane >> 4) + 4 * par);
+    vbw[par] = (uint32_t)(((int64_t)(lane >> 3) * K + ch * 8) * 2);
+    vbx[par] = (uint32_t)(((int64_t)(lane >> 3) * lda + ch * 8) * 2);
+  }
+  auto stage = [&](int kt, half_t* s) __attribute__((always_inline)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto rw = panel_rsrc(W, (int64_t)3 * d * K * 2);
+    const auto rx = panel_rsrc(X + (int64_t)m0 * lda, (int64_t)(M - m0 < QA_BM ? M - m0 : QA_BM) * lda * 2);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int p = w4 * 6 + i;  // rows 8p .. 8p+7 of the tile: segment p >> 3 (Q, K, V)
+      const int grow = (p >> 3) * d + h * DH + 8 * (p & 7);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, SR_LDS(s + p * 8 * 64), 16, vbw[i & 1],
+                                               grow * K * 2 + kt * 128, 0, 0);
+    }
+    int sx = w4 * 8 * 16 * (int)lda + kt * 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      asm volatile("" : "+s"(sx));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, SR_LDS(s + (QA_BN + (w4 * 8 + i) * 8) * 64), 16,
+                                               vbx[i & 1], sx, 0, 0);
+      sx += 16 * (int)lda;
+    }
+#endif
+  };
+
+  float4v acc[6][4];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+  half8 aX[3], aY[3], bX[4], bY[4];
+
+  if (grp == 0) {
+    stage(0, lds);
+    SR_WAITCNT(0, 15);
+  } else if (nk > 1) {
+    stage(1, lds + QA_STAGE);
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 3; ++i) aY[i] = qa_frag(lds, arow + 16 * i, c0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bX[j] = qa_frag(lds + QA_BN * 64, brow + 16 * j, c0);
+
+  for (int kt = 0; kt < (DIAG == 1 ? 0 : nk); ++kt) {
+    half_t* cur = lds + (kt & 1) * QA_STAGE;
+    const half_t* nxt = lds + ((kt + 1) & 1) * QA_STAGE;
+    const half_t* Bc = cur + QA_BN * 64;
+    // p0: A[0..2] x B (k 0..31); reads A[3..5] (k 0..31)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) aX[i] = qa_frag(cur, arow + 16 * (3 + i), c0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bX[j], acc[i][j], 0, 0, 0);
+    SR_QA_INTERLEAVE(3);
+    // p1: A[3..5] x B (k 0..31); reads A[0..2], B (k 32..63)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) aY[i] = qa_frag(cur, arow + 16 * i, c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bY[j] = qa_frag(Bc, brow + 16 * j, c0 + 4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[3 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bX[j], acc[3 + i][j], 0, 0, 0);
+    SR_QA_INTERLEAVE(7);
+    // p2: A[0..2] x B' (k 32..63); reads A[3..5] (k 32..63)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) aX[i] = qa_frag(cur, arow + 16 * (3 + i), c0 + 4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bY[j], acc[i][j], 0, 0, 0);
+    SR_QA_INTERLEAVE(3);
+    SR_WAITCNT(0, 0);  // K-step kt+1 landed (all waves); buffer kt & 1 is no longer read
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk && grp == (kt & 1)) stage(kt + 2, cur);
+    // p3: A[3..5] x B' (k 32..63); reads K-step kt+1's p0 operands
+    const bool rn = kt + 1 < nk;
+    if (rn) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) aY[i] = qa_frag(nxt, arow + 16 * i, c0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bX[j] = qa_frag(nxt + QA_BN * 64, brow + 16 * j, c0);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[3 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bY[j], acc[3 + i][j], 0, 0, 0);
+    if (rn) {
+      SR_QA_INTERLEAVE(7);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---- epilogue -> LDS images (the stages are dead: every wave passed the last barrier after its
+  // final LDS reads, and no staging is in flight) ----
+  half_t* Qi = lds;
+  half_t* Ki = lds + QA_BM * DH;
+  half_t* Vi = lds + 2 * QA_BM * DH;
+  if (tid < QA_BM) {
+    const int m = m0 + tid;
+    kbias[tid] = (m < M && mask[m < M ? m : M - 1] != 0) ? 0.f : -INFINITY;
+  }
+  const int g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int ml = wm * 64 + 16 * j + (lane & 15);
+    const int mg = m0 + ml < M ? m0 + ml : M - 1;
+    float mu = 0.f, rstd = 1.f;
+    if constexpr (LNF) {
+      const float2 v = *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2);
+      mu = v.x;
+      rstd = v.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
+      const int seg = n >> 6, dim = n & 63;
+      const int col = seg * d + h * DH + dim;
+      const float4v b = *reinterpret_cast<const float4v*>(bias + col);
+      half4 y;
+      if constexpr (LNF) {
+        const float4v c = *reinterpret_cast<const float4v*>(colsum + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = (half_t)fmaf(rstd, fmaf(-mu, c[r], acc[i][j][r]), b[r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = (half_t)(acc[i][j][r] + b[r]);
+      }
+      half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
+      const int chunk = seg == 2 ? a2_vswz(ml, dim >> 3) : a2_kswz(ml, dim >> 3);
+      *reinterpret_cast<half4*>(img + ml * DH + chunk * 8 + (dim & 7)) = y;
+    }
+  }
+  __syncthreads();
+
+  // ---- attention: waves 4s .. 4s+3 own sequence s of the panel, 32 queries each ----
+  const int sq = wave >> 2, qw = (wave & 3) * 32;
+  if (m0 + QA_BM / 2 * (sq + 1) > M) return;  // a panel with one sequence (no barrier follows)
+  if constexpr (DIAG == 2) return;
+  const half_t* Qs = Qi + sq * 128 * DH;
+  const half_t* Ks = Ki + sq * 128 * DH;
+  const half_t* Vs = Vi + sq * 128 * DH;
+  const float* kb = kbias + sq * 128;
+  half8 qf[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = qw + 16 * u + (lane & 15);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      qf[u][s2] = *reinterpret_cast<const half8*>(Qs + r * DH + a2_kswz(r, g + 4 * s2) * 8);
+  }
+  float l_run[2] = {0.f, 0.f};
+  float4v o[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
+  {
+    float p[2][8][4];
+    float tmax[2] = {-INFINITY, -INFINITY};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      const int kr = 16 * kt + (lane & 15);
+      const half8 k0f = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+      const half8 k1f = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float4v a = {0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0f, qf[u][0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1f, qf[u][1], a, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = a[r] * scale_log2 + kb[16 * kt + 4 * g + r];
+          p[u][kt][r] = v;
+          tmax[u] = fmaxf(tmax[u], v);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float tm = fmaxf(tmax[u], __shfl_xor(tmax[u], 16, 64));
+      tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      const float m_use = (tm == -INFINITY) ? 0.f : tm;  // (one key block: no rescaling)
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(p[u][kt][r] - m_use);
+          p[u][kt][r] = e;
+          l_run[u] += e;
+        }
+    }
+    // O^T += V^T P^T over 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j)
+    const int q4 = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      half8 pb[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          pb[u][jj] = (half_t)p[u][2 * c][jj];
+          pb[u][4 + jj] = (half_t)p[u][2 * c + 1][jj];
+        }
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        half4 lo, hi;
+        {
+          const int r = 32 * c + 4 * g + q4;
+          lo = tr_read_b64(Vs + r * DH + a2_vswz(r, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
+        }
+        {
+          const int r = 32 * c + 16 + 4 * g + q4;
+          hi = tr_read_b64(Vs + r * DH + a2_vswz(r, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
+        }
+        const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          o[u][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[u], o[u][tt], 0, 0, 0);
+      }
+    }
+  }
+  // normalise and store (permlane16_swap: 8 consecutive dims per lane)
+  const int odd = g & 1;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float l = l_run[u] + __shfl_xor(l_run[u], 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = m0 + sq * 128 + qw + 16 * u + (lane & 15);
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      half8 hv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[u][2 * p2][r]),
+                                                         __float_as_uint(o[u][2 * p2 + 1][r]), false, false);
+        hv[r] = (half_t)(__uint_as_float(sw[0]) * inv);
+        hv[4 + r] = (half_t)(__uint_as_float(sw[1]) * inv);
+      }
+      *reinterpret_cast<half8*>(ctx + (int64_t)q * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2)) = hv;
+    }
+  }
+}
 }  // namespace
 
 static int g_attn_variant = -1;  // test hook: -1 auto, 0 = K5 (64-key tiles), 1 = K5b (4 waves), 2 = K5b with 8 waves
@@ -551,6 +870,47 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
       hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, stream, qkv, mask, ctx, S, Sq, d,
                          scale_log2);
   }
+  SR_LAUNCH_CHECK();
+}
+
+
+bool qkv_attention_supported(int S, int d, int heads) {
+  return S == 128 && heads > 0 && d == heads * 64 && d % 64 == 0;
+}
+
+void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
+                          const LnFold* lf, const int32_t* mask, half_t* ctx, int B, int S, int d,
+                          int heads, hipStream_t stream) {
+  SR_CHECK(qkv_attention_supported(S, d, heads), "qkv_attention: needs S == 128 and d_h == 64");
+  SR_CHECK(epi == EPI_BIAS_F16 || (epi == EPI_LNF_F16 && lf && lf->mr && lf->colsum && lf->stat_ld == 1),
+           "qkv_attention: epilogue EPI_BIAS_F16 or EPI_LNF_F16 (row statistics + column sums)");
+  SR_CHECK(lda >= d && lda % 8 == 0, "qkv_attention: lda must be >= d and a multiple of 8");
+  if (B <= 0) return;
+  const int64_t M = (int64_t)B * S;
+  SR_CHECK(M < (1ll << 31) / 3, "qkv_attention: too many tokens");
+  const double flops = 2.0 * M * 3.0 * d * d + 4.0 * B * heads * (double)S * S * 64;
+  const double bytes = 2.0 * M * d * 2 + 2.0 * 3 * d * (double)d + 4.0 * M;
+  ProfScope prof("qkv_attention", stream, flops, bytes);
+  const float scale_log2 = 1.4426950408889634f / 8.0f;
+  const int64_t tiles = ceil_div(M, 256) * heads;
+  SR_CHECK(tiles < (1ll << 31), "qkv_attention: too many tiles");
+  const dim3 grid((unsigned)tiles), block(512);
+  static const int diag = [] {
+    const char* e = std::getenv("SR_QA_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (epi == EPI_LNF_F16 && diag == 1)
+    hipLaunchKernelGGL((qkv_attn_kernel<true, 1>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
+  else if (epi == EPI_LNF_F16 && diag == 2)
+    hipLaunchKernelGGL((qkv_attn_kernel<true, 2>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
+  else if (epi == EPI_LNF_F16)
+    hipLaunchKernelGGL(qkv_attn_kernel<true>, grid, block, 0, stream, X, lda, W, bias, lf->colsum,
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
+  else
+    hipLaunchKernelGGL(qkv_attn_kernel<false>, grid, block, 0, stream, X, lda, W, bias, nullptr,
+                       nullptr, mask, ctx, (int)M, d, heads, scale_log2);
   SR_LAUNCH_CHECK();
 }
 

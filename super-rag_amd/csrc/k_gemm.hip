@@ -590,13 +590,9 @@ __device__ __forceinline__ void scan_epilogue(float4v (&acc)[8][4], int nw0, int
   }
 }
 
-// Buffer-resource LDS-DMA staging (buffer_load_dwordx4 ... lds): the tile's panel base lives in
-// the SGPR descriptor, the K offset in soffset, so a lane keeps ONE 32-bit VGPR offset per
-// instruction for the whole kernel; rows past num_records read as zero (no clamp needed).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t panel_rsrc(const half_t* base, int64_t bytes) {
-  const int nr = bytes > 0x7fffffffLL ? 0x7fffffff : (int)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nr, 0x00020000);
-}
+// Buffer-resource LDS-DMA staging (buffer_load_dwordx4 ... lds, panel_rsrc in sr_common.h): the
+// tile's panel base lives in the SGPR descriptor, the K offset in soffset, so a lane keeps ONE
+// 32-bit VGPR offset per instruction for the whole kernel; rows past num_records read as zero.
 template <int NI>
 __device__ __forceinline__ void stage_buf(__amdgpu_buffer_rsrc_t rs, const uint32_t (&voff)[NI],
                                           int soff, half_t* lds_tile, int wave) {

@@ -62,6 +62,13 @@ static inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b
 // Device pointer helpers for LDS address space.
 #define SR_LDS(p) ((__attribute__((address_space(3))) void*)(p))
 
+// Buffer resource over `bytes` bytes from `base` (raw buffer: offsets past num_records read as
+// zero), for buffer_load ... lds staging with the panel base in SGPRs.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t panel_rsrc(const half_t* base, int64_t bytes) {
+  const int nr = bytes > 0x7fffffffLL ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nr, 0x00020000);
+}
+
 // s_waitcnt through the builtin (the compiler's own waitcnt pass then knows the counters are
 // satisfied; an asm waitcnt is invisible to it and it re-waits conservatively). gfx9 encoding:
 // vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
