@@ -14,9 +14,21 @@ from .tokenizer import Tokenizer
 
 _lock = threading.Lock()
 _models: dict = {}
+_next = [0]
 
 
 def default_device() -> int:
+    """SUPER_RAG_AMD_DEVICES="0,1,..." places model replicas on those GPUs, one device per call in
+    turn (the reference builds a service object per request, so requests spread over the GPUs);
+    else SUPER_RAG_AMD_DEVICE (default 0)."""
+    devs = os.environ.get("SUPER_RAG_AMD_DEVICES", "").strip()
+    if devs:
+        ids = [int(x) for x in devs.split(",") if x.strip()]
+        if ids:
+            with _lock:
+                i = _next[0] % len(ids)
+                _next[0] += 1
+            return ids[i]
     return int(os.environ.get("SUPER_RAG_AMD_DEVICE", "0"))
 
 
