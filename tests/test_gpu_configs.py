@@ -208,6 +208,32 @@ def test_config4_10m_b256_recall_and_full_step():
     _free()
 
 
+def test_config4_reranker_full_chunk_batch_invariance():
+    """The bench's reranker chunk: 12,800 pairs x 128 tokens = 1,638,400 tokens in one persistent-GEMM
+    launch per layer.  Every stage is row- or sequence-local, so the logits of a 400-pair subset
+    computed inside the full chunk equal the subset's own launch bit for bit (a tile-walk or
+    hand-over fault at 6,400 tiles would break this); four of them against the oracle."""
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    rs = MODELS["bge-reranker-base"]
+    w = random_weights(rs, 12, "hf")
+    rer = Encoder(rs, weights=w, max_tokens=1_638_400)
+    rng = np.random.default_rng(9)
+    B, S = 12_800, 128
+    ids = rng.integers(1000, rs.vocab_size, (B, S)).astype(np.int32)
+    lens = rng.integers(96, S + 1, B)
+    mask = (np.arange(S)[None] < lens[:, None]).astype(np.int32)
+    ids[:, 0] = rs.bos_id
+    ids = np.where(mask == 1, ids, rs.pad_id).astype(np.int32)
+    full = rer.cross_score(ids, mask)[:, 0]
+    pick = np.sort(rng.choice(B, 400, replace=False))[::-1].copy()   # reversed order as well
+    sub = rer.cross_score(ids[pick], mask[pick])[:, 0]
+    np.testing.assert_array_equal(full[pick], sub)
+    ref = R.cross_logits(ref_config(rs), w, ids[pick[:4]], mask[pick[:4]])[:, 0]
+    assert np.abs(sub[:4] - ref).max() <= RERANK_TOL
+    rer.close()
+    _free()
+
+
 @pytest.mark.parametrize("B,S", [(8, 32), (1, 8192)])
 def test_config5_bge_m3_24_layers(B, S, fp32_highest):
     import torch
