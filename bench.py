@@ -331,6 +331,14 @@ def main():
                        "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
         search_roof["traffic"], search_roof["traffic_source"] = pmc_traffic("cosine_scan")
+        # at B = 256 the scan's intensity (2 B flop per row byte) sits at the ridge: its ceiling is
+        # the slower of the HBM time and the MFMA time at spec peak
+        mfma_s = sum(v["flops"] / ((PEAK_F8_TFLOPS if k.startswith("cosine_scan8") else PEAK_F16_TFLOPS) * 1e12)
+                     for k, v in scan.items())
+        ceil_ms = max(sb / (PEAK_HBM_GBS * 1e9), mfma_s) * 1e3
+        search_roof["ceiling"] = {"ms": round(ceil_ms, 3), "achieved_ms": round(sm, 3),
+                                  "frac": round(ceil_ms / sm, 4),
+                                  "note": "max(bytes / 8 TB/s, flop / MFMA peak (2.5 PF/s f16, 5 PF/s fp8)) over the timed steps"}
     else:
         search_roof = None
 
