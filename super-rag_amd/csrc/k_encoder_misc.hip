@@ -65,6 +65,10 @@ __device__ __forceinline__ void ln_store(float4v (&x)[NV], int n4, const float* 
   }
 }
 
+// NV float4 per lane per row (d <= 256 NV): sized to the model so the unrolled gathers do not hold
+// MAXV x 3 vectors in registers (186 VGPRs = 2 waves per SIMD at MAXV for d = 768; the gather is
+// latency-bound and wants occupancy)
+template <int NV>
 __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int32_t* __restrict__ ids, const int32_t* __restrict__ pos,
     const int32_t* __restrict__ types, const half_t* __restrict__ wemb,
@@ -81,9 +85,9 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
   int t = types ? types[m] : 0;
   t = t < 0 ? 0 : (t >= type_vocab ? type_vocab - 1 : t);
   const int n4 = d >> 2;
-  float4v x[MAXV];
+  float4v x[NV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     if (c < n4) {
       const half4 a = reinterpret_cast<const half4*>(wemb + (int64_t)id * d)[c];
@@ -93,7 +97,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
       for (int j = 0; j < 4; ++j) x[i][j] = (float)a[j] + (float)bp[j] + (float)ct[j];
     }
   }
-  ln_store<MAXV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 ? h32 + m * d : nullptr, lane);
+  ln_store<NV>(x, n4, gamma, beta, eps, d, h16 + m * d, h32 ? h32 + m * d : nullptr, lane);
 }
 
 // y (fp32 or fp16, the GEMM epilogue's bias + residual sum) -> LayerNorm -> h16 (+ h32).
@@ -347,11 +351,16 @@ void launch_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* type
                      int max_pos, int type_vocab, half_t* h16, float* h32, hipStream_t s) {
   SR_CHECK(d % 4 == 0 && d <= 64 * 4 * MAXV, "embed_ln: hidden must be a multiple of 4, <= 2048");
   if (M <= 0) return;
-  // word + position + type rows in (fp16), h16 out, + h32 out for fp32-residual models
-  ProfScope prof("embed_ln", s, 0.0, (double)M * d * (3 * 2 + 2 + (h32 ? 4 : 0)));
-  hipLaunchKernelGGL(embed_ln_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, ids, pos,
-                     types, wemb, pemb, temb, gamma, beta, eps, M, d, vocab, max_pos, type_vocab,
-                     h16, h32);
+  // HBM bytes: the gathered word rows (fp16) and ids / positions / types in, h16 out (+ h32 for
+  // fp32-residual models); the position / type tables are cache-resident
+  ProfScope prof("embed_ln", s, 0.0, (double)M * d * (2 + 2 + (h32 ? 4 : 0)) + 12.0 * M);
+  const int nv = (int)ceil_div(d / 4, 64);
+#define SR_EMB(NV)                                                                                   \
+  hipLaunchKernelGGL((embed_ln_kernel<NV>), dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, ids, pos, \
+                     types, wemb, pemb, temb, gamma, beta, eps, M, d, vocab, max_pos, type_vocab,     \
+                     h16, h32)
+  if (nv <= 2) SR_EMB(2); else if (nv <= 3) SR_EMB(3); else if (nv <= 4) SR_EMB(4); else SR_EMB(MAXV);
+#undef SR_EMB
   SR_LAUNCH_CHECK();
 }
 
