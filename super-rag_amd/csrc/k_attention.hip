@@ -169,6 +169,23 @@ __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict
 constexpr int A2_QB = 128;  // query rows per workgroup
 
 __device__ __forceinline__ int a2_kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// max / sum over the 4 lanes that share lane & 15 (one query's scores): v_permlane16_swap and
+// v_permlane32_swap exchange 16-lane rows in VALU, where __shfl_xor is an LDS round trip; with
+// a == b each result pair holds {own, partner}, so the pair's max / sum is the butterfly step (sums
+// are commutative: bit-identical to the shuffle form)
+__device__ __forceinline__ float rows4_max(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rows4_sum(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 __device__ __forceinline__ int a2_vswz(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
 
 __device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
@@ -399,8 +416,7 @@ void attention64_kernel(
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float tm = fmaxf(tmax[u], __shfl_xor(tmax[u], 16, 64));
-      tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      const float tm = rows4_max(tmax[u]);
       const float m_new = fmaxf(m_run[u], tm);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
       const float alpha = exp2f(m_run[u] - m_use);
@@ -486,8 +502,7 @@ void attention64_kernel(
   const int odd = g & 1;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float l = l_run[u] + __shfl_xor(l_run[u], 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    const float l = rows4_sum(l_run[u]);
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int q = qw + 16 * u + (lane & 15);
 #pragma unroll
@@ -759,8 +774,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float tm = fmaxf(tmax[u], __shfl_xor(tmax[u], 16, 64));
-      tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      const float tm = rows4_max(tmax[u]);
       const float m_use = (tm == -INFINITY) ? 0.f : tm;  // (one key block: no rescaling)
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
@@ -805,8 +819,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
   const int odd = g & 1;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float l = l_run[u] + __shfl_xor(l_run[u], 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    const float l = rows4_sum(l_run[u]);
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int q = m0 + sq * 128 + qw + 16 * u + (lane & 15);
 #pragma unroll
