@@ -27,6 +27,9 @@
 #include "sr_common.h"
 #include "sr_kernels.h"
 
+#ifndef SR_GEMM_LINE_GELU
+#define SR_GEMM_LINE_GELU 0  // whole-line stores for the GELU epilogues too (A/B builds)
+#endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
@@ -294,7 +297,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   // 71 vs 19 B/clk of store throughput per CU (tools/diag/store_rate.hip)
   // (not for the GELU epilogues: there the exchange measured slower, FFN1 932 -> 881 TF/s, while
   // QKV gained 1005 -> 1044 and the residual + statistics GEMMs 1072 -> 1078, ab_line3)
-  constexpr bool LINE = LINE_ST && !OUT8 && !Y8 && !GELU && !GELU2;
+  constexpr bool LINE = LINE_ST && !OUT8 && !Y8 && (SR_GEMM_LINE_GELU || (!GELU && !GELU2));
   static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // whole-line epilogue stores: a 4 KiB LDS scratch per wave after the two 64 KiB stages (one
   // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
   constexpr bool LINE = SR_GEMM_LINE_STORE && PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 &&
-                        EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16;
+                        (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0)];
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
