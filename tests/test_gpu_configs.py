@@ -1,5 +1,7 @@
 """GPU: every BASELINE.json configuration at its own size, on the HIP path.
 
+  config 1  bge-small-en embed of 1k chunks (S = 128) through the ingest path + top-5 through the
+            connector (the reference's CPU plumbing configuration, here on the GPU)
   config 2  1M x 768 corpus, 12-layer bge-base-en embed, B = 32, exact top-10
   config 3  the same corpus + 12-layer bge-reranker-base (XLM-R base) at S_pair = 128, top-100 -> 10
   config 4  10M x 768 corpus, B = 256, top-100 -> rerank -> 10 (one GPU holds the whole corpus)
@@ -101,6 +103,50 @@ def corpus_1m():
     yield store, centers, stored
     store.close()
     _free()
+
+
+def test_config1_bge_small_ingest_1k_chunks_top5():
+    """Config 1: 1,000 chunks of 128 tokens embedded by the 12-layer bge-small-en (d_h = 32: the
+    K5 attention) through VectorIndexer.create_index (index/vector_and_full_text_index.py:29-129)
+    into the connector, then top-5 through MI355XVectorStoreConnector.search
+    (seekdb_connector.py:98-155); embeddings against the oracle on a sample, the top-5 against the
+    fp64 oracle over the rows the store holds."""
+    from types import SimpleNamespace
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.embed import EmbeddingService
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    from super_rag_amd.index import VectorIndexer, chunk_text
+    from super_rag_amd.models import QueryWithEmbedding
+    from super_rag_amd.tokenizer import Tokenizer
+    es = MODELS["bge-small-en"]
+    w = random_weights(es, 31, "hf")
+    tok = Tokenizer(es)
+    svc = EmbeddingService("openai", "BAAI/bge-small-en", "", "", 10, encoder=Encoder(es, weights=w),
+                           tokenizer=tok, device_batch=128)
+    rng = np.random.default_rng(32)
+    words = [f"w{i}" for i in range(5000)]
+    parts = [SimpleNamespace(content=" ".join(rng.choice(words, 126)), metadata={"name": f"c{i}.md"})
+             for i in range(1000)]
+    V._collections.clear()
+    conn = V.MI355XVectorStoreConnector({"collection": "config1", "device": 0})
+    ids = VectorIndexer(conn, svc).create_index(parts)["context_ids"]
+    assert len(ids) == 1000
+    stored = conn.get_vectors(ids)
+    texts = [chunk_text(p).replace("\n", " ") for p in parts]
+    for i in (0, 499, 999):
+        t_ids, t_mask = tok.encode_batch([texts[i]])
+        ref = R.embed(ref_config(es), w, t_ids, t_mask)[0]
+        assert np.linalg.norm(stored[i] - ref) <= 4e-3        # fp16-stored row vs fp32 oracle
+    q = stored[rng.choice(1000, 16, replace=False)] + 0.3 * rng.standard_normal((16, es.hidden)).astype(np.float32)
+    got = [[h.metadata["source"] for h in conn.search(QueryWithEmbedding(query="q", top_k=5,
+                                                                         embedding=v.tolist())).results]
+           for v in q]
+    d_ref, r_ref = cosine_topk(stored, quantize_like_store(q), 5, normalize=False)
+    for b in range(16):
+        want = [f"c{r}.md" for r in r_ref[b]]
+        assert got[b] == want or sorted(got[b]) == sorted(want)   # order modulo exact ties
+    conn.delete_collection()
+    V._collections.clear()
 
 
 def test_config2_bge_base_embed_and_top10_over_1m(corpus_1m):
