@@ -21,6 +21,12 @@ namespace sr {
 
 namespace {
 
+// 2^x on the hardware v_exp_f32 alone: the library exp2f wraps it in a denormal-result range
+// reduction (compare, select, add, ldexp: 6 instructions per score) that softmax does not need (a
+// weight below 2^-126 of the row maximum adds nothing to the fp32 sums; -inf still gives 0)
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+
+
 constexpr int KT = 64;  // keys per tile
 
 template <int DH>
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    const float alpha = exp2_fast(m_run - m_use);
     m_run = m_new;
     l_run *= alpha;
 #pragma unroll
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const half_t* __restrict
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(p[kt][r] - m_use);
+        const float e = exp2_fast(p[kt][r] - m_use);
         p[kt][r] = e;
         l_run += e;
       }
@@ -419,7 +425,7 @@ void attention64_kernel(
       const float tm = rows4_max(tmax[u]);
       const float m_new = fmaxf(m_run[u], tm);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run[u] - m_use);
+      const float alpha = exp2_fast(m_run[u] - m_use);
       m_run[u] = m_new;
       l_run[u] *= alpha;
 #pragma unroll
@@ -428,7 +434,7 @@ void attention64_kernel(
       for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(p[u][kt][r] - m_use);
+          const float e = exp2_fast(p[u][kt][r] - m_use);
           p[u][kt][r] = e;
           l_run[u] += e;
         }
@@ -780,7 +786,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
       for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(p[u][kt][r] - m_use);
+          const float e = exp2_fast(p[u][kt][r] - m_use);
           p[u][kt][r] = e;
           l_run[u] += e;
         }
