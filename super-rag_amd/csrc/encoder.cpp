@@ -169,7 +169,7 @@ bool Encoder::fold_enabled() const {
 }
 
 // K5c (fused QKV projection + attention) for the folded layers at S == 128: opt-in
-// (SR_FUSED_QKV_ATTN=1).  Bit-exact with the QKV GEMM + K5b pair but 2 % slower end to end: its
+// (SR_FUSED_QKV_ATTN=1).  Bit-exact with the QKV GEMM + K5b pair but ~1 % slower end to end: its
 // attention phase runs at two waves per SIMD with nothing to overlap.
 static bool fused_qkv_attention_enabled() {
   const char* e = std::getenv("SR_FUSED_QKV_ATTN");

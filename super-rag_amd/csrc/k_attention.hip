@@ -758,66 +758,69 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
   {
-    float p[2][8][4];
-    float tmax[2] = {-INFINITY, -INFINITY};
+    // software-pipelined per 16-query tile u: the MFMAs of tile 1's scores run while tile 0's
+    // softmax VALU issues, tile 0's P.V while tile 1's softmax issues (two waves per SIMD in the
+    // same phase have no partner work to overlap otherwise).  Per-value operation order is K5b's.
+    half8 kf[8][2];
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
       const int kr = 16 * kt + (lane & 15);
-      const half8 k0f = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
-      const half8 k1f = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float4v a = {0.f, 0.f, 0.f, 0.f};
-        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0f, qf[u][0], a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1f, qf[u][1], a, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = a[r] * scale_log2 + kb[16 * kt + 4 * g + r];
-          p[u][kt][r] = v;
-          tmax[u] = fmaxf(tmax[u], v);
-        }
-      }
+      kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+      kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
     }
+    float4v sc[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        float4v a = {0.f, 0.f, 0.f, 0.f};
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
+        sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
+      }
+    // V^T fragments of the four 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j)
+    const int q4 = (lane >> 2) & 3, pp = lane & 3;
+    half8 va[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int r0 = 32 * c + 4 * g + q4, r1 = r0 + 16;
+        const half4 lo = tr_read_b64(Vs + r0 * DH + a2_vswz(r0, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
+        const half4 hi = tr_read_b64(Vs + r1 * DH + a2_vswz(r1, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
+        va[c][tt] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const float tm = rows4_max(tmax[u]);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = sc[u][kt][r] * scale_log2 + kb[16 * kt + 4 * g + r];
+          sc[u][kt][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      const float tm = rows4_max(tmax);
       const float m_use = (tm == -INFINITY) ? 0.f : tm;  // (one key block: no rescaling)
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2_fast(p[u][kt][r] - m_use);
-          p[u][kt][r] = e;
+          const float e = exp2_fast(sc[u][kt][r] - m_use);
+          sc[u][kt][r] = e;
           l_run[u] += e;
         }
-    }
-    // O^T += V^T P^T over 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j)
-    const int q4 = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      half8 pb[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int c = 0; c < 4; ++c) {
+        half8 pb;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          pb[u][jj] = (half_t)p[u][2 * c][jj];
-          pb[u][4 + jj] = (half_t)p[u][2 * c + 1][jj];
+          pb[jj] = (half_t)sc[u][2 * c][jj];
+          pb[4 + jj] = (half_t)sc[u][2 * c + 1][jj];
         }
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        half4 lo, hi;
-        {
-          const int r = 32 * c + 4 * g + q4;
-          lo = tr_read_b64(Vs + r * DH + a2_vswz(r, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
-        }
-        {
-          const int r = 32 * c + 16 + 4 * g + q4;
-          hi = tr_read_b64(Vs + r * DH + a2_vswz(r, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
-        }
-        const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          o[u][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[u], o[u][tt], 0, 0, 0);
+        for (int tt = 0; tt < 4; ++tt)
+          o[u][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][tt], pb, o[u][tt], 0, 0, 0);
       }
     }
   }
