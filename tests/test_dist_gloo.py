@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the sharded retrieve exchange of SearchPipeline — all_gather of the
+"""CPU, world_size 2 / 4 / 8 (gloo): the sharded retrieve exchange of SearchPipeline — all_gather of the
 query embeddings (C1), per-shard top-K, all_to_all of the per-shard lists (C2) and the merge —
 returns exactly the single-process top-K for every rank's own queries.  The shard search and the
 merge are CPU doubles with the semantics of sr_store_search_dev / sr_topk_merge_dev (row offset,
@@ -53,15 +53,15 @@ def _worker(rank, world, port, corpus, queries, k, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_retrieve_matches_single_process(world):
     g = torch.Generator().manual_seed(0)
     corpus = torch.randn(1001, 16, generator=g)
-    queries = torch.randn(6, 16, generator=g)
+    queries = torch.randn(16, 16, generator=g)
     k = 7
     ctx = mp.get_context("spawn")
     out_q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
+    port = 29500 + os.getpid() % 1000 + 7 * world
     procs = [ctx.Process(target=_worker, args=(r, world, port, corpus, queries, k, out_q))
              for r in range(world)]
     for p in procs:
