@@ -168,12 +168,12 @@ bool Encoder::fold_enabled() const {
   return !(e && e[0] == '0');
 }
 
-// K5c (fused QKV projection + attention) for the folded layers at S == 128: opt-in
-// (SR_FUSED_QKV_ATTN=1).  Bit-exact with the QKV GEMM + K5b pair but ~1 % slower end to end: its
-// attention phase runs at two waves per SIMD with nothing to overlap.
+// K5c (fused QKV projection + attention) for the folded layers at S == 128; SR_FUSED_QKV_ATTN=0
+// keeps the QKV GEMM + K5b pair (bit-identical results; A/B tests).  Same-box bench: 461.2 vs
+// 454.3 q/s (profiles/r02_fused_qkv_attention/).
 static bool fused_qkv_attention_enabled() {
   const char* e = std::getenv("SR_FUSED_QKV_ATTN");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }
 
 void Encoder::set_fp8(int mode) {

@@ -12,6 +12,7 @@
 // P.V product (O^T = V^T P^T) with a permuted k order (keys 32c+4g+j and 32c+16+4g+j for lane
 // group g), so P never leaves the registers; V is stored transposed in LDS to match.
 // Accumulation and softmax statistics are fp32; P is rounded to fp16 for the MFMA.
+#include <algorithm>
 #include <cstdlib>
 
 #include "sr_common.h"
@@ -566,20 +567,27 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     const int32_t* __restrict__ mask, half_t* __restrict__ ctx, int M, int d, int heads,
     float scale_log2) {
   constexpr int DH = 64;
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * QA_STAGE];
+  constexpr int IMG = 3 * QA_BM * DH;  // Q, K, V images (96 KiB)
+  // LDS: the images, then one K-step buffer (PB) past them; odd K-steps use PA = the first 56 KiB
+  // of the image area (dead during the K-loop).  So the next tile's K-step 0 (PB) is staged while
+  // this tile's attention reads the images, and its K-step 1 (PA) right after.
+  __shared__ __attribute__((aligned(16))) half_t lds[IMG + QA_STAGE];
   __shared__ float kbias[QA_BM];
-  // tile t = (panel, head), head fastest; every XCD walks a contiguous range of tiles so the
-  // 12 heads of a panel share its X rows in that XCD's L2 (and W stays L2-resident)
+  half_t* const PA = lds;
+  half_t* const PB = lds + IMG;
+  // persistent walkers: tile t = (panel, head), head fastest; every XCD walks a contiguous range
+  // of tiles so the 12 heads of a panel share its X rows in that XCD's L2 (W stays L2-resident)
   const int panels = (M + QA_BM - 1) / QA_BM, nwg = panels * heads;
-  int t;
+  int t, t_end;
+  const int t_step = gridDim.x >> 3;
   {
     const int xcd = blockIdx.x & 7, q = nwg >> 3, rem = nwg & 7;
     const int lo = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
-    const int hi = lo + q + (xcd < rem ? 1 : 0);
+    t_end = lo + q + (xcd < rem ? 1 : 0);
     t = lo + (blockIdx.x >> 3);
-    if (t >= hi) return;
+    if (t >= t_end || t_step <= 0) return;
   }
-  const int h = t % heads, m0 = (t / heads) * QA_BM;
+  int h = t % heads, m0 = (t / heads) * QA_BM;
   const int K = d, nk = K / 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -596,14 +604,14 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     vbw[par] = (uint32_t)(((int64_t)(lane >> 3) * K + ch * 8) * 2);
     vbx[par] = (uint32_t)(((int64_t)(lane >> 3) * lda + ch * 8) * 2);
   }
-  auto stage = [&](int kt, half_t* s) __attribute__((always_inline)) {
+  auto stage = [&](int kt, half_t* s, int mm, int hh) __attribute__((always_inline)) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const auto rw = panel_rsrc(W, (int64_t)3 * d * K * 2);
-    const auto rx = panel_rsrc(X + (int64_t)m0 * lda, (int64_t)(M - m0 < QA_BM ? M - m0 : QA_BM) * lda * 2);
+    const auto rx = panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < QA_BM ? M - mm : QA_BM) * lda * 2);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int p = w4 * 6 + i;  // rows 8p .. 8p+7 of the tile: segment p >> 3 (Q, K, V)
-      const int grow = (p >> 3) * d + h * DH + 8 * (p & 7);
+      const int grow = (p >> 3) * d + hh * DH + 8 * (p & 7);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, SR_LDS(s + p * 8 * 64), 16, vbw[i & 1],
                                                grow * K * 2 + kt * 128, 0, 0);
     }
@@ -619,27 +627,30 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
   };
 
   float4v acc[6][4];
+  half8 aX[3], aY[3], bX[4], bY[4];
+
+  // first tile: group 0 stages K-step 0 (PB) and waits for it, group 1 K-step 1 (PA)
+  if (grp == 0) {
+    stage(0, PB, m0, h);
+    SR_WAITCNT(0, 15);
+  } else if (nk > 1) {
+    stage(1, PA, m0, h);
+  }
+  __builtin_amdgcn_s_barrier();
+
+  for (;;) {
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-  half8 aX[3], aY[3], bX[4], bY[4];
-
-  if (grp == 0) {
-    stage(0, lds);
-    SR_WAITCNT(0, 15);
-  } else if (nk > 1) {
-    stage(1, lds + QA_STAGE);
-  }
-  __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < 3; ++i) aY[i] = qa_frag(lds, arow + 16 * i, c0);
+  for (int i = 0; i < 3; ++i) aY[i] = qa_frag(PB, arow + 16 * i, c0);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bX[j] = qa_frag(lds + QA_BN * 64, brow + 16 * j, c0);
+  for (int j = 0; j < 4; ++j) bX[j] = qa_frag(PB + QA_BN * 64, brow + 16 * j, c0);
 
   for (int kt = 0; kt < (DIAG == 1 ? 0 : nk); ++kt) {
-    half_t* cur = lds + (kt & 1) * QA_STAGE;
-    const half_t* nxt = lds + ((kt + 1) & 1) * QA_STAGE;
+    half_t* cur = (kt & 1) ? PA : PB;
+    const half_t* nxt = (kt & 1) ? PB : PA;
     const half_t* Bc = cur + QA_BN * 64;
     // p0: A[0..2] x B (k 0..31); reads A[3..5] (k 0..31)
 #pragma unroll
@@ -673,7 +684,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     SR_WAITCNT(0, 0);  // K-step kt+1 landed (all waves); buffer kt & 1 is no longer read
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk && grp == (kt & 1)) stage(kt + 2, cur);
+    if (kt + 2 < nk && grp == (kt & 1)) stage(kt + 2, cur, m0, h);
     // p3: A[3..5] x B' (k 32..63); reads K-step kt+1's p0 operands
     const bool rn = kt + 1 < nk;
     if (rn) {
@@ -693,7 +704,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  // ---- epilogue -> LDS images (the stages are dead: every wave passed the last barrier after its
+  // ---- epilogue -> LDS images (PA / PB are dead: every wave passed the last barrier after its
   // final LDS reads, and no staging is in flight) ----
   half_t* Qi = lds;
   half_t* Ki = lds + QA_BM * DH;
@@ -734,11 +745,16 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     }
   }
   __syncthreads();
+  const int t_next = t + t_step;
+  const bool more = t_next < t_end;
+  const int h_n = t_next % heads, m0_n = (t_next / heads) * QA_BM;
+  if (more && grp == 0) stage(0, PB, m0_n, h_n);  // the next tile's K-step 0 lands during attention
 
   // ---- attention: waves 4s .. 4s+3 own sequence s of the panel, 32 queries each ----
   const int sq = wave >> 2, qw = (wave & 3) * 32;
-  if (m0 + QA_BM / 2 * (sq + 1) > M) return;  // a panel with one sequence (no barrier follows)
-  if constexpr (DIAG == 2) return;
+  // (a panel may hold one sequence; DIAG 2 skips the attention)
+  const bool attend = DIAG != 2 && m0 + QA_BM / 2 * (sq + 1) <= M;
+  if (attend) {
   const half_t* Qs = Qi + sq * 128 * DH;
   const half_t* Ks = Ki + sq * 128 * DH;
   const half_t* Vs = Vi + sq * 128 * DH;
@@ -844,6 +860,23 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
       *reinterpret_cast<half8*>(ctx + (int64_t)q * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2)) = hv;
     }
   }
+  }  // attend
+  if (!more) break;
+  // every wave is done with the images: the next tile's K-step 1 goes into PA; K-step 0 (group 0,
+  // older than this wave's 4 ctx stores) must have landed before the barrier
+  __syncthreads();
+  if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
+  if (grp == 0) {
+    if (attend)
+      SR_WAITCNT(4, 15);
+    else
+      SR_WAITCNT(0, 15);
+  }
+  __builtin_amdgcn_s_barrier();
+  t = t_next;
+  h = h_n;
+  m0 = m0_n;
+  }
 }
 }  // namespace
 
@@ -916,7 +949,8 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   const float scale_log2 = 1.4426950408889634f / 8.0f;
   const int64_t tiles = ceil_div(M, 256) * heads;
   SR_CHECK(tiles < (1ll << 31), "qkv_attention: too many tiles");
-  const dim3 grid((unsigned)tiles), block(512);
+  // persistent: 8 XCD groups x G walkers, one 8-wave workgroup per CU (153 KiB of LDS)
+  const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
   static const int diag = [] {
     const char* e = std::getenv("SR_QA_DIAG");
     return e ? std::atoi(e) : 0;

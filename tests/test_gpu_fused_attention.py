@@ -46,7 +46,7 @@ def _both(monkeypatch, fn):
     return fn(), ref
 
 
-@pytest.mark.parametrize("B", [1, 3, 34])
+@pytest.mark.parametrize("B", [1, 3, 34, 201])  # 201: 404 tiles, walkers take several
 def test_fused_cross_encoder_bit_exact(B, monkeypatch):
     from super_rag_amd.encoder import Encoder, ModelSpec, random_weights
     spec = ModelSpec("t", "xlmr", 1000, 256, 3, 4, 512, 200, 1, 1e-5, 1, classifier=1, bos_id=0,
