@@ -47,6 +47,8 @@ def logical(name):
     base = m.group(1) if m else name
     if base.startswith("attention"):
         return "attention"
+    if base == "qkv_attn":
+        return "qkv_attention"   # K5c's ProfScope name
     return base
 
 
