@@ -1,5 +1,5 @@
 """Drive the reranker encoder at S = 128 (PMC / timing harness for K5c, diagnostic):
-    SR_FUSED_QKV_ATTN=1 python tools/qa_shape.py [--pairs 4096] [--reps 3]"""
+    python tools/qa_shape.py [--pairs 4096] [--reps 3]   (K5c is the default; SR_FUSED_QKV_ATTN=0: unfused)"""
 import argparse
 import os
 import sys
