@@ -640,242 +640,242 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 
   for (;;) {
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 3; ++i) aY[i] = qa_frag(PB, arow + 16 * i, c0);
+    for (int i = 0; i < 3; ++i) aY[i] = qa_frag(PB, arow + 16 * i, c0);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bX[j] = qa_frag(PB + QA_BN * 64, brow + 16 * j, c0);
+    for (int j = 0; j < 4; ++j) bX[j] = qa_frag(PB + QA_BN * 64, brow + 16 * j, c0);
 
-  for (int kt = 0; kt < (DIAG == 1 ? 0 : nk); ++kt) {
-    half_t* cur = (kt & 1) ? PA : PB;
-    const half_t* nxt = (kt & 1) ? PB : PA;
-    const half_t* Bc = cur + QA_BN * 64;
-    // p0: A[0..2] x B (k 0..31); reads A[3..5] (k 0..31)
+    for (int kt = 0; kt < (DIAG == 1 ? 0 : nk); ++kt) {
+      half_t* cur = (kt & 1) ? PA : PB;
+      const half_t* nxt = (kt & 1) ? PB : PA;
+      const half_t* Bc = cur + QA_BN * 64;
+      // p0: A[0..2] x B (k 0..31); reads A[3..5] (k 0..31)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) aX[i] = qa_frag(cur, arow + 16 * (3 + i), c0);
+      for (int i = 0; i < 3; ++i) aX[i] = qa_frag(cur, arow + 16 * (3 + i), c0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bX[j], acc[i][j], 0, 0, 0);
-    SR_QA_INTERLEAVE(3);
-    // p1: A[3..5] x B (k 0..31); reads A[0..2], B (k 32..63)
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bX[j], acc[i][j], 0, 0, 0);
+      SR_QA_INTERLEAVE(3);
+      // p1: A[3..5] x B (k 0..31); reads A[0..2], B (k 32..63)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) aY[i] = qa_frag(cur, arow + 16 * i, c0 + 4);
+      for (int i = 0; i < 3; ++i) aY[i] = qa_frag(cur, arow + 16 * i, c0 + 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bY[j] = qa_frag(Bc, brow + 16 * j, c0 + 4);
+      for (int j = 0; j < 4; ++j) bY[j] = qa_frag(Bc, brow + 16 * j, c0 + 4);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[3 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bX[j], acc[3 + i][j], 0, 0, 0);
-    SR_QA_INTERLEAVE(7);
-    // p2: A[0..2] x B' (k 32..63); reads A[3..5] (k 32..63)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) aX[i] = qa_frag(cur, arow + 16 * (3 + i), c0 + 4);
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bY[j], acc[i][j], 0, 0, 0);
-    SR_QA_INTERLEAVE(3);
-    SR_WAITCNT(0, 0);  // K-step kt+1 landed (all waves); buffer kt & 1 is no longer read
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk && grp == (kt & 1)) stage(kt + 2, cur, m0, h);
-    // p3: A[3..5] x B' (k 32..63); reads K-step kt+1's p0 operands
-    const bool rn = kt + 1 < nk;
-    if (rn) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) aY[i] = qa_frag(nxt, arow + 16 * i, c0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bX[j] = qa_frag(nxt + QA_BN * 64, brow + 16 * j, c0);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[3 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bY[j], acc[3 + i][j], 0, 0, 0);
-    if (rn) {
+        for (int j = 0; j < 4; ++j)
+          acc[3 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bX[j], acc[3 + i][j], 0, 0, 0);
       SR_QA_INTERLEAVE(7);
+      // p2: A[0..2] x B' (k 32..63); reads A[3..5] (k 32..63)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) aX[i] = qa_frag(cur, arow + 16 * (3 + i), c0 + 4);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bY[j], acc[i][j], 0, 0, 0);
+      SR_QA_INTERLEAVE(3);
+      SR_WAITCNT(0, 0);  // K-step kt+1 landed (all waves); buffer kt & 1 is no longer read
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 < nk && grp == (kt & 1)) stage(kt + 2, cur, m0, h);
+      // p3: A[3..5] x B' (k 32..63); reads K-step kt+1's p0 operands
+      const bool rn = kt + 1 < nk;
+      if (rn) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) aY[i] = qa_frag(nxt, arow + 16 * i, c0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bX[j] = qa_frag(nxt + QA_BN * 64, brow + 16 * j, c0);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[3 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bY[j], acc[3 + i][j], 0, 0, 0);
+      if (rn) {
+        SR_QA_INTERLEAVE(7);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-  }
 
-  // ---- epilogue -> LDS images (PA / PB are dead: every wave passed the last barrier after its
-  // final LDS reads, and no staging is in flight) ----
-  half_t* Qi = lds;
-  half_t* Ki = lds + QA_BM * DH;
-  half_t* Vi = lds + 2 * QA_BM * DH;
-  if (tid < QA_BM) {
-    const int m = m0 + tid;
-    kbias[tid] = (m < M && mask[m < M ? m : M - 1] != 0) ? 0.f : -INFINITY;
-  }
-  const int g = lane >> 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int ml = wm * 64 + 16 * j + (lane & 15);
-    const int mg = m0 + ml < M ? m0 + ml : M - 1;
-    float mu = 0.f, rstd = 1.f;
-    if constexpr (LNF) {
-      const float2 v = *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2);
-      mu = v.x;
-      rstd = v.y;
+    // ---- epilogue -> LDS images (PA / PB are dead: every wave passed the last barrier after its
+    // final LDS reads, and no staging is in flight) ----
+    half_t* Qi = lds;
+    half_t* Ki = lds + QA_BM * DH;
+    half_t* Vi = lds + 2 * QA_BM * DH;
+    if (tid < QA_BM) {
+      const int m = m0 + tid;
+      kbias[tid] = (m < M && mask[m < M ? m : M - 1] != 0) ? 0.f : -INFINITY;
     }
+    const int g = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
-      const int seg = n >> 6, dim = n & 63;
-      const int col = seg * d + h * DH + dim;
-      const float4v b = *reinterpret_cast<const float4v*>(bias + col);
-      half4 y;
+    for (int j = 0; j < 4; ++j) {
+      const int ml = wm * 64 + 16 * j + (lane & 15);
+      const int mg = m0 + ml < M ? m0 + ml : M - 1;
+      float mu = 0.f, rstd = 1.f;
       if constexpr (LNF) {
-        const float4v c = *reinterpret_cast<const float4v*>(colsum + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = (half_t)fmaf(rstd, fmaf(-mu, c[r], acc[i][j][r]), b[r]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = (half_t)(acc[i][j][r] + b[r]);
+        const float2 v = *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2);
+        mu = v.x;
+        rstd = v.y;
       }
-      half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
-      const int chunk = seg == 2 ? a2_vswz(ml, dim >> 3) : a2_kswz(ml, dim >> 3);
-      *reinterpret_cast<half4*>(img + ml * DH + chunk * 8 + (dim & 7)) = y;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
+        const int seg = n >> 6, dim = n & 63;
+        const int col = seg * d + h * DH + dim;
+        const float4v b = *reinterpret_cast<const float4v*>(bias + col);
+        half4 y;
+        if constexpr (LNF) {
+          const float4v c = *reinterpret_cast<const float4v*>(colsum + col);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = (half_t)fmaf(rstd, fmaf(-mu, c[r], acc[i][j][r]), b[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = (half_t)(acc[i][j][r] + b[r]);
+        }
+        half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
+        const int chunk = seg == 2 ? a2_vswz(ml, dim >> 3) : a2_kswz(ml, dim >> 3);
+        *reinterpret_cast<half4*>(img + ml * DH + chunk * 8 + (dim & 7)) = y;
+      }
     }
-  }
-  __syncthreads();
-  const int t_next = t + t_step;
-  const bool more = t_next < t_end;
-  const int h_n = t_next % heads, m0_n = (t_next / heads) * QA_BM;
-  if (more && grp == 0) stage(0, PB, m0_n, h_n);  // the next tile's K-step 0 lands during attention
+    __syncthreads();
+    const int t_next = t + t_step;
+    const bool more = t_next < t_end;
+    const int h_n = t_next % heads, m0_n = (t_next / heads) * QA_BM;
+    if (more && grp == 0) stage(0, PB, m0_n, h_n);  // the next tile's K-step 0 lands during attention
 
-  // ---- attention: waves 4s .. 4s+3 own sequence s of the panel, 32 queries each ----
-  const int sq = wave >> 2, qw = (wave & 3) * 32;
-  // (a panel may hold one sequence; DIAG 2 skips the attention)
-  const bool attend = DIAG != 2 && m0 + QA_BM / 2 * (sq + 1) <= M;
-  if (attend) {
-  const half_t* Qs = Qi + sq * 128 * DH;
-  const half_t* Ks = Ki + sq * 128 * DH;
-  const half_t* Vs = Vi + sq * 128 * DH;
-  const float* kb = kbias + sq * 128;
-  half8 qf[2][2];
+    // ---- attention: waves 4s .. 4s+3 own sequence s of the panel, 32 queries each ----
+    const int sq = wave >> 2, qw = (wave & 3) * 32;
+    // (a panel may hold one sequence; DIAG 2 skips the attention)
+    const bool attend = DIAG != 2 && m0 + QA_BM / 2 * (sq + 1) <= M;
+    if (attend) {
+      const half_t* Qs = Qi + sq * 128 * DH;
+      const half_t* Ks = Ki + sq * 128 * DH;
+      const half_t* Vs = Vi + sq * 128 * DH;
+      const float* kb = kbias + sq * 128;
+      half8 qf[2][2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int r = qw + 16 * u + (lane & 15);
+      for (int u = 0; u < 2; ++u) {
+        const int r = qw + 16 * u + (lane & 15);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-      qf[u][s2] = *reinterpret_cast<const half8*>(Qs + r * DH + a2_kswz(r, g + 4 * s2) * 8);
-  }
-  float l_run[2] = {0.f, 0.f};
-  float4v o[2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
-  {
-    // software-pipelined per 16-query tile u: the MFMAs of tile 1's scores run while tile 0's
-    // softmax VALU issues, tile 0's P.V while tile 1's softmax issues (two waves per SIMD in the
-    // same phase have no partner work to overlap otherwise).  Per-value operation order is K5b's.
-    half8 kf[8][2];
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      const int kr = 16 * kt + (lane & 15);
-      kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
-      kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
-    }
-    float4v sc[2][8];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int kt = 0; kt < 8; ++kt) {
-        float4v a = {0.f, 0.f, 0.f, 0.f};
-        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
-        sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
+        for (int s2 = 0; s2 < 2; ++s2)
+          qf[u][s2] = *reinterpret_cast<const half8*>(Qs + r * DH + a2_kswz(r, g + 4 * s2) * 8);
       }
-    // V^T fragments of the four 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j)
-    const int q4 = (lane >> 2) & 3, pp = lane & 3;
-    half8 va[4][4];
+      float l_run[2] = {0.f, 0.f};
+      float4v o[2][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const int r0 = 32 * c + 4 * g + q4, r1 = r0 + 16;
-        const half4 lo = tr_read_b64(Vs + r0 * DH + a2_vswz(r0, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
-        const half4 hi = tr_read_b64(Vs + r1 * DH + a2_vswz(r1, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
-        va[c][tt] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
+        for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
+      {
+        // software-pipelined per 16-query tile u: the MFMAs of tile 1's scores run while tile 0's
+        // softmax VALU issues, tile 0's P.V while tile 1's softmax issues (two waves per SIMD in the
+        // same phase have no partner work to overlap otherwise).  Per-value operation order is K5b's.
+        half8 kf[8][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = sc[u][kt][r] * scale_log2 + kb[16 * kt + 4 * g + r];
-          sc[u][kt][r] = v;
-          tmax = fmaxf(tmax, v);
+        for (int kt = 0; kt < 8; ++kt) {
+          const int kr = 16 * kt + (lane & 15);
+          kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+          kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
         }
-      const float tm = rows4_max(tmax);
-      const float m_use = (tm == -INFINITY) ? 0.f : tm;  // (one key block: no rescaling)
+        float4v sc[2][8];
 #pragma unroll
-      for (int kt = 0; kt < 8; ++kt)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = exp2_fast(sc[u][kt][r] - m_use);
-          sc[u][kt][r] = e;
-          l_run[u] += e;
+          for (int kt = 0; kt < 8; ++kt) {
+            float4v a = {0.f, 0.f, 0.f, 0.f};
+            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
+            sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
+          }
+        // V^T fragments of the four 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j)
+        const int q4 = (lane >> 2) & 3, pp = lane & 3;
+        half8 va[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const int r0 = 32 * c + 4 * g + q4, r1 = r0 + 16;
+            const half4 lo = tr_read_b64(Vs + r0 * DH + a2_vswz(r0, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
+            const half4 hi = tr_read_b64(Vs + r1 * DH + a2_vswz(r1, 2 * tt + (pp >> 1)) * 8 + 4 * (pp & 1));
+            va[c][tt] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float tmax = -INFINITY;
+#pragma unroll
+          for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = sc[u][kt][r] * scale_log2 + kb[16 * kt + 4 * g + r];
+              sc[u][kt][r] = v;
+              tmax = fmaxf(tmax, v);
+            }
+          const float tm = rows4_max(tmax);
+          const float m_use = (tm == -INFINITY) ? 0.f : tm;  // (one key block: no rescaling)
+#pragma unroll
+          for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float e = exp2_fast(sc[u][kt][r] - m_use);
+              sc[u][kt][r] = e;
+              l_run[u] += e;
+            }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            half8 pb;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              pb[jj] = (half_t)sc[u][2 * c][jj];
+              pb[4 + jj] = (half_t)sc[u][2 * c + 1][jj];
+            }
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+              o[u][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][tt], pb, o[u][tt], 0, 0, 0);
+          }
         }
+      }
+      // normalise and store (permlane16_swap: 8 consecutive dims per lane)
+      const int odd = g & 1;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        half8 pb;
+      for (int u = 0; u < 2; ++u) {
+        const float l = rows4_sum(l_run[u]);
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        const int q = m0 + sq * 128 + qw + 16 * u + (lane & 15);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          pb[jj] = (half_t)sc[u][2 * c][jj];
-          pb[4 + jj] = (half_t)sc[u][2 * c + 1][jj];
+        for (int p2 = 0; p2 < 2; ++p2) {
+          half8 hv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[u][2 * p2][r]),
+                                                             __float_as_uint(o[u][2 * p2 + 1][r]), false, false);
+            hv[r] = (half_t)(__uint_as_float(sw[0]) * inv);
+            hv[4 + r] = (half_t)(__uint_as_float(sw[1]) * inv);
+          }
+          *reinterpret_cast<half8*>(ctx + (int64_t)q * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2)) = hv;
         }
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt)
-          o[u][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][tt], pb, o[u][tt], 0, 0, 0);
       }
+    }  // attend
+    if (!more) break;
+    // every wave is done with the images: the next tile's K-step 1 goes into PA; K-step 0 (group 0,
+    // older than this wave's 4 ctx stores) must have landed before the barrier
+    __syncthreads();
+    if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
+    if (grp == 0) {
+      if (attend)
+        SR_WAITCNT(4, 15);
+      else
+        SR_WAITCNT(0, 15);
     }
-  }
-  // normalise and store (permlane16_swap: 8 consecutive dims per lane)
-  const int odd = g & 1;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const float l = rows4_sum(l_run[u]);
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    const int q = m0 + sq * 128 + qw + 16 * u + (lane & 15);
-#pragma unroll
-    for (int p2 = 0; p2 < 2; ++p2) {
-      half8 hv;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[u][2 * p2][r]),
-                                                         __float_as_uint(o[u][2 * p2 + 1][r]), false, false);
-        hv[r] = (half_t)(__uint_as_float(sw[0]) * inv);
-        hv[4 + r] = (half_t)(__uint_as_float(sw[1]) * inv);
-      }
-      *reinterpret_cast<half8*>(ctx + (int64_t)q * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2)) = hv;
-    }
-  }
-  }  // attend
-  if (!more) break;
-  // every wave is done with the images: the next tile's K-step 1 goes into PA; K-step 0 (group 0,
-  // older than this wave's 4 ctx stores) must have landed before the barrier
-  __syncthreads();
-  if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
-  if (grp == 0) {
-    if (attend)
-      SR_WAITCNT(4, 15);
-    else
-      SR_WAITCNT(0, 15);
-  }
-  __builtin_amdgcn_s_barrier();
-  t = t_next;
-  h = h_n;
-  m0 = m0_n;
+    __builtin_amdgcn_s_barrier();
+    t = t_next;
+    h = h_n;
+    m0 = m0_n;
   }
 }
 }  // namespace
