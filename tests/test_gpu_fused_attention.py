@@ -86,3 +86,15 @@ def test_fused_bge_reranker_shape_chunked(monkeypatch):
     np.testing.assert_array_equal(got, unfused)
     ref = R.cross_logits(_cfg(spec), w, ids, mask)
     assert np.abs(got - ref).max() <= 1e-2 * (1.0 + np.abs(ref).max())
+
+
+def test_fused_full_chunk_bit_exact(monkeypatch):
+    # the bench's chunk: 12,800 pairs x 128 tokens in one launch per layer (76,800 tiles, 300 per
+    # persistent walker): fused == unfused bit for bit
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    spec = MODELS["bge-reranker-base"]
+    enc = Encoder(spec, weights=random_weights(spec, seed=23, style="hf"), max_tokens=1_638_400)
+    ids, mask = _batch(spec, 12_800, 128, seed=4)
+    got, unfused = _both(monkeypatch, lambda: enc.cross_score(ids, mask))
+    np.testing.assert_array_equal(got, unfused)
+    enc.close()
