@@ -195,6 +195,14 @@ __device__ __forceinline__ float rows4_sum(float x) {
 }
 __device__ __forceinline__ int a2_vswz(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
 
+// A operand of the row-sum MFMA: D = ones(16 x 32) . P^T puts the sum of a query's 32 fp16
+// probabilities in all 16 rows of its column, so the softmax denominator costs one MFMA per
+// 32-key chunk instead of a VALU add per score (and it sums exactly the fp16 weights P.V uses)
+__device__ __forceinline__ half8 a2_ones() {
+  const half_t one = (half_t)1.0f;
+  return half8{one, one, one, one, one, one, one, one};
+}
+
 __device__ __forceinline__ half4 tr_read_b64(const half_t* p) {
   typedef short short4_t __attribute__((ext_vector_type(4)));
   short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -377,12 +385,16 @@ void attention64_kernel(
   if (!SPLIT && !STREAM && !active) return;  // no barrier follows
 
   const int g = lane >> 4;
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
-  float4v o[2][4];
+  float m_run[2] = {-INFINITY, -INFINITY};
+  // o: O^T tiles; lsum: the softmax denominators, accumulated by one extra MFMA per 32-key chunk
+  // with an all-ones A operand (every element of lsum[u] = the row sum of the fp16 P it multiplies)
+  float4v o[2][4], lsum[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < 2; ++u) {
+    lsum[u] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t) o[u][t] = float4v{0.f, 0.f, 0.f, 0.f};
+  }
 
   for (int k0 = 0; k0 < S_pad; k0 += 128) {
     if constexpr (STREAM) {  // key block k0 / 128 (this wave's later blocks may still be in flight)
@@ -392,6 +404,83 @@ void attention64_kernel(
         else SR_WAITCNT(0, 15);
         __builtin_amdgcn_s_barrier();
       }
+      // software-pipelined per 16-query tile u (as K5c): both tiles' score MFMAs and the block's
+      // V^T fragments are issued first, then tile 0's softmax runs while tile 1's scores finish and
+      // tile 1's softmax beside tile 0's P.V.  Per-value operation order is the generic path's.
+      half8 kf[8][2];
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        const int kr = k0 + 16 * kt + (lane & 15);
+        kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+        kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
+      }
+      float4v sc[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt) {
+          float4v a = {0.f, 0.f, 0.f, 0.f};
+          a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
+          sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
+        }
+      const int q = (lane >> 2) & 3, pp = lane & 3;
+      half8 va[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t addr[8];
+        uint2 vv[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int r = k0 + 32 * c + 16 * hh + 4 * g + q;
+            addr[2 * t + hh] = lds_addr(Vs + r * DH + a2_vswz(r, 2 * t + (pp >> 1)) * 8 + 4 * (pp & 1));
+          }
+        tr_read_chunk_asm(addr, vv);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const half4 lo = __builtin_bit_cast(half4, vv[2 * t]), hi = __builtin_bit_cast(half4, vv[2 * t + 1]);
+          va[c][t] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = sc[u][kt][r] * scale_log2 + kbias[k0 + 16 * kt + 4 * g + r];
+            sc[u][kt][r] = v;
+            tmax = fmaxf(tmax, v);
+          }
+        const float tm = rows4_max(tmax);
+        const float m_new = fmaxf(m_run[u], tm);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const float alpha = exp2_fast(m_run[u] - m_use);
+        m_run[u] = m_new;
+        lsum[u] *= alpha;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[u][t] *= alpha;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[u][kt][r] = exp2_fast(sc[u][kt][r] - m_use);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          half8 pb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pb[j] = (half_t)sc[u][2 * c][j];
+            pb[4 + j] = (half_t)sc[u][2 * c + 1][j];
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            o[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][t], pb, o[u][t], 0, 0, 0);
+          lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2_ones(), pb, lsum[u], 0, 0, 0);
+        }
+      }
+      continue;
     }
     const int nkt = (S_pad - k0) >= 128 ? 8 : (S_pad - k0) / 16;  // 16-key tiles in this block
     float p[2][8][4];
@@ -428,17 +517,13 @@ void attention64_kernel(
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
       const float alpha = exp2_fast(m_run[u] - m_use);
       m_run[u] = m_new;
-      l_run[u] *= alpha;
+      lsum[u] *= alpha;
 #pragma unroll
       for (int t = 0; t < 4; ++t) o[u][t] *= alpha;
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = exp2_fast(p[u][kt][r] - m_use);
-          p[u][kt][r] = e;
-          l_run[u] += e;
-        }
+        for (int r = 0; r < 4; ++r) p[u][kt][r] = exp2_fast(p[u][kt][r] - m_use);
     }
     // ---- O^T += V^T P^T over 32-key chunks (key order of the B operand: 32c + 4g + j, then
     //      32c + 16 + 4g + j; the transposed V reads use the same order) ----
@@ -462,27 +547,9 @@ void attention64_kernel(
           }
         // lane 4q+p of group g: V row k0 + 32c + 16hh + 4g + q, dims 16t + 4p .. +3
         const int q = (lane >> 2) & 3, pp = lane & 3;
-        if constexpr (STREAM) {
-          uint32_t addr[8];
-          uint2 vv[8];
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const int r = k0 + 32 * c + 16 * hh + 4 * g + q;
-              addr[2 * t + hh] = lds_addr(Vs + r * DH + a2_vswz(r, 2 * t + (pp >> 1)) * 8 + 4 * (pp & 1));
-            }
-          tr_read_chunk_asm(addr, vv);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const half4 lo = __builtin_bit_cast(half4, vv[2 * t]), hi = __builtin_bit_cast(half4, vv[2 * t + 1]);
-            const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-              o[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[u], o[u][t], 0, 0, 0);
-          }
-          continue;
-        }
+        for (int u = 0; u < 2; ++u)
+          lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2_ones(), pb[u], lsum[u], 0, 0, 0);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           half4 lo, hi;
@@ -509,7 +576,7 @@ void attention64_kernel(
   const int odd = g & 1;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const float l = rows4_sum(l_run[u]);
+    const float l = lsum[u][0];
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int q = qw + 16 * u + (lane & 15);
 #pragma unroll
@@ -767,12 +834,13 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         for (int s2 = 0; s2 < 2; ++s2)
           qf[u][s2] = *reinterpret_cast<const half8*>(Qs + r * DH + a2_kswz(r, g + 4 * s2) * 8);
       }
-      float l_run[2] = {0.f, 0.f};
-      float4v o[2][4];
+      float4v o[2][4], lsum[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u) {
+        lsum[u] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
+      }
       {
         // software-pipelined per 16-query tile u: the MFMAs of tile 1's scores run while tile 0's
         // softmax VALU issues, tile 0's P.V while tile 1's softmax issues (two waves per SIMD in the
@@ -821,11 +889,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 #pragma unroll
           for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float e = exp2_fast(sc[u][kt][r] - m_use);
-              sc[u][kt][r] = e;
-              l_run[u] += e;
-            }
+            for (int r = 0; r < 4; ++r) sc[u][kt][r] = exp2_fast(sc[u][kt][r] - m_use);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             half8 pb;
@@ -837,6 +901,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
               o[u][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][tt], pb, o[u][tt], 0, 0, 0);
+            lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2_ones(), pb, lsum[u], 0, 0, 0);
           }
         }
       }
@@ -844,7 +909,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
       const int odd = g & 1;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const float l = rows4_sum(l_run[u]);
+        const float l = lsum[u][0];
         const float inv = l > 0.f ? 1.f / l : 0.f;
         const int q = m0 + sq * 128 + qw + 16 * u + (lane & 15);
 #pragma unroll
