@@ -303,8 +303,8 @@ int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* st
 /* Diagnostic: one attention launch (K5) on device pointers.  qkv: [B*S, 3d] fp16 (Q | K | V),
  * mask: [B, S] int32 (0 = padding key), ctx: [B*Sq, d] fp16 (first Sq query rows of every
  * sequence).  variant: -1 auto, 0 the 64-key-tile kernel, 1 the whole-head-in-LDS kernel with 4
- * waves per workgroup, 2 the same with 8 waves (d/heads
- * must be 64 and S <= 512). */
+ * waves per workgroup, 2 the same with 8 waves, 3 auto but the per-workgroup K5b STREAM form instead
+ * of the persistent K5d at S_pad = 512 (variants 1-3: d/heads must be 64 and S <= 512). */
 int sr_diag_attention(int variant, const void* qkv, const int32_t* mask, void* ctx, int B, int S,
                       int Sq, int d, int heads, int device, void* stream);
 

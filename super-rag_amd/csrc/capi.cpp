@@ -689,9 +689,9 @@ int sr_diag_attention(int variant, const void* qkv, const int32_t* mask, void* c
   SR_NONNULL(qkv);
   SR_NONNULL(mask);
   SR_NONNULL(ctx);
-  SR_CHECK(variant >= -1 && variant <= 2, "diag_attention: variant must be -1 .. 2");
+  SR_CHECK(variant >= -1 && variant <= 3, "diag_attention: variant must be -1 .. 3");
   SR_CHECK(variant < 1 || (heads > 0 && d == 64 * heads && S <= 512),
-           "diag_attention: variants 1-2 need head dim 64 and S <= 512");
+           "diag_attention: variants 1-3 need head dim 64 and S <= 512");
   sr::DeviceGuard g(device);
   sr::attention_force_variant(variant);
   try {

@@ -232,6 +232,100 @@ __device__ __forceinline__ uint32_t lds_addr(const half_t* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// ---- one 128-key block for a wave's two 16-query tiles, software-pipelined (STREAM / K5d) ----
+// scores S^T = K Q^T of both tiles (16 K fragments, 32 MFMAs)
+__device__ __forceinline__ void a2_blk_scores(const half_t* Ks, int k0, const half8 (&qf)[2][2], int lane,
+                                              float4v (&sc)[2][8]) {
+  constexpr int DH = 64;
+  const int g = lane >> 4;
+  half8 kf[8][2];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    const int kr = k0 + 16 * kt + (lane & 15);
+    kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+    kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      float4v a = {0.f, 0.f, 0.f, 0.f};
+      a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
+      sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
+    }
+}
+
+// V^T fragments of the block's four 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j),
+// each chunk one asm block ending in its own lgkmcnt(0) (tr_read_chunk_asm: no compiler vmcnt(0)
+// for the LDS-DMA pieces still in flight)
+__device__ __forceinline__ void a2_blk_vfrags(const half_t* Vs, int k0, int lane, half8 (&va)[4][4]) {
+  constexpr int DH = 64;
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    uint32_t addr[8];
+    uint2 vv[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = k0 + 32 * c + 16 * hh + 4 * g + q;
+        addr[2 * t + hh] = lds_addr(Vs + r * DH + a2_vswz(r, 2 * t + (pp >> 1)) * 8 + 4 * (pp & 1));
+      }
+    tr_read_chunk_asm(addr, vv);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const half4 lo = __builtin_bit_cast(half4, vv[2 * t]), hi = __builtin_bit_cast(half4, vv[2 * t + 1]);
+      va[c][t] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  }
+}
+
+// online softmax of the block (running max, rescale) and O^T += V^T P^T, lsum += ones . P^T
+__device__ __forceinline__ void a2_blk_softmax_pv(float4v (&sc)[2][8], const half8 (&va)[4][4],
+                                                  const float* kbias, int k0, int lane, float scale_log2,
+                                                  float (&m_run)[2], float4v (&o)[2][4],
+                                                  float4v (&lsum)[2]) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sc[u][kt][r] * scale_log2 + kbias[k0 + 16 * kt + 4 * g + r];
+        sc[u][kt][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    const float tm = rows4_max(tmax);
+    const float m_new = fmaxf(m_run[u], tm);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2_fast(m_run[u] - m_use);
+    m_run[u] = m_new;
+    lsum[u] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[u][t] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc[u][kt][r] = exp2_fast(sc[u][kt][r] - m_use);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      half8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (half_t)sc[u][2 * c][j];
+        pb[4 + j] = (half_t)sc[u][2 * c + 1][j];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        o[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][t], pb, o[u][t], 0, 0, 0);
+      lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2_ones(), pb, lsum[u], 0, 0, 0);
+    }
+  }
+}
+
 // SPLIT (S_pad == 128, all four waves active): the Q fragments and the key mask are requested
 // first, then K (LDS-DMA), then V into registers; the score / softmax phase starts once Q and K
 // have landed (vmcnt(4): each wave's four V loads may still be in flight) and V is written to its
@@ -407,79 +501,11 @@ void attention64_kernel(
       // software-pipelined per 16-query tile u (as K5c): both tiles' score MFMAs and the block's
       // V^T fragments are issued first, then tile 0's softmax runs while tile 1's scores finish and
       // tile 1's softmax beside tile 0's P.V.  Per-value operation order is the generic path's.
-      half8 kf[8][2];
-#pragma unroll
-      for (int kt = 0; kt < 8; ++kt) {
-        const int kr = k0 + 16 * kt + (lane & 15);
-        kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
-        kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
-      }
       float4v sc[2][8];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int kt = 0; kt < 8; ++kt) {
-          float4v a = {0.f, 0.f, 0.f, 0.f};
-          a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
-          sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
-        }
-      const int q = (lane >> 2) & 3, pp = lane & 3;
+      a2_blk_scores(Ks, k0, qf, lane, sc);
       half8 va[4][4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint32_t addr[8];
-        uint2 vv[8];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int r = k0 + 32 * c + 16 * hh + 4 * g + q;
-            addr[2 * t + hh] = lds_addr(Vs + r * DH + a2_vswz(r, 2 * t + (pp >> 1)) * 8 + 4 * (pp & 1));
-          }
-        tr_read_chunk_asm(addr, vv);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const half4 lo = __builtin_bit_cast(half4, vv[2 * t]), hi = __builtin_bit_cast(half4, vv[2 * t + 1]);
-          va[c][t] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = sc[u][kt][r] * scale_log2 + kbias[k0 + 16 * kt + 4 * g + r];
-            sc[u][kt][r] = v;
-            tmax = fmaxf(tmax, v);
-          }
-        const float tm = rows4_max(tmax);
-        const float m_new = fmaxf(m_run[u], tm);
-        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-        const float alpha = exp2_fast(m_run[u] - m_use);
-        m_run[u] = m_new;
-        lsum[u] *= alpha;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) o[u][t] *= alpha;
-#pragma unroll
-        for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sc[u][kt][r] = exp2_fast(sc[u][kt][r] - m_use);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          half8 pb;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            pb[j] = (half_t)sc[u][2 * c][j];
-            pb[4 + j] = (half_t)sc[u][2 * c + 1][j];
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            o[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[c][t], pb, o[u][t], 0, 0, 0);
-          lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2_ones(), pb, lsum[u], 0, 0, 0);
-        }
-      }
+      a2_blk_vfrags(Vs, k0, lane, va);
+      a2_blk_softmax_pv(sc, va, kbias, k0, lane, scale_log2, m_run, o, lsum);
       continue;
     }
     const int nkt = (S_pad - k0) >= 128 ? 8 : (S_pad - k0) / 16;  // 16-key tiles in this block
@@ -595,6 +621,158 @@ void attention64_kernel(
   }
 }
 
+
+// ---- K5d: persistent S_pad = 512 attention (d_h = 64, every query; the long-pair reranker) -------
+// One 8-wave workgroup per CU walks its XCD's contiguous range of (sequence, head) tiles.  The
+// head's whole K / V (4 key blocks of 128 rows, K5b's swizzles) stays in LDS for BOTH 256-query
+// passes (A: queries 0..255, B: 256..511), so K and V leave HBM once per (sequence, head) instead
+// of once per 256 queries (K5b STREAM).  During pass B each key block, once every wave is past
+// it, is refilled by LDS-DMA with the next tile's, and the next pass's Q fragments are loaded right
+// after the last block's score MFMAs, so the next tile's loads run under this tile's pass B.  The
+// block body is STREAM's (a2_blk_*): per-value operation order, and so the results, are K5b's.
+// Waits (per wave, VMEM ops retire in order; stores count): tile prologue vmcnt(12) = block 0,
+// Q, mask (blocks 1..3 in flight); pass A block b: vmcnt(8 / 4 / 0) for blocks 1 / 2 / 3; pass B
+// block 0: vmcnt(4) = its Q (pass A's 4 ctx stores may be in flight); next tile: vmcnt(8) =
+// blocks 0..2, Q and mask (younger: pass B's 4 ctx stores and block 3).  A barrier before every
+// block (measured: refilling blocks 0 / 1 together and 2 / 3 after the pass with four barriers
+// per tile ran 1.57 instead of 1.39 ms per 1024 x 12-head launch).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void attention512_kernel(const half_t* __restrict__ qkv, const int32_t* __restrict__ mask,
+                         half_t* __restrict__ ctx, int B, int S, int Sq, int d, int heads,
+                         float scale_log2) {
+  constexpr int DH = 64, SP = 512;
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * SP * DH + 2 * SP];  // K, V images, key bias
+  half_t* const Ks = lds;
+  half_t* const Vs = lds + SP * DH;
+  float* const kbias = reinterpret_cast<float*>(lds + 2 * SP * DH);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int ntiles = B * heads;
+  int t, t_end;
+  const int t_step = gridDim.x >> 3;
+  {
+    const int xcd = blockIdx.x & 7, q = ntiles >> 3, rem = ntiles & 7;
+    const int lo = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+    t_end = lo + q + (xcd < rem ? 1 : 0);
+    t = lo + (blockIdx.x >> 3);
+    if (t >= t_end || t_step <= 0) return;
+  }
+  const int64_t ld = 3 * (int64_t)d;
+  auto stage_blk = [&](const half_t* base, int blk) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = blk * 16 + wave + 8 * i;
+      const int r = piece * 8 + (lane >> 3);
+      __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(r < S ? r : S - 1) * ld + d +
+                                                     a2_kswz(r, lane & 7) * 8),
+                                       SR_LDS(Ks + piece * 8 * DH), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = blk * 16 + wave + 8 * i;
+      const int r = piece * 8 + (lane >> 3);
+      __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(r < S ? r : S - 1) * ld + 2 * d +
+                                                     a2_vswz(r, lane & 7) * 8),
+                                       SR_LDS(Vs + piece * 8 * DH), 16, 0, 0);
+    }
+  };
+  half8 qf[2][2];
+  auto load_q = [&](const half_t* base, int q0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int qr = q0 + wave * 32 + 16 * u + (lane & 15);
+      qr = qr < S ? qr : S - 1;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        qf[u][s2] = *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + 8 * (lane >> 4) + 32 * s2);
+    }
+  };
+  int b = t / heads, h = t % heads;
+  const half_t* base = qkv + (int64_t)b * S * ld + h * DH;
+  stage_blk(base, 0);
+  load_q(base, 0);
+  int32_t mk = mask[(int64_t)b * S + (tid < S ? tid : S - 1)];
+  stage_blk(base, 1);
+  stage_blk(base, 2);
+  stage_blk(base, 3);
+  SR_WAITCNT(12, 15);
+  kbias[tid] = (tid < S && mk != 0) ? 0.f : -INFINITY;  // 512 threads = SP keys
+
+  for (;;) {
+    const int t_next = t + t_step;
+    const bool more = t_next < t_end;
+    const int b_n = more ? t_next / heads : b, h_n = more ? t_next % heads : h;
+    const half_t* base_n = qkv + (int64_t)b_n * S * ld + h_n * DH;
+    for (int pass = 0; pass < 2; ++pass) {
+      float m_run[2] = {-INFINITY, -INFINITY};
+      float4v o[2][4], lsum[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        lsum[u] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll 1
+      for (int blk = 0; blk < 4; ++blk) {
+        if (pass == 0) {
+          if (blk == 1) SR_WAITCNT(8, 15);
+          else if (blk == 2) SR_WAITCNT(4, 15);
+          else if (blk == 3) SR_WAITCNT(0, 15);
+        } else if (blk == 0) {
+          SR_WAITCNT(4, 15);
+        }
+        __builtin_amdgcn_s_barrier();
+        // pass B: every wave is past block blk - 1 -> the next tile's block blk - 1 goes there
+        if (pass == 1 && blk > 0 && more) stage_blk(base_n, blk - 1);
+        const int k0 = blk * 128;
+        float4v sc[2][8];
+        a2_blk_scores(Ks, k0, qf, lane, sc);
+        if (blk == 3) {  // qf is free: the next pass's Q fragments (and the next tile's mask word)
+          if (pass == 0) {
+            load_q(base, 256);
+          } else if (more) {
+            load_q(base_n, 0);
+            mk = mask[(int64_t)b_n * S + (tid < S ? tid : S - 1)];
+          }
+        }
+        half8 va[4][4];
+        a2_blk_vfrags(Vs, k0, lane, va);
+        a2_blk_softmax_pv(sc, va, kbias, k0, lane, scale_log2, m_run, o, lsum);
+      }
+      // normalise and store this pass's 256 queries (permlane16_swap: 8 consecutive dims per lane)
+      const int odd = g & 1;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float l = lsum[u][0];
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        const int q = pass * 256 + wave * 32 + 16 * u + (lane & 15);
+#pragma unroll
+        for (int p2 = 0; p2 < 2; ++p2) {
+          half8 hv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[u][2 * p2][r]),
+                                                             __float_as_uint(o[u][2 * p2 + 1][r]), false, false);
+            hv[r] = (half_t)(__uint_as_float(sw[0]) * inv);
+            hv[4 + r] = (half_t)(__uint_as_float(sw[1]) * inv);
+          }
+          if (q < Sq)
+            *reinterpret_cast<half8*>(ctx + ((int64_t)b * Sq + q) * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2)) = hv;
+        }
+      }
+    }
+    if (!more) break;
+    __builtin_amdgcn_s_barrier();  // every wave is past block 3 and done with the key bias
+    stage_blk(base_n, 3);
+    SR_WAITCNT(8, 15);
+    kbias[tid] = (tid < S && mk != 0) ? 0.f : -INFINITY;
+    t = t_next;
+    b = b_n;
+    h = h_n;
+    base = base_n;
+  }
+}
 
 // ---- K5c: fused QKV projection + attention (S == 128, d_h == 64; the cross-encoder layers) ------
 // One workgroup per (256-token panel = two sequences, head h): the 256 x 192 tile
@@ -945,7 +1123,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 }
 }  // namespace
 
-static int g_attn_variant = -1;  // test hook: -1 auto, 0 = K5 (64-key tiles), 1 = K5b (4 waves), 2 = K5b with 8 waves
+static int g_attn_variant = -1;  // test hook: -1 auto, 0 = K5 (64-key tiles), 1 = K5b (4 waves), 2 = K5b with 8 waves, 3 = auto with K5b STREAM instead of K5d
 void attention_force_variant(int v) { g_attn_variant = v; }
 
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
@@ -963,7 +1141,7 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
     const int S_pad = (S + 31) & ~31;
     const bool split = S_pad == 128 && Sq > 96;  // K5b SPLIT: one key block, all waves active
     // long sequences: 8 waves (256 queries) per workgroup share one K/V image (auto: S_pad > 256)
-    const int nw = (g_attn_variant == 2 || (g_attn_variant < 0 && S_pad > 256)) ? 8 : 4;
+    const int nw = (g_attn_variant == 2 || ((g_attn_variant < 0 || g_attn_variant == 3) && S_pad > 256)) ? 8 : 4;
     // SPLIT also stages the workgroup's 128 Q rows (a third S_pad x 64 image)
     const size_t shmem = (size_t)(split && nw == 4 ? 3 : 2) * S_pad * 64 * sizeof(half_t) +
                          (size_t)S_pad * sizeof(float);
@@ -971,9 +1149,15 @@ void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B
     if (split && nw == 4)
       hipLaunchKernelGGL((attention64_kernel<true, 4>), grid, block, shmem, stream, qkv, mask, ctx, S,
                          Sq, d, scale_log2);
-    else if (nw == 8 && S_pad == 512 && Sq > 480 && g_attn_variant != 2)  // every wave active
+    else if (nw == 8 && S_pad == 512 && Sq > 480 && g_attn_variant == 3)  // K5b STREAM (A/B)
       hipLaunchKernelGGL((attention64_kernel<false, 8, true>), grid, block, shmem, stream, qkv, mask, ctx,
                          S, Sq, d, scale_log2);
+    else if (nw == 8 && S_pad == 512 && Sq > 480 && g_attn_variant != 2) {  // every query: K5d
+      const int64_t tiles = (int64_t)B * heads;
+      const int walkers = 8 * (int)std::min<int64_t>(32, (tiles + 7) / 8);
+      hipLaunchKernelGGL(attention512_kernel, dim3(walkers), dim3(512), 0, stream, qkv, mask, ctx, B, S,
+                         Sq, d, heads, scale_log2);
+    }
     else if (nw == 8)
       hipLaunchKernelGGL((attention64_kernel<false, 8>), grid, block, shmem, stream, qkv, mask, ctx, S,
                          Sq, d, scale_log2);

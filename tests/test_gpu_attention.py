@@ -36,14 +36,14 @@ def _run(variant, B, S, Sq, heads, dh=64, seed=0, lens=None):
     return (ctx.float() - ref).abs().max().item()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, -1])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, -1])
 @pytest.mark.parametrize("S,Sq", [(128, 128), (128, 1), (32, 32), (100, 100), (7, 7), (200, 200),
                                   (512, 512), (300, 1), (130, 130),
                                   # K5b SPLIT boundaries (S_pad == 128 and Sq > 96): first / last
                                   # S of the split range, the last query tile partly stored, and
                                   # Sq = 96 (non-split: wave 3 idle)
                                   (97, 97), (128, 97), (128, 96), (120, 110),
-                                  # K5b STREAM (auto, 8 waves, S_pad = 512, Sq > 480)
+                                  # K5d (auto) / K5b STREAM (variant 3): 8 waves, S_pad = 512, Sq > 480
                                   (500, 500), (512, 481), (512, 480)])
 def test_attention_vs_torch(variant, S, Sq):
     err = _run(variant, 6, S, Sq, heads=3, seed=S * 7 + Sq)
@@ -53,6 +53,38 @@ def test_attention_vs_torch(variant, S, Sq):
 def test_attention_single_key_rows():
     import torch
     lens = torch.tensor([1, 1, 2, 128], device="cuda")
-    for variant in (0, 1, 2, -1):
+    for variant in (0, 1, 2, 3, -1):
         err = _run(variant, 4, 128, 128, heads=2, seed=3, lens=lens)
         assert err <= 4e-3, f"variant {variant}: max|err| {err:.3e}"
+
+
+@pytest.mark.parametrize("S,Sq", [(512, 512), (500, 500), (512, 481)])
+def test_attention_k5d_persistent_walkers(S, Sq):
+    # K5d (auto at S_pad = 512, every query): 600 (sequence, head) tiles over 256 walkers, so
+    # walkers take 2-3 tiles and every key block, query panel and key bias is refilled from the
+    # next tile during pass B; ragged lengths per sequence.  Must equal K5b STREAM (variant 3) bit
+    # for bit (same block code and operation order) and the torch reference within 4e-3.
+    import torch
+    from super_rag_amd import _native as NT
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(S + Sq)
+    B, heads, dh = 150, 4, 64
+    d = heads * dh
+    qkv = (torch.randn(B * S, 3 * d, device=dev, generator=g) * 1.5).half()
+    lens = torch.randint(1, S + 1, (B,), device=dev, generator=g)
+    lens[::7] = S
+    mask = (torch.arange(S, device=dev)[None] < lens[:, None]).int().contiguous()
+    outs = {}
+    for variant in (3, -1):
+        ctx = torch.full((B * Sq, d), float("nan"), device=dev, dtype=torch.float16)
+        NT.call("sr_diag_attention", variant, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), B, S,
+                Sq, d, heads, 0, torch.cuda.current_stream().cuda_stream)
+        outs[variant] = ctx
+    torch.cuda.synchronize()
+    assert torch.equal(outs[-1], outs[3])
+    x = qkv.float().view(B, S, 3, heads, dh)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    sc = q @ k.transpose(-1, -2) / dh ** 0.5
+    sc = sc.masked_fill(mask[:, None, None, :] == 0, float("-inf"))
+    ref = (torch.softmax(sc, -1) @ v).transpose(1, 2)[:, :Sq].reshape(B * Sq, d)
+    assert (outs[-1].float() - ref).abs().max().item() <= 4e-3

@@ -30,11 +30,14 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     byt = 2.0 * a.B * a.S * 3 * d + 2.0 * a.B * a.Sq * d
     fl = 4.0 * a.B * a.heads * a.Sq * a.S * 64
-    res = {0: [], 1: [], 2: [], -1: []}
+    res = {0: [], 1: [], 2: [], 3: [], -1: []}
     for _ in range(3):
-        for v in (0, 1, 2, -1):
-            N.call("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B, a.S,
-                   a.Sq, d, a.heads, 0, st)
+        for v in (0, 1, 2, 3, -1):
+            try:
+                N.call("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B,
+                       a.S, a.Sq, d, a.heads, 0, st)
+            except N.NativeError:  # an older library without this variant
+                continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
@@ -44,6 +47,8 @@ def main():
             torch.cuda.synchronize()
             res[v].append(e0.elapsed_time(e1) / a.reps)
     for v, ms in res.items():
+        if not ms:
+            continue
         ms.sort()
         m = ms[len(ms) // 2]
         print(f"attention v{v} B={a.B} S={a.S} Sq={a.Sq}: {m:.3f} ms  {byt / m / 1e6:.0f} GB/s  "
