@@ -563,30 +563,95 @@ struct PipeEpi {
 // rows with sim >= tau[q] are appended to q's candidate list (cap entries, overflow counted).
 // Reading the rows' live flags here cost a load per row per tile on the critical path (and VGPRs
 // the fp8 main loop needs): the selection filters tombstoned rows instead.
-__device__ __forceinline__ void scan_epilogue(float4v (&acc)[8][4], int nw0, int mw0, int lane, int B,
-                                              int nrows, const float* __restrict__ tau,
-                                              const uint8_t* __restrict__ live,
+// tau of the lane's 4 query columns from the workgroup's LDS copy (written once per launch by
+// scan_tau_table; q >= B holds +inf).  Loading them from global memory in the epilogue made the
+// wait (vmcnt counts in order) also wait for the next tile's 32 in-flight staging pieces, and
+// holding them in VGPRs across the last K-step spilled.
+__device__ __forceinline__ void scan_tau(float (&t)[4], int mw0, int lane, const float* tau_lds) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t[j] = tau_lds[mw0 + 16 * j + (lane & 15)];
+}
+
+__device__ __forceinline__ void scan_epilogue(float4v (&acc)[8][4], const float (&t)[4], int nw0,
+                                              int mw0, int lane, int nrows,
                                               uint64_t* __restrict__ cand, int cap, const LnFold& lf) {
-  float t[4];
+  // Fast rejection: almost every tile of a threshold chunk has no key above tau, and testing the
+  // 128 values one by one cost a compare + exec-mask branch each (~3k cycles per wave per tile,
+  // as long as the fp8 tile's main loop).  A v_max3 tree per query column decides it in ~45 VALU;
+  // only lanes holding a hit take the exact per-value path below (same keys).  Rows past nrows
+  // (zero-padded by the staging; only in a chunk's last tile) are masked out of the maxima.
+  bool hit = false;
+  if (nw0 + 128 <= nrows) {  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mx = acc[0][j][0];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = (i == 0 ? 1 : 0); r < 4; ++r) mx = fmaxf(mx, acc[i][j][r]);
+      hit |= mx >= t[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int nb = nw0 + 16 * i + 4 * (lane_id_here() >> 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, nb + r < nrows ? acc[i][j][r] : -INFINITY);
+      }
+      hit |= mx >= t[j];
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(hit) == 0) return;  // wave-uniform: no key in this wave's tile
+  // lane-derived offsets re-derived here (kept live from the kernel's prologue, the fp8 kernel
+  // spilled one and its reload waited vmcnt(0) on the next tile's staging every tile)
+  lane = lane_id_here();
+  const int g = lane >> 4;
+  int* const cnt = reinterpret_cast<int*>(lf.stat_out);
+  // Slot reservation: one returning atomic per (query column, wave) instead of one per key.  In
+  // the early threshold chunks (tau still loose) most tiles hold keys, and the per-key atomics,
+  // each awaited before its store, serialised on the 256 shared counters (a 65k-row chunk took
+  // 200 us for one tile per CU).  The 4 lanes of a query column (lane & 15 equal, g = 0..3) add
+  // their counts by two xor-shuffles; lane g = 0 reserves the column's range; each lane writes its
+  // keys from base + (keys of the lanes g' < g).  Counts, overflow and the key set are unchanged.
+  int c[4], pre[4], base[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int q = mw0 + 16 * j + (lane & 15);
-    t[j] = q < B ? tau[q] : INFINITY;
+    c[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int nb = nw0 + 16 * i + 4 * g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c[j] += (nb + r < nrows && acc[i][j][r] >= t[j]) ? 1 : 0;
+    }
+    const int x1 = __shfl_xor(c[j], 16, 64);
+    const int s2 = c[j] + x1;
+    const int x2 = __shfl_xor(s2, 32, 64);
+    pre[j] = ((g & 1) ? x1 : 0) + ((g & 2) ? x2 : 0);
+    c[j] = s2 + x2;  // the column's total from here on
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // the 4 reservations in flight together
+    base[j] = 0;
+    if (g == 0 && c[j] > 0) base[j] = atomicAdd(cnt + mw0 + 16 * j + (lane & 15), c[j]);
   }
   // (no live flags here: tombstoned rows' keys are dropped by the selection, topk_select)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int nb = nw0 + 16 * i + 4 * (lane >> 4);
+  for (int j = 0; j < 4; ++j) {
+    if (c[j] == 0) continue;  // no key in this column (any lane): skip the broadcast too
+    const int q = mw0 + 16 * j + (lane & 15);
+    int pos = __shfl(base[j], lane & 15, 64) + pre[j];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (nb + r >= nrows) continue;
+    for (int i = 0; i < 8; ++i) {
+      const int nb = nw0 + 16 * i + 4 * g;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int r = 0; r < 4; ++r) {
         const float sim = acc[i][j][r];
-        if (sim >= t[j]) {  // false for padded queries (t = inf)
-          const int q = mw0 + 16 * j + (lane & 15);
-          const int pos = atomicAdd(reinterpret_cast<int*>(lf.stat_out) + q, 1);
+        if (nb + r < nrows && sim >= t[j]) {  // false for padded queries (t = inf)
           if (pos < cap) cand[(int64_t)q * cap + pos] = make_key(sim, (uint32_t)(lf.stat_ld + nb + r));
+          ++pos;
         }
       }
     }
@@ -663,7 +728,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
   constexpr bool LINE = SR_GEMM_LINE_STORE && PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 &&
                         (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0)];
+  // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (SCAN ? 512 : 0)];
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -764,6 +830,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   if (PERSIST && lf.stagger > 0) {  // de-phase the walkers of an XCD (their store bursts)
     const int n_sleep = ((blockIdx.x >> 3) & 7) * lf.stagger;
     for (int i = 0; i < n_sleep; ++i) __builtin_amdgcn_s_sleep(8);
+  }
+  float* const tau_lds = reinterpret_cast<float*>(lds + 2 * STAGE);
+  if constexpr (SCAN) {  // tau table (bias = tau, M = B <= 256, host-checked); the prologue's
+                         // barrier publishes it
+    for (int q = tid; q < 256; q += blockDim.x) tau_lds[q] = q < M ? bias[q] : INFINITY;
   }
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
@@ -1009,8 +1080,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
       if (sacc == 12345.678f) reinterpret_cast<float*>(Y)[tid] = sacc;
     } else if constexpr (SCAN) {
-      scan_epilogue(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                    reinterpret_cast<const uint8_t*>(R), reinterpret_cast<uint64_t*>(Y), (int)ldy, lf);
+      float tq[4];
+      scan_tau(tq, m0 + wm * 64, lane, tau_lds);
+      scan_epilogue(acc, tq, n0 + wn * 128, m0 + wm * 64, lane, N, reinterpret_cast<uint64_t*>(Y),
+                    (int)ldy, lf);
     } else if (full) {
       PipeEpi<EPI_OUT>::template run<false, LINE>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                   R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048);
