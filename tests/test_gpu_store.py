@@ -276,3 +276,44 @@ def test_fp8_scan_rescored_matches_fp16(dim, B, k):
     s8.set_scan_dtype("fp16")
     d, r = s8.search(q, k)
     np.testing.assert_array_equal(r, r16c)
+
+
+@pytest.mark.parametrize("scan", ["fp16", "fp8"])
+def test_gemm_scan_key_buffer_overflow_near_identical_queries(scan):
+    # K1 on the GEMM main loop (B > 128 fp16, B > 64 fp8) collects each workgroup's keys in an
+    # LDS buffer and appends them once per launch; lanes whose keys no longer fit go to the global
+    # lists directly.  Near-identical queries (as a random-weight embedder produces) hit the same
+    # rows together and k = 1000 keeps tau loose, so workgroups overflow the buffer mid-launch with
+    # reservations straddling its end (a flush that read the unwritten tail of such a
+    # reservation returned garbage rows).  Every result row must be a real row and the top-k the
+    # oracle's.
+    dim, n, B, k = 768, 600_000, 256, 1000
+    x = _clustered(n, dim, seed=41)
+    rng = np.random.default_rng(42)
+    v = rng.standard_normal((2, dim)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    q = v[np.arange(B) % 2] + 1e-3 * rng.standard_normal((B, dim)).astype(np.float32)
+    s = _store(dim)
+    s.add(x)
+    if scan == "fp8":
+        s.set_scan_dtype("fp8")
+    d, r = s.search(q, k)
+    assert ((r >= 0) & (r < n)).all()
+    assert (np.diff(d, axis=1) >= -1e-7).all()
+    # oracle on two of the queries (one per direction) over the stored rows
+    stored = s.get(np.arange(n)).astype(np.float64)
+    pick = np.array([0, 1])
+    qq = quantize_like_store(q[pick]).astype(np.float64)
+    d_ref, r_ref = cosine_topk(stored, qq, k, normalize=False)
+    if scan == "fp16":
+        s_ref = 1.0 - d_ref
+        s_gpu = 1.0 - d[pick].astype(np.float64)
+        assert same_topk_modulo_ties(r[pick], s_gpu, r_ref, s_ref, EPS)
+        np.testing.assert_allclose(d[pick], d_ref, atol=EPS)
+    else:  # fp8 stage + exact re-scoring: exact distances of the returned rows; recall is an fp8
+        # fidelity property here, not the buffer's: at k = 1000 the fp8 stage keeps only
+        # kk = SR_MAX_TOPK = 1024 candidates, and random query directions against the clustered
+        # corpus score near 0 where e4m3 noise reorders neighbours (measured 0.96)
+        assert recall_at_k(r[pick], r_ref) >= 0.9
+        sims = stored[r[pick]] @ qq[:, :, None]
+        np.testing.assert_allclose(d[pick], 1.0 - sims[..., 0], atol=EPS)
