@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2),
                     help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
                          "e4m3 residual copies (dtype f16+fp8ffn / f16+fp8gemm)")
+    ap.add_argument("--replicate-passages", action="store_true",
+                    help="N > 1: keep the whole passage token table on every rank (default: each "
+                         "rank holds its shard's rows, the candidates' rows are fetched per batch, "
+                         "SearchPipeline shard_passages / C3)")
     ap.add_argument("--dist-backend", default=os.environ.get("SR_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     a = ap.parse_args()
@@ -199,7 +203,8 @@ def main():
     torch.cuda.synchronize()
     if a.workload == "config5":
         store.set_scan_dtype("fp8")   # config 5: the fp8 MFMA scan (exact fp16 re-scoring)
-    # replicated passage token table for the cross-encoder (content tokens, no specials)
+    # passage token table for the cross-encoder (content tokens, no specials), generated whole so
+    # every world size sees the same tokens; at N > 1 each rank keeps only its shard's rows
     gp = torch.Generator(device=dev)
     gp.manual_seed(5)
     p_tok = torch.randint(1000, rs.vocab_size, (N_total, a.passage_len), generator=gp, device=dev,
@@ -222,9 +227,13 @@ def main():
         qlen = torch.full((a.batch,), lq, dtype=torch.int32, device=dev)
         batches.append((ids, mask, qtok, qlen))
     lexical = build_lexical(p_tok[r0:r1], p_len[r0:r1], local) if a.workload == "config5" else None
+    shard_p = world > 1 and not a.replicate_passages
+    if shard_p:
+        p_tok, p_len = p_tok[r0:r1].clone(), p_len[r0:r1].clone()
+        torch.cuda.empty_cache()
     pipe = SearchPipeline(embedder, reranker, store, p_tok, p_len, k_candidates=a.k_cand,
                           k_final=a.k, pair_len=a.pair_len, shard_offset=r0, lexical=lexical,
-                          k_each=a.k_cand)
+                          k_each=a.k_cand, shard_passages=shard_p)
     setup_s = time.time() - t_setup
 
     # ---- warmup + timed region -----------------------------------------------------------------
@@ -367,7 +376,8 @@ def main():
         "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
                    "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
-                   "parallelism": f"corpus row-shard x{world}, query DP x{world}"},
+                   "parallelism": f"corpus row-shard x{world}, query DP x{world}",
+                   "passages": "sharded (C3 fetch)" if shard_p else "replicated"},
         "recall_at_10": recall,
         **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
         "roofline": roof,

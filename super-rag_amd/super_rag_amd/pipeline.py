@@ -7,8 +7,11 @@ flag check.  With torch.distributed initialised (one process per GPU, backend "n
 xGMI) the corpus is row-sharded: each rank embeds its own B queries, the query embeddings are
 all-gathered (C1), every rank scans its shard for all world*B queries, the per-shard top-K lists
 are exchanged with one all_to_all (C2: each rank receives the lists of ITS queries) and merged by
-K2, and each rank reranks its own B queries.  Passage tokens for the cross-encoder are replicated
-per GPU (N x Lp int32, 3.8 GB at 10M x 94) so the pair packer never crosses ranks.
+K2, and each rank reranks its own B queries.  Passage tokens for the cross-encoder are either
+replicated per GPU (N x Lp int32: 3.8 GB at 10M x 94, 18.8 GB at 50M) or, with
+``shard_passages=True``, held per shard like the rows (passage_tok = the shard's rows) and the
+candidates' tokens fetched from their owning ranks per batch (C3: all_gather of the candidate ids,
+one all_to_all of the owned token rows, world * B * K * Lp * 4 bytes per rank: 77 MB at 8 ranks).
 
 Hybrid mode (``lexical=`` a NativeLexIndex over the shard's rows, BASELINE config 5): the rerank
 candidates are the rrf fusion (graphiti rrf, search_utils.py:1762-1778) of the dense top-k_each and
@@ -40,7 +43,7 @@ class SearchPipeline:
                  passage_tok: torch.Tensor, passage_len: torch.Tensor, k_candidates: int = 100,
                  k_final: int = 10, pair_len: int = 128, shard_offset: int = 0, group=None,
                  merge_fn=topk_merge_dev, lexical=None, k_each: int | None = None,
-                 rank_const: int = 1, force_exchange: bool = False):
+                 rank_const: int = 1, force_exchange: bool = False, shard_passages: bool = False):
         self.embedder = embedder
         self.reranker = reranker
         self.store = store
@@ -61,6 +64,8 @@ class SearchPipeline:
         # force_exchange: run the collectives even in a world of one (the RCCL calls of the
         # sharded path exercised on a one-GPU box)
         self.exchange = self.world > 1 or bool(force_exchange)
+        # passage_tok / passage_len hold only rows [shard_offset, shard_offset + len) (C3 fetch)
+        self.shard_passages = bool(shard_passages) and self.exchange
 
     def embed(self, q_ids: torch.Tensor, q_mask: torch.Tensor) -> torch.Tensor:
         return self.embedder.embed_dev(q_ids, q_mask, fp16=True)
@@ -141,9 +146,44 @@ class SearchPipeline:
         score, fused = rrf_fuse_dev(rows, lrows, self.K, self.rank_const)
         return score.float(), fused
 
+    def passages(self, cand_rows: torch.Tensor):
+        """(token table, lengths, [B, K] indices into them) for this rank's candidates (global
+        rows, -1 = none).  Replicated: the full table and the rows themselves.  Sharded (C3): the
+        candidate ids of every rank are all-gathered, each rank copies the token rows it owns
+        (zeros elsewhere) into the slots of the asking rank, one all_to_all returns every rank its
+        candidates' rows from all owners, and the sum over sources (exactly one owner per row)
+        is the compact [B * K, Lp] table of this rank's candidates."""
+        if not self.shard_passages:
+            return self.p_tok, self.p_len, cand_rows
+        import torch.distributed as dist
+        B, K = cand_rows.shape
+        dev = cand_rows.device
+        host = dist.get_backend(self.group) == "gloo" and cand_rows.is_cuda
+        rx = cand_rows.contiguous().cpu() if host else cand_rows.contiguous()
+        allr = torch.empty((self.world * B, K), dtype=rx.dtype, device=rx.device)
+        dist.all_gather_into_tensor(allr, rx, group=self.group)
+        allr = allr.to(self.p_tok.device)
+        loc = allr - self.offset
+        own = (allr >= 0) & (loc >= 0) & (loc < self.p_tok.shape[0])
+        li = torch.where(own, loc, torch.zeros_like(loc))
+        tok = self.p_tok[li] * own.unsqueeze(-1).to(self.p_tok.dtype)   # [world*B, K, Lp]
+        ln = self.p_len[li] * own.to(self.p_len.dtype)                   # [world*B, K]
+        if host:
+            tok, ln = tok.cpu(), ln.cpu()
+        rt, rl = torch.empty_like(tok), torch.empty_like(ln)
+        dist.all_to_all_single(rt, tok, group=self.group)
+        dist.all_to_all_single(rl, ln, group=self.group)
+        Lp = tok.shape[-1]
+        tq = rt.view(self.world, B * K, Lp).sum(0, dtype=self.p_tok.dtype).to(dev)
+        lq = rl.view(self.world, B * K).sum(0, dtype=self.p_len.dtype).to(dev)
+        idx = torch.arange(B * K, device=dev, dtype=cand_rows.dtype).view(B, K)
+        idx = torch.where(cand_rows >= 0, idx, torch.full_like(idx, -1))
+        return tq, lq, idx
+
     def rerank(self, q_tok: torch.Tensor, q_len: torch.Tensor, cand_rows: torch.Tensor):
         B = cand_rows.shape[0]
-        ids, mask, types = build_pairs_dev(q_tok, q_len, self.p_tok, self.p_len, cand_rows, self.S,
+        p_tok, p_len, prow = self.passages(cand_rows)
+        ids, mask, types = build_pairs_dev(q_tok, q_len, p_tok, p_len, prow, self.S,
                                            self.reranker.spec,
                                            with_types=self.reranker.spec.pair_style == 1)
         logits = self.reranker.cross_score_dev(ids, mask, types)[:, 0].view(B, self.K)

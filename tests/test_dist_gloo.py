@@ -76,3 +76,52 @@ def test_sharded_retrieve_matches_single_process(world):
         s, rows = res[r]
         assert np.array_equal(rows, full_r[r * B:(r + 1) * B].numpy())
         np.testing.assert_allclose(s, full_s[r * B:(r + 1) * B].numpy(), atol=1e-6)
+
+
+def _passage_worker(rank, world, port, p_tok, p_len, cand, out_q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "super-rag_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from super_rag_amd.pipeline import SearchPipeline
+    n = p_tok.shape[0]
+    per = (n + world - 1) // world
+    r0, r1 = rank * per, min(n, (rank + 1) * per)
+    pipe = SearchPipeline(None, None, None, p_tok[r0:r1].clone(), p_len[r0:r1].clone(),
+                          k_candidates=cand.shape[-1], shard_offset=r0, shard_passages=True)
+    tq, lq, idx = pipe.passages(cand[rank])
+    out_q.put((rank, tq.numpy(), lq.numpy(), idx.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_passage_fetch_equals_replicated_table(world):
+    # C3 (SearchPipeline.passages, shard_passages=True): every rank holds only its shard's
+    # passage rows; the candidates' token rows fetched from their owners (all_gather of the ids,
+    # one all_to_all) must equal a gather from the full table, -1 candidates staying -1
+    g = torch.Generator().manual_seed(3)
+    n, Lp, B, K = 1003, 9, 5, 7
+    p_tok = torch.randint(5, 3000, (n, Lp), generator=g, dtype=torch.int32)
+    p_len = torch.randint(0, Lp + 1, (n,), generator=g, dtype=torch.int32)
+    cand = torch.randint(0, n, (world, B, K), generator=g, dtype=torch.int64)
+    cand[:, 0, -2:] = -1          # short result lists
+    cand[:, 1, :] = n - 1         # the last row (last shard) for every slot
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000 + 11 * world
+    procs = [ctx.Process(target=_passage_worker, args=(r, world, port, p_tok, p_len, cand, out_q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (t, l, i)) for r, t, l, i in (out_q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        tq, lq, idx = res[r]
+        c = cand[r].numpy()
+        assert np.array_equal(idx < 0, c < 0)
+        ok = c >= 0
+        np.testing.assert_array_equal(tq[idx[ok]], p_tok.numpy()[c[ok]])
+        np.testing.assert_array_equal(lq[idx[ok]], p_len.numpy()[c[ok]])

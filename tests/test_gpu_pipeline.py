@@ -127,7 +127,8 @@ def _sharded_worker(rank, world, port, out_q):
         torch.cuda.set_device(0)
         res = _run_pipeline(rank, world)
         res_h = _run_pipeline(rank, world, hybrid=True)
-        out_q.put((rank, (res, res_h)))
+        res_p = _run_pipeline(rank, world, shard_passages=True)
+        out_q.put((rank, (res, res_h, res_p)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -149,7 +150,8 @@ def _rccl_worker(port, out_q):
         assert dist.get_backend() == "nccl"
         res = _run_pipeline(0, 1, force_exchange=True)
         res_h = _run_pipeline(0, 1, hybrid=True, force_exchange=True)
-        out_q.put((res, res_h))
+        res_p = _run_pipeline(0, 1, force_exchange=True, shard_passages=True)
+        out_q.put((res, res_h, res_p))
     finally:
         dist.destroy_process_group()
 
@@ -161,16 +163,16 @@ def test_rccl_exchange_world_one_equals_plain_path():
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(29500 + os.getpid() % 150, q))
     p.start()
-    res, res_h = q.get(timeout=240)
+    res, res_h, res_p = q.get(timeout=240)
     p.join(timeout=60)
     assert p.exitcode == 0
     plain, plain_h = _run_pipeline(0, 1), _run_pipeline(0, 1, hybrid=True)
-    for got, want in ((res, plain), (res_h, plain_h)):
+    for got, want in ((res, plain), (res_h, plain_h), (res_p, plain)):
         for f in ("rows", "cand_rows", "cand_sims", "logits"):
             np.testing.assert_array_equal(got[f], want[f])
 
 
-def _run_pipeline(rank, world, sharded=True, hybrid=False, force_exchange=False):
+def _run_pipeline(rank, world, sharded=True, hybrid=False, force_exchange=False, shard_passages=False):
     # rank's B queries; sharded: over rows [r0, r1) of the corpus (shard_offset r0) inside a
     # world-size process group, else over the whole corpus in a single process
     import torch
@@ -204,9 +206,12 @@ def _run_pipeline(rank, world, sharded=True, hybrid=False, force_exchange=False)
         lex = NativeLexIndex()
         lex.add([(p_tok[i, :p_len[i]] % 97 + 5).tolist() for i in range(r0, r1)])
         q_tok = q_tok % 97 + 5
-    pipe = SearchPipeline(emb, rer, store, t(p_tok), t(p_len), k_candidates=K, k_final=k,
+    # shard_passages: this rank holds only its shard's passage rows; the C3 fetch brings the
+    # candidates' rows from their owners
+    pt, pl = (p_tok[r0:r1], p_len[r0:r1]) if shard_passages else (p_tok, p_len)
+    pipe = SearchPipeline(emb, rer, store, t(pt), t(pl), k_candidates=K, k_final=k,
                           pair_len=S, shard_offset=r0, lexical=lex, k_each=16 if hybrid else None,
-                          force_exchange=force_exchange)
+                          force_exchange=force_exchange, shard_passages=shard_passages)
     mine = slice(rank * B, (rank + 1) * B)
     res = pipe.run(t(q_ids[mine]), t(np.ones_like(q_ids[mine])), t(q_tok[mine]), t(q_len[mine]))
     torch.cuda.synchronize()
@@ -229,6 +234,7 @@ def test_two_rank_sharded_pipeline_equals_single_process():
     got_both = dict(q.get(timeout=240) for _ in range(world))
     got = {r: v[0] for r, v in got_both.items()}
     got_h = {r: v[1] for r, v in got_both.items()}
+    got_p = {r: v[2] for r, v in got_both.items()}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -247,6 +253,9 @@ def test_two_rank_sharded_pipeline_equals_single_process():
         np.testing.assert_allclose(got[r]["cand_sims"], full[r]["cand_sims"], atol=1e-6)
         np.testing.assert_array_equal(got[r]["rows"], full[r]["rows"])
         np.testing.assert_allclose(got[r]["logits"], full[r]["logits"], atol=1e-5)
+        # sharded passage tokens (C3 fetch) == the replicated table, bit for bit
+        for f in ("rows", "cand_rows", "cand_sims", "logits"):
+            np.testing.assert_array_equal(got_p[r][f], got[r][f])
 
 
 def test_bench_launches_its_own_ranks():
