@@ -119,6 +119,28 @@ int sr_store_load(const char* path, int device, sr_store** out);
 int sr_store_compact(sr_store* s, int64_t* old_to_new);
 void sr_store_destroy(sr_store* s);
 
+/* ------------------------------------------------------------------------------------------------
+ * Multi-device collection: SURVEY §8(b)'s sr_store_create(dim, dtype, devices, n_dev) — the
+ * reference configures one vector DB per deployment (super_rag/config.py:65-67, adaptor
+ * vectorstore/connector.py:4-15); here a collection is row-sharded over the listed devices (the
+ * same device may repeat).  Global row ids are the insertion order across shards (each add batch
+ * goes to the shard with the fewest rows), so every result equals one sr_store's bit for bit:
+ * shards are searched concurrently (K1 + K2 on each device) and merged by (dist asc, row asc).
+ * dtype: SR_DTYPE_F16, or SR_DTYPE_FP8_E4M3 for the fp8 scan copy (sr_store_set_scan_dtype).
+ * Snapshots, compaction and the device-buffer entry points stay per shard (sr_store_*; the Python
+ * connector's ShardedStore composes them). */
+typedef struct sr_store_set sr_store_set;
+int sr_store_set_create(int dim, int dtype, const int* devices, int n_dev, sr_store_set** out);
+int sr_store_set_add(sr_store_set* s, const float* vecs, int64_t n, int64_t* out_rows);
+int sr_store_set_remove(sr_store_set* s, const int64_t* rows, int64_t n);
+int sr_store_set_count(sr_store_set* s, int64_t* n_rows, int64_t* n_live, int* n_shards);
+int sr_store_set_get(sr_store_set* s, const int64_t* rows, int64_t n, float* out);
+/* sr_store_search semantics; allow (host, n_rows bytes) may be NULL, else as sr_store_search_masked. */
+int sr_store_set_search(sr_store_set* s, const float* q, int B, int k, const uint8_t* allow,
+                        int64_t mask_key, float* out_dist, int64_t* out_rows);
+int sr_store_set_set_scan_dtype(sr_store_set* s, int dtype);
+void sr_store_set_destroy(sr_store_set* s);
+
 /* Merge P per-shard top-k lists (device buffers P x B x k of similarity and global row, as written
  * by sr_store_search_dev) into one B x k_out list per query, on `device`. */
 int sr_topk_merge_dev(const float* sims, const int64_t* rows, int P, int B, int k, int k_out,

@@ -17,6 +17,9 @@ struct sr_encoder {
 struct sr_lex {
   sr::LexIndex* impl;
 };
+struct sr_store_set {
+  sr::StoreSet* impl;
+};
 
 namespace sr {
 
@@ -280,6 +283,73 @@ int sr_store_compact(sr_store* s, int64_t* old_to_new) {
 }
 
 void sr_store_destroy(sr_store* s) {
+  if (!s) return;
+  delete s->impl;
+  delete s;
+}
+
+// ---- multi-device collection (SURVEY 8(b) sr_store_create(dim, dtype, devices, n_dev)) ---------
+int sr_store_set_create(int dim, int dtype, const int* devices, int n_dev, sr_store_set** out) {
+  SR_API_BEGIN
+  SR_NONNULL(out);
+  SR_NONNULL(devices);
+  *out = nullptr;
+  *out = new sr_store_set{new sr::StoreSet(dim, dtype, devices, n_dev)};
+  SR_API_END
+}
+
+int sr_store_set_add(sr_store_set* s, const float* vecs, int64_t n, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->add_host(vecs, n, out_rows);
+  SR_API_END
+}
+
+int sr_store_set_remove(sr_store_set* s, const int64_t* rows, int64_t n) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->remove(rows, n);
+  SR_API_END
+}
+
+int sr_store_set_count(sr_store_set* s, int64_t* n_rows, int64_t* n_live, int* n_shards) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  if (n_rows) *n_rows = s->impl->rows();
+  if (n_live) *n_live = s->impl->live();
+  if (n_shards) *n_shards = s->impl->shards();
+  SR_API_END
+}
+
+int sr_store_set_get(sr_store_set* s, const int64_t* rows, int64_t n, float* out) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->get(rows, n, out);
+  SR_API_END
+}
+
+int sr_store_set_search(sr_store_set* s, const float* q, int B, int k, const uint8_t* allow,
+                        int64_t mask_key, float* out_dist, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->search_host(q, B, k, out_dist, out_rows, allow, allow ? mask_key : 0);
+  SR_API_END
+}
+
+int sr_store_set_set_scan_dtype(sr_store_set* s, int dtype) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->set_scan_dtype(dtype);
+  SR_API_END
+}
+
+void sr_store_set_destroy(sr_store_set* s) {
   if (!s) return;
   delete s->impl;
   delete s;

@@ -1,6 +1,8 @@
 // Host runtime objects behind the C-ABI: the in-HBM vector store and the transformer encoder.
 #pragma once
 
+#include <memory>
+
 #include <map>
 #include <mutex>
 #include <string>
@@ -67,8 +69,10 @@ class Store {
   void remove(const int64_t* rows, int64_t n);
   void get(const int64_t* rows, int64_t n, float* out);
   // allow: optional host eligibility mask (n_rows bytes), cached on the device per mask_key
+  // raw_sim: out_dist receives the similarities (descending) instead of 1 - sim, for callers
+  // that merge lists (1 - sim in fp32 can merge two neighbouring similarities into one distance)
   void search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows,
-                   const uint8_t* allow = nullptr, int64_t mask_key = 0);
+                   const uint8_t* allow = nullptr, int64_t mask_key = 0, bool raw_sim = false);
   void search_dev(const void* q, int q_dtype, int B, int k, float* out_sim, int64_t* out_rows,
                   int64_t row_offset, hipStream_t s, const uint8_t* elig = nullptr);
   // device eligibility mask live & allow (cached per mask_key and store version); null for null
@@ -115,6 +119,34 @@ class Store {
   // filtered search: device eligibility mask (live & allow) and what it was built from
   DevBuf mask_;
   int64_t version_ = 0, mask_key_ = 0, mask_version_ = -1, mask_rows_ = -1;
+};
+
+// One collection row-sharded over several devices (store_set.cpp; C-ABI sr_store_set_*).
+class StoreSet {
+ public:
+  StoreSet(int dim, int dtype, const int* devices, int n_dev);
+  int dim() const { return dim_; }
+  int shards() const { return (int)shards_.size(); }
+  int64_t rows() const;
+  int64_t live() const;
+  void add_host(const float* vecs, int64_t n, int64_t* out_rows);
+  void remove(const int64_t* rows, int64_t n);
+  void get(const int64_t* rows, int64_t n, float* out);
+  void search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows,
+                   const uint8_t* allow = nullptr, int64_t mask_key = 0);
+  void set_scan_dtype(int dtype);
+
+  std::mutex mu;
+
+ private:
+  // rows -> per-shard local rows and their positions in the argument
+  void split(const int64_t* rows, int64_t n, std::vector<std::vector<int64_t>>& local,
+             std::vector<std::vector<int64_t>>& pos) const;
+  int dim_;
+  std::vector<std::unique_ptr<Store>> shards_;
+  std::vector<std::vector<int64_t>> tables_;  // per shard: local row -> global row
+  std::vector<int32_t> shard_of_;             // global row -> shard
+  std::vector<int64_t> local_of_;             // global row -> local row
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -405,7 +405,7 @@ const uint8_t* Store::eligibility(const uint8_t* allow, int64_t mask_key) {
 }
 
 void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* out_rows,
-                        const uint8_t* allow, int64_t mask_key) {
+                        const uint8_t* allow, int64_t mask_key, bool raw_sim) {
   SR_CHECK(B >= 0 && (B == 0 || (q && out_dist && out_rows)), "store.search: null buffer");
   if (B == 0) return;
   DeviceGuard g(device_);
@@ -421,6 +421,7 @@ void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* 
   SR_HIP(hipMemcpyAsync(out_dist, dsim, (size_t)B * k * sizeof(float), hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipMemcpyAsync(out_rows, drows, (size_t)B * k * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipStreamSynchronize(stream_));
+  if (raw_sim) return;
   for (int64_t i = 0; i < (int64_t)B * k; ++i)
     out_dist[i] = out_rows[i] >= 0 ? 1.0f - out_dist[i] : INFINITY;
 }

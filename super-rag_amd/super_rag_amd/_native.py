@@ -80,6 +80,15 @@ SIGNATURES = {
     "sr_store_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
     "sr_store_compact": (c_int, [c_void_p, c_void_p]),
     "sr_store_destroy": (None, [c_void_p]),
+    "sr_store_set_create": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
+    "sr_store_set_add": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "sr_store_set_remove": (c_int, [c_void_p, c_void_p, c_int64]),
+    "sr_store_set_count": (c_int, [c_void_p, P_I64, P_I64, P_I32]),
+    "sr_store_set_get": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "sr_store_set_search": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p,
+                                    c_void_p]),
+    "sr_store_set_set_scan_dtype": (c_int, [c_void_p, c_int]),
+    "sr_store_set_destroy": (None, [c_void_p]),
     "sr_lex_create": (c_int, [c_int, c_float, c_float, POINTER(c_void_p)]),
     "sr_lex_add": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, P_I64]),
     "sr_lex_remove": (c_int, [c_void_p, c_void_p, c_int64]),

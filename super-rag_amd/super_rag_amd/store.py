@@ -151,6 +151,86 @@ def topk_merge_dev(sims, rows, k_out: int, device: int = 0, stream=None):
     return out_sim, out_rows
 
 
+class NativeStoreSet:
+    """One collection row-sharded over several devices behind ONE native handle
+    (sr_store_set_*, SURVEY §8(b)'s sr_store_create(dim, dtype, devices, n_dev)): the library keeps
+    one in-HBM store per listed device, hands out global row ids in insertion order, searches the
+    shards concurrently and merges by (distance asc, row asc) — results equal one NativeStore's.
+    Host-buffer interface (add / remove / get / count / search with an optional allow mask);
+    snapshots, compaction and the device-buffer paths stay with ShardedStore / NativeStore."""
+
+    def __init__(self, dim: int, devices, dtype: str = "fp16"):
+        N.require_gpu()
+        devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+        if devs.size == 0:
+            raise ValueError("NativeStoreSet needs at least one device")
+        code = {"fp16": N.SR_DTYPE_F16, "fp8": N.SR_DTYPE_FP8_E4M3}[dtype]
+        self._h = None
+        h = ctypes.c_void_p()
+        N.call("sr_store_set_create", int(dim), code, N.ptr(devs), int(devs.size), ctypes.byref(h))
+        self._h = h
+        self.dim = int(dim)
+        self.devices = [int(d) for d in devs]
+
+    def close(self) -> None:
+        if self._h:
+            N.load().sr_store_set_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, vecs) -> np.ndarray:
+        v = np.ascontiguousarray(np.asarray(vecs, dtype=np.float32))
+        if v.ndim != 2 or v.shape[1] != self.dim:
+            raise ValueError(f"expected (n, {self.dim}) vectors, got {v.shape}")
+        rows = np.empty(v.shape[0], dtype=np.int64)
+        N.call("sr_store_set_add", self._h, N.ptr(v), int(v.shape[0]), N.ptr(rows))
+        return rows
+
+    def remove(self, rows) -> None:
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int64))
+        N.call("sr_store_set_remove", self._h, N.ptr(r), int(r.size))
+
+    def count(self):
+        n, live, sh = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+        N.call("sr_store_set_count", self._h, ctypes.byref(n), ctypes.byref(live), ctypes.byref(sh))
+        return int(n.value), int(live.value)
+
+    def get(self, rows) -> np.ndarray:
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int64))
+        out = np.empty((r.size, self.dim), dtype=np.float32)
+        N.call("sr_store_set_get", self._h, N.ptr(r), int(r.size), N.ptr(out))
+        return out
+
+    def set_scan_dtype(self, dtype: str) -> None:
+        N.call("sr_store_set_set_scan_dtype", self._h,
+               {"fp16": N.SR_DTYPE_F16, "fp8": N.SR_DTYPE_FP8_E4M3}[dtype])
+
+    def search(self, queries, k: int, allow=None, mask_key: int = 0):
+        q = np.ascontiguousarray(np.asarray(queries, dtype=np.float32))
+        if q.ndim == 1:
+            q = q[None]
+        if q.shape[1] != self.dim:
+            raise ValueError(f"query dim {q.shape[1]} != store dim {self.dim}")
+        B = q.shape[0]
+        dist = np.empty((B, k), dtype=np.float32)
+        rows = np.empty((B, k), dtype=np.int64)
+        a = None
+        if allow is not None:
+            n, _ = self.count()
+            a = np.ascontiguousarray(np.asarray(allow, dtype=np.uint8))
+            if a.shape != (n,):
+                raise ValueError(f"allow mask must have {n} entries, got {a.shape}")
+        N.call("sr_store_set_search", self._h, N.ptr(q), B, int(k),
+               N.ptr(a) if a is not None else None, int(mask_key) if a is not None else 0,
+               N.ptr(dist), N.ptr(rows))
+        return dist, rows
+
+
 class ShardedStore:
     """One collection row-sharded over several stores / devices (VECTOR_DB_CONTEXT "devices").
 

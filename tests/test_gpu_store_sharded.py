@@ -77,3 +77,55 @@ def test_connector_devices_ctx_matches_single_device(tmp_path):
     again.delete_collection()
     single.delete_collection()
     V._collections.clear()
+
+
+@pytest.mark.parametrize("dtype", ["fp16", "fp8"])
+def test_native_store_set_equals_single_store(dtype):
+    # ONE native handle over three shards (sr_store_set_*, SURVEY 8(b) sr_store_create(dim, dtype,
+    # devices, n_dev)); the same device listed three times runs the multi-GPU code on one card:
+    # concurrent per-shard K1 + K2 (one host thread per shard), global rows, host merge
+    from super_rag_amd.store import NativeStore, NativeStoreSet
+    dim = 384
+    x = _data(50_000, dim, 3)
+    one, st = NativeStore(dim), NativeStoreSet(dim, [0, 0, 0], dtype=dtype)
+    if dtype == "fp8":
+        one.set_scan_dtype("fp8")
+    for s, e in ((0, 9_000), (9_000, 9_001), (9_001, 30_000), (30_000, 41_000), (41_000, 50_000)):
+        assert one.add(x[s:e]).tolist() == st.add(x[s:e]).tolist()      # uneven batches
+    dup = np.repeat(x[7:8], 4, 0)
+    one.add(dup)
+    st.add(dup)                                                          # exact ties across shards
+    rows_all = np.arange(50_004)
+    assert np.array_equal(one.get(rows_all[::97]), st.get(rows_all[::97]))
+    q = _data(300, dim, 4)
+    q[0] = x[7]
+    for k in (1, 10, 100):
+        d1, r1 = one.search(q, k)
+        d2, r2 = st.search(q, k)
+        bad = np.argwhere(r1 != r2)
+        if bad.size:
+            b0, j0 = bad[0]
+            print("k", k, "first mismatch", b0, j0, "rows", r1[b0, j0 - 1:j0 + 2], r2[b0, j0 - 1:j0 + 2],
+                  "dist", d1[b0, j0 - 1:j0 + 2], d2[b0, j0 - 1:j0 + 2], "n bad", len(bad),
+                  "queries", np.unique(bad[:, 0])[:20])
+            s1 = dict(zip(r1[b0].tolist(), d1[b0].tolist()))
+            s2 = dict(zip(r2[b0].tolist(), d2[b0].tolist()))
+            print("dist of same rows differ:", [(r, s1[r], s2[r]) for r in s1 if r in s2 and s1[r] != s2[r]][:5])
+        np.testing.assert_array_equal(d1, d2)
+        np.testing.assert_array_equal(r1, r2)
+    dead = np.arange(1, 50_004, 7)
+    one.remove(dead)
+    st.remove(dead)
+    assert one.count() == st.count()
+    allow = (np.arange(50_004) % 3 != 0).astype(np.uint8)
+    for key in (0, 11, 11):                                              # cached mask reused
+        d1, r1 = one.search(q[:40], 20, allow=allow, mask_key=key)
+        d2, r2 = st.search(q[:40], 20, allow=allow, mask_key=key)
+        assert np.array_equal(r1, r2)
+        assert np.array_equal(d1, d2)
+    # short lists: k beyond the live rows of a tiny set
+    tiny = NativeStoreSet(dim, [0, 0], dtype=dtype)
+    tiny.add(x[:3])
+    d, r = tiny.search(q[:2], 5)
+    assert (r[:, 3:] == -1).all() and np.isinf(d[:, 3:]).all()
+    assert sorted(r[0, :3].tolist()) == [0, 1, 2]
