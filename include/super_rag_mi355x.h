@@ -98,6 +98,11 @@ int sr_store_search(sr_store* s, const float* q, int B, int k, float* out_dist, 
  * and the store contents are unchanged; mask_key 0 uploads it every call. */
 int sr_store_search_masked(sr_store* s, const float* q, int B, int k, const uint8_t* allow,
                            int64_t mask_key, float* out_dist, int64_t* out_rows);
+/* sr_store_search / sr_store_search_masked (allow may be NULL) returning the similarities
+ * (descending, -inf when missing) instead of 1 - sim: for callers that merge several stores' lists
+ * (two neighbouring fp32 similarities can round to one fp32 distance). */
+int sr_store_search_sim(sr_store* s, const float* q, int B, int k, const uint8_t* allow,
+                        int64_t mask_key, float* out_sim, int64_t* out_rows);
 /* Device variant: q is B x dim on the device (SR_DTYPE_F32 or SR_DTYPE_F16), out_sim/out_rows
  * device buffers of B x k (similarity = 1 - dist, rows int64; -1 / -inf when missing).
  * row_offset is added to every returned row (global row id of a shard).  Synchronises `stream`

@@ -231,6 +231,15 @@ int sr_store_search_masked(sr_store* s, const float* q, int B, int k, const uint
   SR_API_END
 }
 
+int sr_store_search_sim(sr_store* s, const float* q, int B, int k, const uint8_t* allow,
+                        int64_t mask_key, float* out_sim, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(s);
+  std::lock_guard<std::mutex> lk(s->impl->mu);
+  s->impl->search_host(q, B, k, out_sim, out_rows, allow, allow ? mask_key : 0, true);
+  SR_API_END
+}
+
 int sr_store_search_dev(sr_store* s, const void* q, int q_dtype, int B, int k, float* out_sim,
                         int64_t* out_rows, int64_t row_offset, void* stream) {
   SR_API_BEGIN

@@ -73,6 +73,8 @@ SIGNATURES = {
     "sr_store_search": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sr_store_search_masked": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p,
                                        c_void_p]),
+    "sr_store_search_sim": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p,
+                                    c_void_p]),
     "sr_store_search_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                     c_int64, c_void_p]),
     "sr_store_set_scan_dtype": (c_int, [c_void_p, c_int]),

@@ -123,6 +123,29 @@ class NativeStore:
                    N.ptr(dist), N.ptr(rows))
         return dist, rows
 
+    def search_sim(self, queries, k: int, allow=None, mask_key: int = 0):
+        """search() returning (sim [B,k] fp32 descending, -inf when missing; rows [B,k]): the
+        exact similarities, for merging several stores' lists (ShardedStore)."""
+        q = np.ascontiguousarray(np.asarray(queries, dtype=np.float32))
+        if q.ndim == 1:
+            q = q[None]
+        if q.shape[1] != self.dim:
+            raise ValueError(f"query dim {q.shape[1]} != store dim {self.dim}")
+        B = q.shape[0]
+        sim = np.empty((B, k), dtype=np.float32)
+        rows = np.empty((B, k), dtype=np.int64)
+        a = None
+        if allow is not None:
+            n, _ = self.count()
+            a = np.ascontiguousarray(np.asarray(allow, dtype=np.uint8))
+            if a.shape != (n,):
+                raise ValueError(f"allow mask must have {n} entries, got {a.shape}")
+            if n == 0:
+                a = np.zeros(1, dtype=np.uint8)
+        N.call("sr_store_search_sim", self._h, N.ptr(q), B, int(k), N.ptr(a) if a is not None else None,
+               int(mask_key) if a is not None else 0, N.ptr(sim), N.ptr(rows))
+        return np.where(rows >= 0, sim, -np.inf).astype(np.float32), rows
+
     def search_dev(self, q, k: int, out_sim=None, out_rows=None, row_offset: int = 0, stream=None):
         """Device path: q [B, >=dim] fp16/fp32 device tensor (only the first `dim` columns are
         read when q is exactly [B, dim]; a padded fp16 [B, ld] query must be sliced by the caller).
@@ -345,9 +368,16 @@ class ShardedStore:
     def _search_host(self, q, k, allow, mask_key):
         B = q.shape[0]
         dists, rows = [], []
+        # native shards hand back their exact similarities: the merge then orders by similarity as
+        # one store does (1 - sim in fp32 can merge two neighbouring similarities into one distance)
+        exact = all(hasattr(sh, "search_sim") for sh in self.shards)
         for s, sh in enumerate(self.shards):
             a = None if allow is None else np.asarray(allow, dtype=np.uint8)[self.tables[s]]
-            d, r = sh.search(q, k, allow=a, mask_key=mask_key) if a is not None else sh.search(q, k)
+            if exact:
+                sim, r = sh.search_sim(q, k, allow=a, mask_key=mask_key)
+                d = -sim.astype(np.float64)    # merge key; converted back to 1 - sim below
+            else:
+                d, r = sh.search(q, k, allow=a, mask_key=mask_key) if a is not None else sh.search(q, k)
             d = np.asarray(d)          # the shards' own precision (fp32 from the device)
             g = np.where(r >= 0, self.tables[s][np.clip(r, 0, None)] if len(self.tables[s]) else -1, -1)
             dists.append(np.where(g >= 0, d, np.inf))
@@ -359,6 +389,9 @@ class ShardedStore:
             big = np.where(R[b] >= 0, R[b], np.iinfo(np.int64).max)
             o = np.lexsort((big, D[b]))[:k]
             out_d[b], out_r[b] = D[b][o], np.where(np.isfinite(D[b][o]), R[b][o], -1)
+        if exact:  # -sim -> 1 - sim in fp32, as the single store reports it
+            ok = out_r >= 0
+            out_d = np.where(ok, (np.float32(1.0) - (-out_d).astype(np.float32)), np.inf).astype(np.float32)
         return out_d, out_r
 
     def _search_device(self, q, k):

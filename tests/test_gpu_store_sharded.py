@@ -42,6 +42,13 @@ def test_sharded_store_equals_single_store():
     d1, r1 = one.search(q, 50, allow=allow, mask_key=7)
     d2, r2 = sh.search(q, 50, allow=allow, mask_key=7)   # per-shard masked search, host merge
     assert np.array_equal(r1, r2) and np.array_equal(d1, d2)
+    # 300 queries x k = 100 through the host merge: neighbours whose fp32 similarities differ by
+    # one ulp but share one fp32 distance keep one store's order (merge on the similarities)
+    q3 = _data(300, dim, 5)
+    d1, r1 = one.search(q3, 100, allow=allow, mask_key=8)
+    d2, r2 = sh.search(q3, 100, allow=allow, mask_key=8)
+    np.testing.assert_array_equal(d1, d2)
+    np.testing.assert_array_equal(r1, r2)
     assert np.array_equal(one.compact(), sh.compact())
     d1, r1 = one.search(q, 100)
     d2, r2 = sh.search(q, 100)
