@@ -128,7 +128,8 @@ def _sharded_worker(rank, world, port, out_q):
         res = _run_pipeline(rank, world)
         res_h = _run_pipeline(rank, world, hybrid=True)
         res_p = _run_pipeline(rank, world, shard_passages=True)
-        out_q.put((rank, (res, res_h, res_p)))
+        res_hp = _run_pipeline(rank, world, hybrid=True, shard_passages=True)
+        out_q.put((rank, (res, res_h, res_p, res_hp)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -235,6 +236,7 @@ def test_two_rank_sharded_pipeline_equals_single_process():
     got = {r: v[0] for r, v in got_both.items()}
     got_h = {r: v[1] for r, v in got_both.items()}
     got_p = {r: v[2] for r, v in got_both.items()}
+    got_hp = {r: v[3] for r, v in got_both.items()}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -253,9 +255,10 @@ def test_two_rank_sharded_pipeline_equals_single_process():
         np.testing.assert_allclose(got[r]["cand_sims"], full[r]["cand_sims"], atol=1e-6)
         np.testing.assert_array_equal(got[r]["rows"], full[r]["rows"])
         np.testing.assert_allclose(got[r]["logits"], full[r]["logits"], atol=1e-5)
-        # sharded passage tokens (C3 fetch) == the replicated table, bit for bit
+        # sharded passage tokens (C3 fetch) == the replicated table, bit for bit (dense and hybrid)
         for f in ("rows", "cand_rows", "cand_sims", "logits"):
             np.testing.assert_array_equal(got_p[r][f], got[r][f])
+            np.testing.assert_array_equal(got_hp[r][f], got_h[r][f])
 
 
 def test_bench_launches_its_own_ranks():
