@@ -776,6 +776,7 @@ void LexIndex::save(const char* path) {
   ok = ok && (P_ == 0 || std::fwrite(ft.data(), 4, (size_t)P_, f) == (size_t)P_);
   ok = ok && (P_ == 0 || std::fwrite(fv.data(), 8, (size_t)P_, f) == (size_t)P_);
   ok = (std::fclose(f) == 0) && ok;
+  ok = ok && fsync_path(tmp);
   if (!ok || std::rename(tmp.c_str(), path) != 0)
     throw Error(SR_ERR_IO, std::string("lex.save: write failed for ") + path);
 }

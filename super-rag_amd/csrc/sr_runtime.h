@@ -8,9 +8,21 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include "sr_common.h"
 
 namespace sr {
+
+// Flush a written file's data to stable storage before it is renamed into place (snapshot
+// writers: a commit must never name a base whose bytes are still only in the page cache).
+inline bool fsync_path(const std::string& path) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  const bool ok = ::fsync(fd) == 0;
+  return (::close(fd) == 0) && ok;
+}
 
 // RAII device allocation.
 struct DevBuf {

@@ -281,7 +281,7 @@ void Store::search_block8(const half_t* qn, int B, int k, float* out_sim, int64_
   if (n == 0) {
     launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, true, asim, arow, 0, s, live);
   } else {
-    // B <= 128: the small-block fp8 kernel (dense first chunk, then threshold chunks); larger
+    // B <= 64: the small-block fp8 kernel (dense first chunk, then threshold chunks); larger
     // blocks: the 256 x 256 fp8 GEMM main loop (its first chunk in threshold mode at tau = -inf)
     const bool small = B <= 64;   // (at 128 queries the GEMM main loop is faster: 4.4 ms vs ~3.7)
     const int64_t dense = std::min<int64_t>(n, safe ? (int64_t)(cap - kk) : kDenseRows);
@@ -427,8 +427,8 @@ void Store::search_host(const float* q, int B, int k, float* out_dist, int64_t* 
 }
 
 // Snapshot format (little endian): "SRMISTO1", int32 dim, int64 n_rows, n_rows x dim fp16
-// (normalised rows, unpadded), n_rows bytes of live flags.  Written to "<path>.tmp" and renamed
-// over <path>, so a crash mid-save leaves the previous snapshot intact.
+// (normalised rows, unpadded), n_rows bytes of live flags.  Written to "<path>.tmp", fsync'd and
+// renamed over <path>, so a crash mid-save leaves the previous snapshot intact.
 void Store::save(const char* path) {
   DeviceGuard g(device_);
   begin(stream_);
@@ -454,6 +454,7 @@ void Store::save(const char* path) {
   f.flush();
   if (!f) throw Error(SR_ERR_IO, std::string("store.save: write failed for ") + tmp);
   f.close();
+  if (!fsync_path(tmp)) throw Error(SR_ERR_IO, std::string("store.save: fsync failed for ") + tmp);
   if (std::rename(tmp.c_str(), path) != 0)
     throw Error(SR_ERR_IO, std::string("store.save: cannot rename ") + tmp + " to " + path);
 }

@@ -15,7 +15,7 @@ import ctypes
 import json
 import logging
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field, replace
 
 import numpy as np
 
@@ -65,10 +65,18 @@ class ModelSpec:
     pad_id: int = 0
     max_length: int = 512
     residual_fp16: bool = False  # fp16 residual stream (rerankers: ranking fidelity, less traffic)
+    # the model directory the spec was resolved from (its checkpoint and tokenizer live there);
+    # None: $SUPER_RAG_AMD_WEIGHTS/<name>
+    source_dir: str | None = field(default=None, compare=False)
 
     @property
     def pair_style(self) -> int:
         return 0 if self.arch == "xlmr" else 1
+
+    @property
+    def asset_dir(self) -> str | None:
+        """Directory holding model.safetensors / tokenizer.json for this spec, or None."""
+        return self.source_dir or model_dir(self.name)
 
 
 def _bert(name, d, L, H, F, **kw):
@@ -157,13 +165,17 @@ def spec_from_dir(path: str, name: str | None = None) -> ModelSpec:
 
 def resolve_spec(model: str) -> ModelSpec:
     """Map a reference model name (e.g. "BAAI/bge-m3", "bge-base-en-v1.5") to a ModelSpec: the
-    built-in shapes of MODELS, else the config.json of $SUPER_RAG_AMD_WEIGHTS/<model>."""
+    built-in shapes of MODELS, else the config.json of $SUPER_RAG_AMD_WEIGHTS/<model>.  The
+    directory is looked up under the name as given (its case and version suffix kept, as Hugging
+    Face names it: ".../bge-base-en-v1.5"), and the spec remembers it, so the checkpoint and the
+    tokenizer come from the same directory the spec did."""
     key = _key(model)
-    if key in MODELS:
-        return MODELS[key]
     d = model_dir(model)
-    if d and os.path.exists(os.path.join(d, "config.json")):
-        return spec_from_dir(d, key)
+    has_dir = bool(d) and os.path.isdir(d)
+    if key in MODELS:
+        return replace(MODELS[key], source_dir=d) if has_dir else MODELS[key]
+    if has_dir and os.path.exists(os.path.join(d, "config.json")):
+        return replace(spec_from_dir(d, key), source_dir=d)
     raise KeyError(f"unknown encoder model '{model}' (known: {sorted(MODELS)}; or a model "
                    f"directory with config.json under SUPER_RAG_AMD_WEIGHTS)")
 
@@ -243,7 +255,7 @@ def load_safetensors(path: str) -> dict:
 def find_checkpoint(spec: ModelSpec) -> str | None:
     """$SUPER_RAG_AMD_WEIGHTS/<model>/model.safetensors, or None when the variable is unset.
     Raises ModelAssetsError when the variable is set but the file is missing (misconfiguration)."""
-    d = model_dir(spec.name)
+    d = spec.asset_dir
     if d is None:
         return None
     p = os.path.join(d, "model.safetensors")

@@ -14,7 +14,9 @@ mutations are journaled and only compaction / journal growth writes a new base:
 A checkpoint writes the gen+1 base files, then replaces <name>.json (atomic rename: the commit),
 then resets the journal and removes the gen files.  Restore loads the base named by the json,
 checks its row count, and replays the journal lines of that generation in order; a torn last line
-(crash mid-append) and lines of older generations are ignored.  Replaying an add re-inserts the
+(crash mid-append) is cut off the log before anything is appended after it (otherwise the next
+record would be glued onto the fragment and the whole line lost on the restore after that), and
+lines of older generations are ignored.  Replaying an add re-inserts the
 same fp32 vectors through the same normalisation, so the restored rows are bit-identical.
 Journal bytes per add are proportional to the rows added (vectors 4·dim B per row + their text
 and metadata), independent of the collection size.
@@ -65,8 +67,33 @@ class Journal:
         return sum(os.path.getsize(p) for p in (self.log_path, self.vlog_path) if os.path.exists(p))
 
     def base_bytes(self) -> int:
-        return os.path.getsize(self.store_path(self.gen)) if self.gen is not None and \
-            os.path.exists(self.store_path(self.gen)) else 0
+        """Bytes of the committed base: the store file plus, for a sharded collection, its shard
+        stores and row tables (<name>.g<gen>.srmi is then only the manifest), plus the lexical
+        index, so the checkpoint ratio compares the journal with the real snapshot size."""
+        if self.gen is None or not os.path.isdir(self.dir):
+            return 0
+        pat = self._pattern(re.escape(f".g{self.gen}"))
+        return sum(os.path.getsize(os.path.join(self.dir, fn)) for fn in os.listdir(self.dir)
+                   if pat.fullmatch(fn) and not fn.endswith(".tmp"))
+
+    def _sync_generation(self, gen: int) -> None:
+        """fsync every file of base generation `gen` and the directory, before the commit names it."""
+        pat = self._pattern(re.escape(f".g{gen}"))
+        for fn in os.listdir(self.dir):
+            if pat.fullmatch(fn) and not fn.endswith(".tmp"):
+                fd = os.open(os.path.join(self.dir, fn), os.O_RDONLY)
+                try:
+                    os.fsync(fd)
+                finally:
+                    os.close(fd)
+        self._sync_dir()
+
+    def _sync_dir(self) -> None:
+        fd = os.open(self.dir, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+        finally:
+            os.close(fd)
 
     # -- checkpoint -----------------------------------------------------------------------------------
     def checkpoint(self, c) -> None:
@@ -80,10 +107,12 @@ class Journal:
         if c.lex is not None:
             c.lex.save(self.lex_path(gen))
             meta["lex_vocab"] = c.vocab.terms
+        self._sync_generation(gen)                            # base bytes durable before the commit
         tmp = self.meta_path + ".tmp"
         with open(tmp, "w", encoding="utf-8") as f:
             _fsync_write(f, json.dumps(meta))
         os.replace(tmp, self.meta_path)                       # commit
+        self._sync_dir()
         old = self.gen
         self.gen = gen
         for p in (self.log_path, self.vlog_path):
@@ -127,17 +156,28 @@ class Journal:
             return json.load(f)
 
     def records(self, gen) -> List[dict]:
-        """Journal lines of generation `gen`, in order; a torn last line is dropped."""
+        """Journal lines of generation `gen`, in order.  A torn last line (a crash mid-append:
+        never acknowledged) is dropped AND truncated away, so the next _append starts on a fresh
+        line instead of extending the fragment into a line no later restore could parse."""
         if not os.path.exists(self.log_path):
             return []
         out = []
-        with open(self.log_path, encoding="utf-8") as f:
+        good = 0                                   # byte offset just past the last complete line
+        with open(self.log_path, "rb") as f:
             for line in f:
-                if not line.endswith("\n"):
-                    break                      # torn append: never acknowledged
-                rec = json.loads(line)
+                if not line.endswith(b"\n"):
+                    break
+                good += len(line)
+                rec = json.loads(line.decode("utf-8"))
                 if rec.get("g") == gen:
                     out.append(rec)
+        if good != os.path.getsize(self.log_path):
+            os.truncate(self.log_path, good)
+            fd = os.open(self.log_path, os.O_RDONLY)
+            try:
+                os.fsync(fd)
+            finally:
+                os.close(fd)
         return out
 
     def vectors(self, rec: dict, dim: int) -> np.ndarray:

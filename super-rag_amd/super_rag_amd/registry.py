@@ -36,7 +36,7 @@ def get_model(model: str | ModelSpec, device: int | None = None, seed: int = 0):
     """Return the shared (Encoder, Tokenizer) for a model name such as "BAAI/bge-m3"."""
     spec = model if isinstance(model, ModelSpec) else resolve_spec(model)
     dev = default_device() if device is None else int(device)
-    key = (spec.name, dev)
+    key = (spec.name, spec.asset_dir, dev)
     with _lock:
         hit = _models.get(key)
         if hit is None:

@@ -49,12 +49,12 @@ def longest_first(a: int, b: int, budget: int):
 
 class Tokenizer:
     def __init__(self, spec, path: str | None = None, synthetic: bool | None = None):
-        from .encoder import ModelAssetsError, model_dir, synthetic_allowed
+        from .encoder import ModelAssetsError, synthetic_allowed
         self.spec = spec
         self.max_length = spec.max_length
         self._hf = None
         if path is None and not synthetic:
-            d = model_dir(spec.name)
+            d = spec.asset_dir
             if d is not None:
                 path = os.path.join(d, "tokenizer.json")
         if path:

@@ -99,3 +99,29 @@ def test_tokenizer_pairs_match_the_hf_post_processor(product_env):
         p = " ".join(rng.choice(WORDS, rng.integers(1, 40)))
         ids, mask, _ = ours.encode_pairs(q, [p])
         assert ids[0][mask[0] == 1].tolist() == hf.encode(q, p).ids
+
+
+def test_hf_directory_names_keep_case_and_version_suffix(product_env):
+    """"BAAI/bge-base-en-v1.5" and "Local/Tiny-Embed-v1.5": spec, checkpoint and tokenizer all come
+    from the directory named as the model is named (the spec key is lowercased and
+    suffix-stripped, the directory is not)."""
+    from super_rag_amd.encoder import MODELS, find_checkpoint, model_weights, resolve_spec
+    from super_rag_amd.tokenizer import Tokenizer
+    d = write_model_dir(str(product_env), "Tiny-Embed-v1.5", "bert", seed=5)
+    e = resolve_spec("Local/Tiny-Embed-v1.5")
+    assert e.name == "tiny-embed" and e.source_dir == d and e.hidden == 128
+    assert find_checkpoint(e) == d + "/model.safetensors"
+    assert "encoder.layer.1.output.dense.weight" in model_weights(e)
+    assert not Tokenizer(e).synthetic
+    # a built-in shape whose Hugging Face directory carries the version suffix
+    import os
+    import shutil
+    hf_dir = os.path.join(str(product_env), "bge-base-en-v1.5")
+    os.makedirs(hf_dir)
+    shutil.copy(d + "/tokenizer.json", hf_dir)
+    b = resolve_spec("BAAI/bge-base-en-v1.5")
+    assert b == MODELS["bge-base-en"] and b.source_dir == hf_dir
+    assert Tokenizer(b)._hf is not None
+    from super_rag_amd.encoder import ModelAssetsError
+    with pytest.raises(ModelAssetsError, match="bge-base-en-v1.5/model.safetensors"):
+        find_checkpoint(b)

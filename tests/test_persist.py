@@ -107,6 +107,33 @@ def test_torn_journal_tail_and_stale_generations_are_ignored(doubles, tmp_path):
     con2 = doubles.MI355XVectorStoreConnector(ctx)
     assert _state(con2, ["doc 5", "doc 1"]) == want
     assert doubles._get("tt").store.count() == (6, 6)
+    # the recovered collection keeps journaling: the torn fragment must not swallow the next add
+    new_ids = con2.add([_node(6)])
+    con2.delete(ids=[new_ids[0]])
+    con2.add([_node(7)])
+    want2 = _state(con2, ["doc 7", "doc 5", "doc 1"])
+    doubles._collections.clear()
+    con3 = doubles.MI355XVectorStoreConnector(ctx)
+    assert _state(con3, ["doc 7", "doc 5", "doc 1"]) == want2
+    assert doubles._get("tt").store.count() == (8, 7)
+    with open(tmp_path / "tt.log", "rb") as f:
+        assert all(json.loads(l) for l in f.read().splitlines())   # every line parses again
+
+
+def test_base_bytes_counts_shard_files(tmp_path):
+    """A sharded collection's <name>.g<gen>.srmi is a small manifest: the checkpoint ratio must see
+    the shard stores and row tables too."""
+    from super_rag_amd.persist import Journal
+    j = Journal(str(tmp_path), "sh")
+    j.gen = 3
+    (tmp_path / "sh.g3.srmi").write_bytes(b"m" * 10)
+    (tmp_path / "sh.g3.srmi.s0").write_bytes(b"x" * 1000)
+    (tmp_path / "sh.g3.srmi.s1").write_bytes(b"x" * 2000)
+    (tmp_path / "sh.g3.srmi.rows.npz").write_bytes(b"r" * 300)
+    (tmp_path / "sh.g3.srlex").write_bytes(b"l" * 40)
+    (tmp_path / "sh.g2.srmi.s0").write_bytes(b"o" * 99999)         # another generation
+    (tmp_path / "other.g3.srmi").write_bytes(b"o" * 99999)         # another collection
+    assert j.base_bytes() == 10 + 1000 + 2000 + 300 + 40
 
 
 def test_restore_refuses_an_inconsistent_snapshot(doubles, tmp_path):
