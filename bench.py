@@ -39,8 +39,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); without WORLD_SIZE the script launches them itself")
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--corpus-rows", type=int, default=10_000_000)
     ap.add_argument("--batch", type=int, default=256, help="queries per rank per step")
     ap.add_argument("--dim", type=int, default=768)
@@ -58,7 +58,11 @@ def parse():
                     help="cross-encoder tokens per chunk (workspace ~15 KB per token; 1,638,400 = "
                          "2 chunks per step: +0.8 %% over 524,288, profiles/r02_ab_chunks.log)")
     ap.add_argument("--cpu-queries", type=int, default=32,
-                    help="cpu_baseline: queries embedded and reranked (100 pairs each) on the host")
+                    help="cpu_baseline: queries embedded (and at most this many reranked) on the host")
+    ap.add_argument("--cpu-rerank-budget-s", type=float, default=20.0,
+                    help="cpu_baseline: rerank whole queries (100 pairs each) until this many seconds "
+                         "of host time are spent (at least one query; the per-query time is the "
+                         "mean over the queries done, no extrapolation)")
     ap.add_argument("--cpu-search-rows", type=int, default=0,
                     help="cpu_baseline: corpus rows scanned by the host search (0 = the whole corpus)")
     ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
@@ -303,6 +307,11 @@ def main():
                         "final_logit_std_f16": round(float(l16.std()), 5),
                         "queries": int(f8.shape[0])}
 
+    # ---- ranking fidelity on a discriminative reranker (outside the timed region) ---------------
+    fidelity = None
+    if rank == 0 and not a.no_extras:
+        fidelity = rerank_fidelity(rs, local)
+
     # ---- roofline of the dominant kernel -------------------------------------------------------
     dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
@@ -380,6 +389,7 @@ def main():
                    "passages": "sharded (C3 fetch)" if shard_p else "replicated"},
         "recall_at_10": recall,
         **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
+        "rerank_fidelity": fidelity,
         "roofline": roof,
         "search_roofline": search_roof,
         "search_b32": search32,
@@ -434,6 +444,56 @@ def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
                 sum(len(set(r8[i].tolist()) & set(ref_rows[i].tolist())) for i in range(32)) / 320, 4)
     store.set_scan_dtype("fp16")
     out["fp8_speedup"] = round(out["fp16"]["ms_per_batch"] / out["fp8"]["ms_per_batch"], 3)
+    return out
+
+
+def rerank_fidelity(rs, device):
+    """Ranking fidelity of the cross-encoder kernels at the bench shape (12 layers, 768-d, S_pair =
+    128) on a DISCRIMINATIVE reranker: the relevance-structured weights of super_rag_amd/synthetic.py
+    (the bench's seeded-random reranker spreads one query's logits by std ~1e-2 only) on 8 queries
+    x 100 candidates sharing 0..15 query terms, against the fp32 oracle's logits committed in
+    tests/golden/rerank_fidelity.npz (data; tests/golden/gen_rerank_fidelity.py).  Per precision
+    mode: max |logit error|, the smallest per-query (logit std / max error), top-10 identical modulo
+    ties within 1 % of the logit std, mean top-10 overlap, top-1 equal."""
+    from super_rag_amd.encoder import Encoder
+    from super_rag_amd.synthetic import fidelity_setup
+    path = os.path.join(ROOT, "tests", "golden", "rerank_fidelity.npz")
+    if not os.path.exists(path):
+        return None
+    fx = np.load(path)
+    w, ids, mask, _, m = fidelity_setup(rs)
+    if not np.array_equal(ids, fx["ids"]):
+        return {"error": "fidelity fixture does not match its generator"}
+    ref = fx["logits"].reshape(-1, m["cand"])
+    std = ref.std(1)
+    enc = Encoder(rs, device=device, weights=w, max_tokens=ids.size)
+    dids = torch.from_numpy(ids).to(f"cuda:{device}")
+    dmask = torch.from_numpy(mask).to(f"cuda:{device}")
+    out = {"set": (f"{ref.shape[0]} queries x {m['cand']} pairs, S_pair={m['pair_len']}, "
+                   f"{rs.name} shape, relevance-structured weights (super_rag_amd/synthetic.py) vs the "
+                   f"fp32 oracle (tests/golden/rerank_fidelity.npz)"),
+           "logit_std_mean": round(float(std.mean()), 4)}
+    try:
+        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2")):
+            enc.set_fp8(mode)
+            lg = enc.cross_score_dev(dids, dmask)[:, 0].float().cpu().numpy().reshape(ref.shape)
+            err = np.abs(lg - ref).max(1)
+            ident = 0
+            overlap = []
+            for b in range(ref.shape[0]):
+                want = np.argsort(-ref[b], kind="stable")[:10]
+                got = np.argsort(-lg[b], kind="stable")[:10]
+                kth = ref[b][want[-1]]
+                ident += int(all(abs(ref[b][j] - kth) <= 0.01 * std[b] for j in set(want) ^ set(got)))
+                overlap.append(len(set(want) & set(got)) / 10)
+            out[name] = {"max_logit_err": round(float(err.max()), 5),
+                         "min_std_over_err": round(float((std / np.maximum(err, 1e-12)).min()), 1),
+                         "top10_identical_mod_ties": f"{ident}/{ref.shape[0]}",
+                         "top10_overlap": round(float(np.mean(overlap)), 3),
+                         "top1_equal": round(float(np.mean([np.argmax(lg[b]) == np.argmax(ref[b])
+                                                            for b in range(ref.shape[0])])), 3)}
+    finally:
+        enc.close()
     return out
 
 
@@ -537,8 +597,8 @@ def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total, e
       search  the full batch of queries (this rank's B) against the whole corpus as a batched
               fp32 torch matmul + topk, streamed in 1M-row chunks (each chunk is generated and
               L2-normalised on the GPU and copied to pinned host memory outside the timed part);
-      rerank  a.cpu_queries queries x k_cand (query, passage) pairs at S_pair through the fp32
-              cross-encoder, one query's pairs per call.
+      rerank  whole queries of k_cand (query, passage) pairs at S_pair through the fp32
+              cross-encoder, one query's pairs per call, until --cpu-rerank-budget-s is spent.
     End-to-end q/s = 1 / (embed + search + rerank seconds per query)."""
     from oracle import encoder_ref as R
     threads = cpu_cores()
@@ -589,14 +649,17 @@ def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total, e
                                   np.arange(nq * a.k_cand).reshape(nq, a.k_cand), a.pair_len, 0,
                                   rs.bos_id, rs.eos_id, rs.pad_id)
     t_rerank = 0.0
+    nq_r = 0
     for i in range(nq):
         sl = slice(i * a.k_cand, (i + 1) * a.k_cand)
         t0 = time.perf_counter()
         R.cross_logits(cfg(rs), wt_r, pids[sl], pmask[sl])
         t_rerank += time.perf_counter() - t0
-        if i % 4 == 3 or i == nq - 1:
-            log(f"rerank {i + 1}/{nq} queries: {t_rerank:.1f} s")
-    per_q = {"embed": t_embed / nq, "search": t_search / q.shape[0], "rerank": t_rerank / nq}
+        nq_r += 1
+        log(f"rerank {nq_r} queries: {t_rerank:.1f} s")
+        if t_rerank >= a.cpu_rerank_budget_s:
+            break
+    per_q = {"embed": t_embed / nq, "search": t_search / q.shape[0], "rerank": t_rerank / nq_r}
     # (iv) the reference flow's own host-side orchestration per query (NodeflowEngine + runners,
     # constant-time stub backends), measured in the build container by tools/ref_orchestration.py
     orch = None
@@ -610,13 +673,16 @@ def cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batch, p_tok, N_total, e
             "sample": (f"oracle (torch-CPU fp32) on {threads} threads, no extrapolation: embed "
                        f"{nq} queries (S={a.q_len}); exact cosine top-{a.k_cand} of {q.shape[0]} "
                        f"queries over all {rows_total} x {a.dim} rows as a batched fp32 matmul + "
-                       f"topk in 1M-row chunks; rerank {nq} queries x {a.k_cand} pairs "
-                       f"(S={a.pair_len}); end to end = 1 / sum of per-query stage times"),
+                       f"topk in 1M-row chunks; rerank {nq_r} whole queries x {a.k_cand} pairs "
+                       f"(S={a.pair_len}; as many as fit a {a.cpu_rerank_budget_s:.0f} s host-time "
+                       f"budget, measured not extrapolated); end to end = 1 / sum of per-query "
+                       f"stage times"),
             "cpu_model": cpu_model(), "machine_cpus": os.cpu_count(),
             "stage_s_per_query": {k: round(v, 5) for k, v in per_q.items()},
             "stage_qps": {k: round(1.0 / v, 3) for k, v in per_q.items()},
             "stage_s_total": {"embed": round(t_embed, 3), "search": round(t_search, 3),
                               "rerank": round(t_rerank, 3)},
+            "stage_queries": {"embed": nq, "search": int(q.shape[0]), "rerank": nq_r},
             "orchestration_source": (f"{os.path.relpath(orch_path, ROOT)} ({orch['method']}; "
                                      f"{orch['note']})") if orch else None}
 
