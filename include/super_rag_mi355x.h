@@ -189,6 +189,11 @@ typedef struct sr_lex_global {
   int n_terms;
 } sr_lex_global;
 int sr_lex_totals(sr_lex* x, int64_t* n_live, int64_t* sum_dl);
+/* sr_lex_search scored with the corpus-wide statistics of a row-sharded collection (one shard of a
+ * multi-device fulltext / hybrid collection; global NULL = sr_lex_search). */
+int sr_lex_search_global(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                         const uint8_t* allow, int64_t mask_key, const sr_lex_global* global,
+                         float* out_score, int64_t* out_rows);
 int sr_lex_df(sr_lex* x, const int32_t* terms, int n, int64_t* out_df);
 /* Device outputs (B x k on the index's device, score fp32 / row int64 + row_offset; -inf / -1 past
  * the matches), asynchronous on `stream` after the host-side term preparation; global may be NULL
@@ -196,6 +201,18 @@ int sr_lex_df(sr_lex* x, const int32_t* terms, int n, int64_t* out_df);
 int sr_lex_search_dev(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
                       const sr_lex_global* global, float* out_score, int64_t* out_rows,
                       int64_t row_offset, void* stream);
+/* Device-resident queries (the batched hybrid pipeline: query tokens already in HBM, no host copy
+ * and no synchronisation).  tok: B x Lq int32 device (row stride Lq), qlen: B int32 device.
+ * sr_lex_query_stats_dev writes out_stats[0] = live rows, [1] = summed document length, [2 + q Lq +
+ * i] = live df of query q's i-th token (0 past qlen[q]): 2 + B Lq int64 on the device, the vector a
+ * row-sharded corpus sums over its shards (one all-reduce).  sr_lex_search_tok_dev = sr_lex_search_dev
+ * for those queries, scored with the summed vector gstats (device, NULL = this index's own
+ * statistics); same results bit for bit. */
+int sr_lex_query_stats_dev(sr_lex* x, const int32_t* tok, const int32_t* qlen, int B, int Lq,
+                           int64_t* out_stats, void* stream);
+int sr_lex_search_tok_dev(sr_lex* x, const int32_t* tok, const int32_t* qlen, int B, int Lq, int k,
+                          const int64_t* gstats, float* out_score, int64_t* out_rows,
+                          int64_t row_offset, void* stream);
 int sr_lex_save(sr_lex* x, const char* path);
 int sr_lex_load(const char* path, int device, sr_lex** out);
 int sr_lex_compact(sr_lex* x, int64_t* old_to_new);

@@ -77,12 +77,18 @@ class LexCorpus:
                          self.tf[self.off[i]:self.off[i + 1]].tolist())) for i in range(self.n)]
 
 
-def bm25_fixed_scores(corpus: LexCorpus, query, k1=1.2, b=0.75, allow=None):
+def bm25_fixed_scores(corpus: LexCorpus, query, k1=1.2, b=0.75, allow=None, stats=None):
     """Fixed-point score (int64) of every row for one query (list of term ids, repeats count);
-    0 = no match."""
+    0 = no match.  stats = (n_live, sum_dl, df: term -> int) of a whole row-sharded corpus (every
+    shard scores its rows with the corpus-wide N, avgdl and df), or None for this corpus's own."""
     k1, b, omb, k1p1 = _consts(k1, b)
-    n_live = int(corpus.live.sum())
-    adl = avgdl32(corpus.dl, corpus.live)
+    if stats is None:
+        n_live = int(corpus.live.sum())
+        adl = avgdl32(corpus.dl, corpus.live)
+        df_of = lambda t: int(corpus.df[t])
+    else:
+        n_live, sum_dl, df_of = int(stats[0]), int(stats[1]), stats[2]
+        adl = np.float32(float(sum_dl) / n_live) if n_live > 0 else np.float32(1.0)
     acc = np.zeros(corpus.n, dtype=np.int64)
     elig = corpus.live if allow is None else corpus.live & np.asarray(allow, dtype=bool)
     for t, mult in Counter(int(x) for x in query).items():
@@ -93,7 +99,7 @@ def bm25_fixed_scores(corpus: LexCorpus, query, k1=1.2, b=0.75, allow=None):
         keep = elig[rows]
         rows, tf = rows[keep], tf[keep]
         d = corpus.dl[rows].astype(np.float32)
-        idf = idf32(n_live, int(corpus.df[t]))
+        idf = idf32(n_live, df_of(t))
         t1 = d / adl
         norm = k1 * (omb + b * t1)
         w = idf * ((tf * k1p1) / (tf + norm))
@@ -123,13 +129,15 @@ def bm25_scores_loop(docs, dl, live, query, k1=1.2, b=0.75):
     return out
 
 
-def bm25_topk(corpus: LexCorpus, queries, k, k1=1.2, b=0.75, allow=None):
-    """-> (score [B,k] fp32 desc, rows [B,k] int64); -inf / -1 past the matching rows."""
+def bm25_topk(corpus: LexCorpus, queries, k, k1=1.2, b=0.75, allow=None, stats=None):
+    """-> (score [B,k] fp32 desc, rows [B,k] int64); -inf / -1 past the matching rows.  stats: as
+    bm25_fixed_scores (a list of per-query stats, or one for every query)."""
     B = len(queries)
     scores = np.full((B, k), -np.inf, dtype=np.float32)
     rows = np.full((B, k), -1, dtype=np.int64)
     for i, q in enumerate(queries):
-        acc = bm25_fixed_scores(corpus, q, k1, b, allow)
+        st = stats[i] if isinstance(stats, list) else stats
+        acc = bm25_fixed_scores(corpus, q, k1, b, allow, st)
         hit = np.nonzero(acc)[0]
         order = hit[np.lexsort((hit, -acc[hit]))][:k]
         m = len(order)

@@ -432,6 +432,22 @@ int sr_lex_search(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, 
   SR_API_END
 }
 
+int sr_lex_search_global(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                         const uint8_t* allow, int64_t mask_key, const sr_lex_global* global,
+                         float* out_score, int64_t* out_rows) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  if (B > 0) {
+    SR_NONNULL(qoff);
+    SR_NONNULL(out_score);
+    SR_NONNULL(out_rows);
+    if (qoff[B] > 0) SR_NONNULL(qterms);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->search_host(qoff, qterms, B, k, allow, mask_key, out_score, out_rows, global);
+  SR_API_END
+}
+
 int sr_lex_totals(sr_lex* x, int64_t* n_live, int64_t* sum_dl) {
   SR_API_BEGIN
   SR_NONNULL(x);
@@ -467,6 +483,38 @@ int sr_lex_search_dev(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int
   std::lock_guard<std::mutex> lk(x->impl->mu);
   x->impl->search_dev(qoff, qterms, B, k, nullptr, 0, out_score, out_rows,
                       reinterpret_cast<hipStream_t>(stream), global, row_offset);
+  SR_API_END
+}
+
+int sr_lex_query_stats_dev(sr_lex* x, const int32_t* tok, const int32_t* qlen, int B, int Lq,
+                           int64_t* out_stats, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  SR_NONNULL(out_stats);
+  SR_CHECK(B >= 0 && Lq >= 0, "lex.query_stats: negative shape");
+  if ((int64_t)B * Lq > 0) {
+    SR_NONNULL(tok);
+    SR_NONNULL(qlen);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->query_stats_dev(tok, qlen, B, Lq, out_stats, reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
+int sr_lex_search_tok_dev(sr_lex* x, const int32_t* tok, const int32_t* qlen, int B, int Lq, int k,
+                          const int64_t* gstats, float* out_score, int64_t* out_rows,
+                          int64_t row_offset, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  if (B > 0) {
+    SR_NONNULL(qlen);
+    SR_NONNULL(out_score);
+    SR_NONNULL(out_rows);
+    if (Lq > 0) SR_NONNULL(tok);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->search_tok_dev(tok, qlen, B, Lq, k, gstats, out_score, out_rows,
+                          reinterpret_cast<hipStream_t>(stream), row_offset);
   SR_API_END
 }
 

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "sr_kernels.h"
@@ -125,8 +126,8 @@ __global__ void lex_bounds_kernel(const LexTerm* __restrict__ terms, int nslots,
 __global__ __launch_bounds__(LEX_THREADS) void lex_score_kernel(
     const LexTerm* __restrict__ terms, const int* __restrict__ slot_off, const int32_t* __restrict__ bnd,
     int NB, const uint64_t* __restrict__ post, const int32_t* __restrict__ dlen,
-    const uint8_t* __restrict__ elig, int64_t rows, float avgdl, float k1, float b,
-    int* __restrict__ kcnt, const int64_t* __restrict__ koff, uint64_t* __restrict__ keys) {
+    const uint8_t* __restrict__ elig, int64_t rows, const float* __restrict__ avgdl_p, float k1,
+    float b, int* __restrict__ kcnt, const int64_t* __restrict__ koff, uint64_t* __restrict__ keys) {
   extern __shared__ __attribute__((aligned(16))) uint32_t acc[];
   const int q = blockIdx.x, blk = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int s0 = slot_off[q], s1 = slot_off[q + 1];
@@ -147,6 +148,7 @@ __global__ __launch_bounds__(LEX_THREADS) void lex_score_kernel(
   __syncthreads();
   if (s_total == 0) return;  // uniform: no posting of this query in this row block
   for (int i = tid; i < LEX_RB; i += LEX_THREADS) acc[i] = 0u;
+  const float avgdl = *avgdl_p;  // (host path: uploaded; device path: lex_qprep_kernel)
   const float one_minus_b = 1.f - b, k1p1 = k1 + 1.f;
   const int64_t r0 = (int64_t)blk * LEX_RB;
   for (int tb = s0; tb < s1; tb += TB) {
@@ -216,6 +218,95 @@ __global__ __launch_bounds__(LEX_THREADS) void lex_score_kernel(
     }
     kl += __popcll(bal);
   }
+}
+
+// ---- device-resident query preparation (padded query-token matrix) ------------------------------
+// The host path (LexIndex::search_dev) builds the per-query term slots, idf and key offsets on the
+// host from its df mirror.  For a batch whose query tokens are already on the device (the hybrid
+// pipeline) that would mean a device -> host copy and a synchronisation in the middle of a step;
+// these kernels do the same on the device from the inverted index's offsets.
+//
+// lex_qstats_kernel: out[0] = live rows, out[1] = summed document length (this index), out[2 +
+//   q Lq + i] = live document frequency of query q's i-th token (0 past its length / unknown): the
+//   vector a row-sharded corpus all-reduces into corpus-wide statistics.
+__global__ void lex_qstats_kernel(const int32_t* __restrict__ tok, const int32_t* __restrict__ qlen,
+                                  int B, int Lq, const int64_t* __restrict__ off, int64_t T,
+                                  int64_t n_live, int64_t sum_dl, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    out[0] = n_live;
+    out[1] = sum_dl;
+  }
+  if (i >= (int64_t)B * Lq) return;
+  const int q = (int)(i / Lq), p = (int)(i % Lq);
+  const int32_t t = tok[i];
+  out[2 + i] = (p < qlen[q] && t >= 0 && t < T) ? off[t + 1] - off[t] : 0;
+}
+
+// lex_qprep_kernel: one workgroup, thread q = query q of the group (G <= 1024).  Slot q Lq + i is
+// the query's i-th token if that is its FIRST occurrence of a term with postings here (start, len,
+// idf, multiplicity = occurrences in the query), else empty (len 0): the host path's slots in the
+// same order.  idf uses the corpus-wide df / N when gst is given (gst[0], gst[1], gst[2 + df_base +
+// q Lq + i] as written by lex_qstats_kernel for the whole batch and summed over the shards; df_base
+// = the group's first query x Lq), else this index's.  koff = exclusive
+// scan of cap = min(sum of len, rows); kcnt = 0; *avgdl_out = sum_dl / N as the host computes it.
+__device__ __forceinline__ float lex_idf_dev(int64_t df, int64_t n_live) {
+  const double N = (double)n_live, d = (double)df;
+  return (float)log(1.0 + (N - d + 0.5) / (d + 0.5));
+}
+
+__global__ __launch_bounds__(1024) void lex_qprep_kernel(
+    const int32_t* __restrict__ tok, const int32_t* __restrict__ qlen, int G, int Lq,
+    const int64_t* __restrict__ off, int64_t T, int64_t rows, int64_t n_live, int64_t sum_dl,
+    const int64_t* __restrict__ gst, int64_t df_base, LexTerm* __restrict__ slots,
+    int* __restrict__ slot_off,
+    int64_t* __restrict__ koff, int* __restrict__ kcnt, float* __restrict__ avgdl_out) {
+  __shared__ int64_t s_wave[16];
+  const int q = threadIdx.x, lane = q & 63, wave = q >> 6;
+  const int64_t N = gst ? gst[0] : n_live;
+  const int64_t sdl = gst ? gst[1] : sum_dl;
+  int64_t cap = 0;
+  if (q < G) {
+    const int32_t* tq = tok + (int64_t)q * Lq;
+    const int L = min(max(qlen[q], 0), Lq);
+    for (int i = 0; i < Lq; ++i) {
+      LexTerm e = {0, 0, 0.f, 0, 0};
+      const int32_t t = tq[i];
+      if (i < L && t >= 0 && t < T) {
+        const int64_t st = off[t], len = off[t + 1] - st;
+        bool first = len > 0;
+        for (int j = 0; j < i && first; ++j) first = tq[j] != t;
+        if (first) {
+          int mult = 0;
+          for (int j = i; j < L; ++j) mult += tq[j] == t ? 1 : 0;
+          const int64_t df = gst ? gst[2 + df_base + (int64_t)q * Lq + i] : len;
+          e = {st, (int32_t)len, lex_idf_dev(df, N), mult, 0};
+          cap += len;
+        }
+      }
+      slots[(int64_t)q * Lq + i] = e;
+    }
+    cap = cap < rows ? cap : rows;
+    kcnt[q] = 0;
+    slot_off[q] = q * Lq;
+  }
+  // exclusive scan of cap over the group (waves of 64, then the wave totals)
+  int64_t incl = cap;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  int64_t base = 0;
+  for (int w = 0; w < wave; ++w) base += s_wave[w];
+  if (q < G) koff[q] = base + incl - cap;
+  if (q == G - 1) {
+    koff[G] = base + incl;
+    slot_off[G] = G * Lq;
+  }
+  if (q == 0) *avgdl_out = N > 0 ? (float)((double)sdl / (double)N) : 1.f;
 }
 
 // ---- L2 -----------------------------------------------------------------------------------------
@@ -499,6 +590,7 @@ void LexIndex::rebuild(hipStream_t s) {
   nnz_ = 0;
   off_.reserve((size_t)(T + 1) * 8);
   if (P_ == 0 || T == 0) {
+    max_df_ = 0;
     off_host_.assign((size_t)T + 1, 0);
     SR_HIP(hipMemsetAsync(off_.p, 0, (size_t)(T + 1) * 8, s));
     SR_HIP(hipStreamSynchronize(s));
@@ -538,7 +630,11 @@ void LexIndex::rebuild(hipStream_t s) {
   SR_HIP(hipMemcpyAsync(off_host_.data(), off_.p, (size_t)(T + 1) * 8, hipMemcpyDeviceToHost, s));
   SR_HIP(hipStreamSynchronize(s));
   nnz_ = off_host_[(size_t)T];
-  for (int64_t t = 0; t < T; ++t) df_host_[(size_t)t] = (int32_t)(off_host_[(size_t)t + 1] - off_host_[(size_t)t]);
+  max_df_ = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    df_host_[(size_t)t] = (int32_t)(off_host_[(size_t)t + 1] - off_host_[(size_t)t]);
+    max_df_ = std::max<int64_t>(max_df_, df_host_[(size_t)t]);
+  }
   dirty_ = false;
 }
 
@@ -682,7 +778,7 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
       return at;
     };
     const size_t o_sl = carve(b_sl), o_so = carve(b_so), o_ko = carve(b_ko), o_cnt = carve(b_cnt),
-                 o_bnd = carve(b_bnd), o_keys = carve(b_keys);
+                 o_bnd = carve(b_bnd), o_keys = carve(b_keys), o_avg = carve(4);
     ws_.reserve(o);
     char* w = ws_.as<char>();
     LexTerm* d_sl = reinterpret_cast<LexTerm*>(w + o_sl);
@@ -691,6 +787,10 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
     int* d_cnt = reinterpret_cast<int*>(w + o_cnt);
     int32_t* d_bnd = reinterpret_cast<int32_t*>(w + o_bnd);
     uint64_t* d_keys = reinterpret_cast<uint64_t*>(w + o_keys);
+    float* d_avg = reinterpret_cast<float*>(w + o_avg);
+    uint32_t adl_bits;
+    std::memcpy(&adl_bits, &adl, 4);
+    SR_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_avg), (int)adl_bits, 1, s));
     if (nslots) SR_HIP(hipMemcpyAsync(d_sl, slots.data(), slots.size() * sizeof(LexTerm), hipMemcpyHostToDevice, s));
     SR_HIP(hipMemcpyAsync(d_so, slot_off.data(), b_so, hipMemcpyHostToDevice, s));
     SR_HIP(hipMemcpyAsync(d_ko, koff.data(), b_ko, hipMemcpyHostToDevice, s));
@@ -703,7 +803,7 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
       ProfScope prof("lex_score", s, 0.0, (double)scored * 12.0);
       hipLaunchKernelGGL(lex_score_kernel, dim3((unsigned)qb, (unsigned)NB), dim3(LEX_THREADS),
                          LEX_RB * 4, s, d_sl, d_so, d_bnd, NB, post_.as<uint64_t>(),
-                         dlen_.as<int32_t>(), elig, rows_, adl, k1_, b_, d_cnt, d_ko, d_keys);
+                         dlen_.as<int32_t>(), elig, rows_, d_avg, k1_, b_, d_cnt, d_ko, d_keys);
       SR_LAUNCH_CHECK();
     }
     {
@@ -720,9 +820,98 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
   end(s);
 }
 
+void LexIndex::query_stats_dev(const int32_t* tok, const int32_t* qlen, int B, int Lq,
+                               int64_t* out, hipStream_t s) {
+  SR_CHECK(B >= 0 && Lq >= 0, "lex.query_stats: negative shape");
+  DeviceGuard g(device_);
+  begin(s);
+  rebuild(s);
+  off_.reserve(8);
+  const int64_t n = (int64_t)B * Lq;
+  hipLaunchKernelGGL(lex_qstats_kernel, dim3((unsigned)std::max<int64_t>(1, ceil_div(n, 256))), dim3(256),
+                     0, s, tok, qlen, B, Lq, off_.as<int64_t>(), vocab_, live_n_, sum_dl_, out);
+  SR_LAUNCH_CHECK();
+  end(s);
+}
+
+void LexIndex::search_tok_dev(const int32_t* tok, const int32_t* qlen, int B, int Lq, int k,
+                              const int64_t* gstats, float* out_score, int64_t* out_rows,
+                              hipStream_t s, int64_t row_offset) {
+  SR_CHECK(B >= 0 && Lq >= 0, "lex.search_tok: negative shape");
+  SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "lex.search: top_k must be in [1, 1024]");
+  if (B == 0) return;
+  DeviceGuard g(device_);
+  begin(s);
+  rebuild(s);
+  off_.reserve(8);
+  const int64_t rows = std::max<int64_t>(rows_, 1);
+  const int NB = (int)ceil_div(rows, LEX_RB);
+  SR_CHECK(NB <= 65535, "lex.search: more than 2^30 rows per index");
+  static bool attr_set = false;
+  if (!attr_set) {
+    SR_HIP(hipFuncSetAttribute((const void*)lex_score_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LEX_RB * 4));
+    SR_HIP(hipFuncSetAttribute((const void*)lex_select_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(LexSelSmem)));
+    attr_set = true;
+  }
+  // keys per query <= min(Lq * max df, rows), known on the host without looking at the queries:
+  // query groups of G <= 1024 sized so the group's keys stay within LEX_KEY_BUDGET
+  const int64_t per_q = std::max<int64_t>(1, std::min<int64_t>((int64_t)Lq * max_df_, rows_));
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>({1024, (int64_t)B, LEX_KEY_BUDGET / per_q}));
+  const int64_t nslots = (int64_t)G * Lq;
+  size_t o = 0;
+  auto carve = [&](size_t bytes) {
+    const size_t at = o;
+    o += (size_t)round_up((int64_t)std::max<size_t>(bytes, 1), 256);
+    return at;
+  };
+  const size_t o_sl = carve((size_t)nslots * sizeof(LexTerm)), o_so = carve((size_t)(G + 1) * 4),
+               o_ko = carve((size_t)(G + 1) * 8), o_cnt = carve((size_t)G * 4),
+               o_bnd = carve((size_t)nslots * (NB + 1) * 4), o_keys = carve((size_t)G * per_q * 8),
+               o_avg = carve(4);
+  ws_.reserve(o);
+  char* w = ws_.as<char>();
+  LexTerm* d_sl = reinterpret_cast<LexTerm*>(w + o_sl);
+  int* d_so = reinterpret_cast<int*>(w + o_so);
+  int64_t* d_ko = reinterpret_cast<int64_t*>(w + o_ko);
+  int* d_cnt = reinterpret_cast<int*>(w + o_cnt);
+  int32_t* d_bnd = reinterpret_cast<int32_t*>(w + o_bnd);
+  uint64_t* d_keys = reinterpret_cast<uint64_t*>(w + o_keys);
+  float* d_avg = reinterpret_cast<float*>(w + o_avg);
+  for (int b0 = 0; b0 < B; b0 += G) {
+    const int qb = std::min(G, B - b0);
+    hipLaunchKernelGGL(lex_qprep_kernel, dim3(1), dim3(1024), 0, s, tok + (int64_t)b0 * Lq, qlen + b0,
+                       qb, Lq, off_.as<int64_t>(), vocab_, rows_, live_n_, sum_dl_, gstats,
+                       (int64_t)b0 * Lq, d_sl, d_so, d_ko, d_cnt, d_avg);
+    SR_LAUNCH_CHECK();
+    const int64_t ns = (int64_t)qb * Lq;
+    if (ns) {
+      const int64_t nb = ns * (NB + 1);
+      hipLaunchKernelGGL(lex_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, s, d_sl,
+                         (int)ns, NB, post_.as<uint64_t>(), d_bnd);
+      SR_LAUNCH_CHECK();
+      ProfScope prof("lex_score", s, 0.0, 0.0);
+      hipLaunchKernelGGL(lex_score_kernel, dim3((unsigned)qb, (unsigned)NB), dim3(LEX_THREADS),
+                         LEX_RB * 4, s, d_sl, d_so, d_bnd, NB, post_.as<uint64_t>(),
+                         dlen_.as<int32_t>(), (const uint8_t*)nullptr, rows_, d_avg, k1_, b_, d_cnt,
+                         d_ko, d_keys);
+      SR_LAUNCH_CHECK();
+    }
+    {
+      ProfScope prof("lex_select", s, 0.0, 0.0);
+      hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), sizeof(LexSelSmem), s,
+                         d_keys, d_cnt, d_ko, k, out_score + (int64_t)b0 * k,
+                         out_rows + (int64_t)b0 * k, row_offset);
+      SR_LAUNCH_CHECK();
+    }
+  }
+  end(s);
+}
+
 void LexIndex::search_host(const int64_t* qoff, const int32_t* qterms, int B, int k,
                            const uint8_t* allow, int64_t mask_key, float* out_score,
-                           int64_t* out_rows) {
+                           int64_t* out_rows, const sr_lex_global* glob) {
   if (B == 0) return;
   SR_CHECK(out_score && out_rows, "lex.search: null output");
   DeviceGuard g(device_);
@@ -730,7 +919,7 @@ void LexIndex::search_host(const int64_t* qoff, const int32_t* qterms, int B, in
   out_.reserve((size_t)round_up((int64_t)ob * 4, 16) + ob * 8);
   float* ds = out_.as<float>();
   int64_t* dr = reinterpret_cast<int64_t*>(out_.as<char>() + round_up((int64_t)ob * 4, 16));
-  search_dev(qoff, qterms, B, k, allow, mask_key, ds, dr, stream_);
+  search_dev(qoff, qterms, B, k, allow, mask_key, ds, dr, stream_, glob);
   SR_HIP(hipMemcpyAsync(out_score, ds, ob * 4, hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipMemcpyAsync(out_rows, dr, ob * 8, hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipStreamSynchronize(stream_));

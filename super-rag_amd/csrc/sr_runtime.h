@@ -247,10 +247,20 @@ class LexIndex {
   void search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
                   int64_t mask_key, float* out_score, int64_t* out_rows, hipStream_t s,
                   const sr_lex_global* glob = nullptr, int64_t row_offset = 0);
+  // device-resident queries: tok [B, Lq] int32 (row stride Lq), qlen [B] int32, both in HBM.
+  // query_stats_dev writes [n_live, sum_dl, df of every (query, position)] (2 + B Lq int64, the
+  // vector a row-sharded corpus sums over its shards); search_tok_dev scores with those summed
+  // statistics (gstats, device) or this index's own (null).  No host synchronisation.
+  void query_stats_dev(const int32_t* tok, const int32_t* qlen, int B, int Lq, int64_t* out,
+                       hipStream_t s);
+  void search_tok_dev(const int32_t* tok, const int32_t* qlen, int B, int Lq, int k,
+                      const int64_t* gstats, float* out_score, int64_t* out_rows, hipStream_t s,
+                      int64_t row_offset);
   void totals(int64_t* n_live, int64_t* sum_dl) const;
   void df(const int32_t* terms, int n, int64_t* out);
   void search_host(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
-                   int64_t mask_key, float* out_score, int64_t* out_rows);
+                   int64_t mask_key, float* out_score, int64_t* out_rows,
+                   const sr_lex_global* glob = nullptr);
   void stats(int64_t* rows, int64_t* live, int64_t* postings, int64_t* vocab, double* avgdl);
   void save(const char* path);
   static LexIndex* load(const char* path, int device);
@@ -274,7 +284,7 @@ class LexIndex {
   float k1_, b_;
   hipStream_t stream_ = nullptr;
   hipEvent_t done_ = nullptr;
-  int64_t rows_ = 0, live_n_ = 0, P_ = 0, vocab_ = 0, nnz_ = 0, sum_dl_ = 0;
+  int64_t rows_ = 0, live_n_ = 0, P_ = 0, vocab_ = 0, nnz_ = 0, sum_dl_ = 0, max_df_ = 0;
   bool dirty_ = true;
   // device: forward index, per-row data, inverted index, workspaces
   DevBuf fterm_, fval_, dlen_, live_, off_, post_, ws_, out_, mask_;

@@ -101,6 +101,12 @@ SIGNATURES = {
     "sr_lex_df": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "sr_lex_search_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                   c_void_p, c_int64, c_void_p]),
+    "sr_lex_search_global": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64,
+                                     c_void_p, c_void_p, c_void_p]),
+    "sr_lex_query_stats_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                       c_void_p]),
+    "sr_lex_search_tok_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                      c_void_p, c_void_p, c_int64, c_void_p]),
     "sr_lex_save": (c_int, [c_void_p, c_char_p]),
     "sr_lex_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
     "sr_lex_compact": (c_int, [c_void_p, c_void_p]),

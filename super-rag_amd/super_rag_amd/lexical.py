@@ -176,8 +176,10 @@ class NativeLexIndex:
         return {"rows": v[0].value, "live": v[1].value, "postings": v[2].value,
                 "vocab": v[3].value, "avgdl": a.value}
 
-    def search(self, queries: Sequence[Sequence[int]], k: int, allow=None, mask_key: int = 0):
-        """BM25 top-k per query (token-id lists) -> (score [B,k] fp32 desc, rows [B,k] int64)."""
+    def search(self, queries: Sequence[Sequence[int]], k: int, allow=None, mask_key: int = 0,
+               global_stats=None):
+        """BM25 top-k per query (token-id lists) -> (score [B,k] fp32 desc, rows [B,k] int64).
+        global_stats: (n_live, sum_dl, terms, df) of a whole row-sharded corpus (ShardedLex)."""
         Bq = len(queries)
         scores = np.empty((Bq, k), dtype=np.float32)
         rows = np.empty((Bq, k), dtype=np.int64)
@@ -185,8 +187,17 @@ class NativeLexIndex:
             return scores, rows
         qoff, qterms = query_arrays(queries)
         a = None if allow is None else _mask(allow, self.stats()["rows"])
-        N.call("sr_lex_search", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
-               None if a is None else N.ptr(a), int(mask_key), N.ptr(scores), N.ptr(rows))
+        if global_stats is None:
+            N.call("sr_lex_search", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+                   None if a is None else N.ptr(a), int(mask_key), N.ptr(scores), N.ptr(rows))
+        else:
+            n_live, sum_dl, gt, gdf = global_stats
+            gt = np.ascontiguousarray(gt, dtype=np.int32)
+            gdf = np.ascontiguousarray(gdf, dtype=np.int64)
+            g = LexGlobalC(int(n_live), int(sum_dl), gt.ctypes.data, gdf.ctypes.data, int(gt.size))
+            N.call("sr_lex_search_global", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+                   None if a is None else N.ptr(a), int(mask_key), ctypes.byref(g), N.ptr(scores),
+                   N.ptr(rows))
         return scores, rows
 
     def totals(self):
@@ -228,11 +239,210 @@ class NativeLexIndex:
                int(row_offset), N.stream_handle(stream))
         return out_score, out_rows
 
+    def query_stats_dev(self, tok, qlen, stream=None):
+        """Device-resident queries (torch int32 tok [B, Lq], qlen [B] on this device) -> int64 device
+        vector [live rows, summed length, df of every (query, position)]: the statistics a
+        row-sharded corpus all-reduces before search_tok_dev (no host synchronisation)."""
+        import torch
+        tok, qlen = _dev_i32(tok), _dev_i32(qlen)
+        B, Lq = tok.shape
+        out = torch.empty(2 + B * Lq, dtype=torch.int64, device=tok.device)
+        N.call("sr_lex_query_stats_dev", self._h, N.ptr(tok), N.ptr(qlen), B, Lq, N.ptr(out),
+               N.stream_handle(stream))
+        return out
+
+    def search_tok_dev(self, tok, qlen, k: int, gstats=None, row_offset: int = 0, stream=None):
+        """BM25 top-k of device-resident queries (query i = tok[i, :qlen[i]], term ids) -> device
+        (score [B, k] fp32, rows [B, k] int64 + row_offset); gstats: the all-reduced
+        query_stats_dev vector of a row-sharded corpus, or None for this index's own statistics.
+        Identical results to search_dev on the same queries, without the host round trip."""
+        import torch
+        tok, qlen = _dev_i32(tok), _dev_i32(qlen)
+        B, Lq = tok.shape
+        score = torch.empty((B, k), dtype=torch.float32, device=tok.device)
+        rows = torch.empty((B, k), dtype=torch.int64, device=tok.device)
+        if gstats is not None:
+            gstats = gstats.contiguous()
+            assert gstats.dtype == torch.int64 and gstats.numel() == 2 + B * Lq and gstats.is_cuda
+        N.call("sr_lex_search_tok_dev", self._h, N.ptr(tok), N.ptr(qlen), B, Lq, int(k),
+               None if gstats is None else N.ptr(gstats), N.ptr(score), N.ptr(rows),
+               int(row_offset), N.stream_handle(stream))
+        return score, rows
+
     def hybrid(self, store, queries, query_terms, k: int, k_each: Optional[int] = None,
                rank_const: int = 1, min_score: float = float("-inf"), allow=None, mask_key: int = 0):
         """hybrid_search over (store, this index)."""
         return hybrid_search(store, self, queries, query_terms, k, k_each, rank_const, min_score,
                              allow, mask_key)
+
+
+class ShardedLex:
+    """BM25 index of a row-sharded collection (store.ShardedStore, ctx "devices"): one lexical shard
+    per store shard, on the same device and holding the same rows (the store's routing tables), so
+    a fulltext / hybrid collection can span GPUs.  Every shard scores with the corpus-wide N,
+    summed length and df of the query terms (sr_lex_search_global; the totals and df are summed on
+    the host, as the connector's queries are host arrays), each shard's top-k is mapped to global
+    rows and the lists merge on (score desc, global row asc) -- one index's order, so results equal
+    a single-device collection's (exactly while a query's BM25 score stays below 256, where its
+    2^-16 fixed-point value is still exact in the fp32 score the shards report).  Global rows are
+    the store's: ``add`` must follow the store's add of the same rows (the connector's order)."""
+
+    MAGIC = "SRMILEXSHARDS1"
+
+    def __init__(self, store, factory=None, _shards=None, _tables=None):
+        self.store = store
+        self.devices = list(store.devices)
+        factory = factory or (lambda dev: NativeLexIndex(dev))
+        self.shards = _shards if _shards is not None else [factory(d) for d in self.devices]
+        self.tables = _tables if _tables is not None else [np.zeros(0, np.int64) for _ in self.devices]
+
+    def _n(self) -> int:
+        return sum(len(t) for t in self.tables)
+
+    def add(self, docs) -> int:
+        """Documents of global rows [first, first + n) (first = rows so far), each to the shard
+        the store put its row on."""
+        first = self._n()
+        n = len(docs)
+        g = np.arange(first, first + n, dtype=np.int64)
+        if n and (g[-1] >= len(self.store.shard_of)):
+            raise RuntimeError("lexical rows ahead of the store")
+        for s, sh in enumerate(self.shards):
+            sel = np.nonzero(self.store.shard_of[g] == s)[0] if n else np.zeros(0, np.int64)
+            if not sel.size:
+                continue
+            loc = self.store.local_of[g[sel]]
+            got = sh.add([docs[i] for i in sel.tolist()])
+            if int(got) != int(loc[0]) or not np.array_equal(loc, np.arange(loc[0], loc[0] + len(loc))):
+                raise RuntimeError("lexical shard rows out of step with the store shard")
+            self.tables[s] = np.concatenate([self.tables[s], g[sel]])
+        return first
+
+    def _route(self, rows):
+        r = np.asarray(rows, dtype=np.int64)
+        owner = np.full(self._n(), -1, np.int64)
+        local = np.full(self._n(), -1, np.int64)
+        for s, t in enumerate(self.tables):
+            owner[t] = s
+            local[t] = np.arange(len(t))
+        return r, owner, local
+
+    def remove(self, rows) -> None:
+        r, owner, local = self._route(rows)
+        for s, sh in enumerate(self.shards):
+            sel = r[owner[r] == s]
+            if sel.size:
+                sh.remove(local[sel])
+
+    def compact(self) -> np.ndarray:
+        n = self._n()
+        alive = np.zeros(n, bool)
+        for s, sh in enumerate(self.shards):
+            m = np.asarray(sh.compact())
+            keep = m >= 0
+            alive[self.tables[s][keep]] = True
+            self.tables[s] = self.tables[s][keep]
+        remap = np.full(n, -1, np.int64)
+        remap[alive] = np.arange(int(alive.sum()))
+        self.tables = [remap[t] for t in self.tables]
+        return remap
+
+    def stats(self) -> dict:
+        out = {"rows": 0, "live": 0}
+        for sh in self.shards:
+            st = sh.stats()
+            out["rows"] += st["rows"]
+            out["live"] += st["live"]
+        return out
+
+    def totals(self):
+        n = d = 0
+        for sh in self.shards:
+            a, b = sh.totals()
+            n, d = n + a, d + b
+        return n, d
+
+    def global_stats(self, queries):
+        terms = np.unique(np.asarray([int(t) for q in queries for t in q], dtype=np.int64)).astype(np.int32)
+        n_live, sum_dl = self.totals()
+        df = np.zeros(terms.size, np.int64)
+        for sh in self.shards:
+            df += np.asarray(sh.df(terms), np.int64)
+        return n_live, sum_dl, terms, df
+
+    def search(self, queries, k: int, allow=None, mask_key: int = 0):
+        Bq = len(queries)
+        st = self.global_stats(queries)
+        scores, rows = [], []
+        for s, sh in enumerate(self.shards):
+            a = None if allow is None else np.asarray(allow, dtype=np.uint8)[self.tables[s]]
+            sc, r = sh.search(queries, k, allow=a, mask_key=(int(mask_key) << 6) | s if a is not None else 0,
+                              global_stats=st)
+            t = self.tables[s]
+            g = np.where(r >= 0, t[np.clip(r, 0, None)] if len(t) else -1, -1)
+            scores.append(np.where(g >= 0, np.asarray(sc, np.float32), -np.inf))
+            rows.append(g)
+        S, R = np.concatenate(scores, 1), np.concatenate(rows, 1)
+        out_s = np.full((Bq, k), -np.inf, np.float32)
+        out_r = np.full((Bq, k), -1, np.int64)
+        for b in range(Bq):
+            big = np.where(R[b] >= 0, R[b], np.iinfo(np.int64).max)
+            o = np.lexsort((big, -S[b].astype(np.float64)))[:k]
+            ok = R[b][o] >= 0
+            out_s[b, : ok.sum()] = S[b][o][ok]
+            out_r[b, : ok.sum()] = R[b][o][ok]
+        return out_s, out_r
+
+    def hybrid(self, store, queries, query_terms, k: int, k_each: Optional[int] = None,
+               rank_const: int = 1, min_score: float = float("-inf"), allow=None, mask_key: int = 0):
+        """Dense top-k_each over the sharded store and BM25 top-k_each over these shards, fused by
+        rrf (sr_hybrid_search's three steps on a sharded collection)."""
+        k_each = int(k_each or k)
+        _, dense = store.search(queries, k_each, allow=allow, mask_key=mask_key)
+        _, lex = self.search(query_terms, k_each, allow=allow, mask_key=mask_key)
+        return _rrf_rows(dense, lex, k, rank_const, min_score, self.devices[0])
+
+    def save(self, path: str) -> None:
+        import json
+        import os
+        for i, sh in enumerate(self.shards):
+            sh.save(f"{path}.s{i}")
+        np.savez(f"{path}.rows.tmp.npz", **{f"s{i}": t for i, t in enumerate(self.tables)})
+        os.replace(f"{path}.rows.tmp.npz", f"{path}.rows.npz")
+        with open(path + ".tmp", "w") as f:
+            json.dump({"magic": self.MAGIC, "shards": len(self.shards)}, f)
+        os.replace(path + ".tmp", path)
+
+    @classmethod
+    def is_manifest(cls, path: str) -> bool:
+        with open(path, "rb") as f:
+            return cls.MAGIC.encode() in f.read(64)
+
+    @classmethod
+    def load(cls, path: str, store, loader=None) -> "ShardedLex":
+        import json
+        with open(path) as f:
+            man = json.load(f)
+        if man.get("magic") != cls.MAGIC or int(man["shards"]) != len(store.devices):
+            raise IOError(f"{path}: a {man.get('shards')}-shard lexical index cannot load on "
+                          f"devices {store.devices}")
+        loader = loader or (lambda p, dev: NativeLexIndex.load(p, dev))
+        shards = [loader(f"{path}.s{i}", d) for i, d in enumerate(store.devices)]
+        with np.load(f"{path}.rows.npz") as z:
+            tables = [z[f"s{i}"].astype(np.int64) for i in range(len(store.devices))]
+        return cls(store, _shards=shards, _tables=tables)
+
+
+def _rrf_rows(rows_a, rows_b, k, rank_const, min_score, device):
+    """rrf of two host row lists on the device (rrf_fuse), or through the test seam."""
+    return _rrf_impl[0](rows_a, rows_b, k, rank_const, min_score, device)
+
+
+def _dev_i32(t):
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise TypeError("device-resident lexical queries must be CUDA tensors")
+    return t.to(torch.int32).contiguous()
 
 
 def rrf_fuse(rows_a, rows_b, k: int, rank_const: int = 1, min_score: float = 0.0,
@@ -286,3 +496,11 @@ def hybrid_search(store, lex: NativeLexIndex, queries, query_terms: Sequence[Seq
            k_each, int(rank_const), float(min_score), None if a is None else N.ptr(a),
            int(mask_key), N.ptr(scores), N.ptr(rows))
     return scores, rows
+
+
+_rrf_impl = [lambda a, b, k, rc, ms, dev: rrf_fuse(a, b, k, rc, ms, dev)]
+
+
+def set_rrf_backend(fn) -> None:
+    """Test seam: replace the host-list rrf used by ShardedLex.hybrid (CPU doubles)."""
+    _rrf_impl[0] = fn or (lambda a, b, k, rc, ms, dev: rrf_fuse(a, b, k, rc, ms, dev))

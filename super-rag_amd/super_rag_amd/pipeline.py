@@ -102,14 +102,18 @@ class SearchPipeline:
 
     def retrieve_hybrid(self, q_emb: torch.Tensor, q_tok: torch.Tensor, q_len: torch.Tensor):
         """Dense top-k_each + BM25 top-k_each (query tokens) fused by rrf -> (rrf score, rows)
-        [B, K] of this rank's queries."""
-        import numpy as np
-        from .lexical import query_arrays, rrf_fuse_dev
+        [B, K] of this rank's queries.  Everything stays on the device: the query tokens go to the
+        lexical kernels as a padded [B, Lq] matrix (sr_lex_search_tok_dev), and sharded, the
+        corpus-wide N, summed length and per-(query, position) df are one device vector
+        (sr_lex_query_stats_dev) summed by one all_reduce (RCCL) before scoring."""
+        from .lexical import rrf_fuse_dev
         B = q_emb.shape[0]
         dev = q_emb.device
         ke = self.k_each
+        toks, lens = q_tok.to(torch.int32).contiguous(), q_len.to(torch.int32).contiguous()
+        gst = None
         if not self.exchange:
-            allq, toks, lens = q_emb, q_tok, q_len
+            allq = q_emb
         else:
             import torch.distributed as dist
             host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda
@@ -120,24 +124,16 @@ class SearchPipeline:
                                   device=x.device)
                 dist.all_gather_into_tensor(out, x, group=self.group)
                 return out.to(dev) if host else out
-            allq, toks, lens = gather(q_emb), gather(q_tok), gather(q_len)
-        t_np, l_np = toks.cpu().numpy(), lens.cpu().numpy()
-        queries = [t_np[i, :l_np[i]] for i in range(t_np.shape[0])]
-        qoff, qterms = query_arrays(queries)
-        stats = None
-        if self.exchange:
-            import torch.distributed as dist
-            host = dist.get_backend(self.group) == "gloo"
-            terms = np.unique(qterms[: qoff[-1]]).astype(np.int32)
-            n_live, sum_dl = self.lexical.totals()
-            v = torch.from_numpy(np.concatenate([[n_live, sum_dl], self.lexical.df(terms)]).astype(np.int64))
-            v = v if host else v.to(dev)
-            dist.all_reduce(v, group=self.group)
-            v = v.cpu().numpy()
-            stats = (int(v[0]), int(v[1]), terms, v[2:])
+            allq, toks, lens = gather(q_emb), gather(toks), gather(lens)
+            gst = self.lexical.query_stats_dev(toks, lens)
+            if host:
+                g = gst.cpu()
+                dist.all_reduce(g, group=self.group)
+                gst = g.to(dev)
+            else:
+                dist.all_reduce(gst, group=self.group)
         sims, rows = self.store.search_dev(allq, ke, row_offset=self.offset)
-        lsc, lrows = self.lexical.search_dev(qoff, qterms, ke, global_stats=stats,
-                                             row_offset=self.offset)
+        lsc, lrows = self.lexical.search_tok_dev(toks, lens, ke, gstats=gst, row_offset=self.offset)
         if self.exchange:
             import torch.distributed as dist
             host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda

@@ -12,7 +12,9 @@ Mirrors SeekDBVectorStoreConnector (super_rag/vectorstore/seekdb_connector.py:31
 Opt-in lexical retrieval (ctx ``fulltext``): every added node's text is also indexed for BM25 on
 the device (lexical.py, k_lex.hip); ``fulltext_search(text, top_k, keywords)`` backs the
 reference's ``fulltext_search`` node type, and ctx ``hybrid`` makes ``search`` fuse the dense and
-the BM25 rankings by reciprocal rank on the device (score = rrf score, descending).
+the BM25 rankings by reciprocal rank on the device (score = rrf score, descending).  Both work on
+collections sharded over several devices (ctx ``devices``: lexical.ShardedLex, corpus-wide BM25
+statistics), with the same results as one device.
 Collections are process-wide (like a server): every connector object for the same collection
 name sees the same rows.  Row ids <-> uuid strings, texts and metadata live on the host; vectors
 live in HBM.  With ``ctx["snapshot_dir"]`` a collection is reloaded at construction and
@@ -118,12 +120,16 @@ class _Collection:
         self.journal = None     # persist.Journal with ctx["snapshot_dir"]
 
     def ensure_lex(self) -> None:
-        """Create the lexical index, back-filling the rows added before it existed."""
+        """Create the lexical index, back-filling the rows added before it existed.  A collection
+        sharded over several devices gets a ShardedLex over the same shards."""
         if self.lex is not None:
             return
-        from .lexical import Vocab, analyze
+        from .lexical import ShardedLex, Vocab, analyze
         vocab = Vocab()
-        lex = _lex_factory(self.device)
+        if hasattr(self.store, "shard_of"):
+            lex = ShardedLex(self.store, factory=lambda dev: _lex_factory(dev))
+        else:
+            lex = _lex_factory(self.device)
         if self.ids:
             lex.add([vocab.doc_ids(analyze(t)) if t is not None else [] for t in self.texts])
             dead = [r for r, u in enumerate(self.ids) if u is None]
@@ -200,8 +206,13 @@ class _Collection:
         c.metadatas = meta["metadatas"]
         c.row_of = {u: i for i, u in enumerate(c.ids) if u is not None}
         if "lex_vocab" in meta and os.path.exists(j.lex_path(gen)):
-            from .lexical import Vocab
-            c.lex = _lex_loader(j.lex_path(gen), device)
+            from .lexical import ShardedLex, Vocab
+            if ShardedLex.is_manifest(j.lex_path(gen)):
+                if not hasattr(store, "shard_of"):
+                    raise IOError(f"{j.lex_path(gen)}: a sharded lexical index for a single-device store")
+                c.lex = ShardedLex.load(j.lex_path(gen), store, loader=lambda p, d: _lex_loader(p, d))
+            else:
+                c.lex = _lex_loader(j.lex_path(gen), device)
             c.vocab = Vocab(meta["lex_vocab"])
         j.gen = gen
         c.journal = j
@@ -234,8 +245,6 @@ class MI355XVectorStoreConnector:
         # ctx "devices": shard the collection's rows over several GPUs (store.ShardedStore)
         devs = ctx.get("devices")
         self.devices = [int(d) for d in devs] if devs else None
-        if self.devices and len(self.devices) > 1 and (ctx.get("fulltext") or ctx.get("hybrid")):
-            raise ValueError("fulltext / hybrid collections are single-device (ctx 'devices')")
         self.snapshot_dir = ctx.get("snapshot_dir")
         self.coalesce = bool(ctx.get("coalesce", True))
         self.max_batch = int(ctx.get("max_batch", 256))

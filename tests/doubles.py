@@ -126,9 +126,23 @@ class NumpyLex:
         x.docs, x.live = d["docs"], np.asarray(d["live"], bool)
         return x
 
-    def search(self, queries, k, allow=None, mask_key=0):
+    def totals(self):
+        c = self._corpus()
+        return int(c.live.sum()), int(c.dl[c.live].sum())
+
+    def df(self, terms):
+        c = self._corpus()
+        return np.asarray([int(c.df[t]) if 0 <= t < c.vocab else 0 for t in np.asarray(terms).tolist()],
+                          np.int64)
+
+    def search(self, queries, k, allow=None, mask_key=0, global_stats=None):
         from oracle.bm25 import bm25_topk
-        return bm25_topk(self._corpus(), queries, k, allow=allow)
+        st = None
+        if global_stats is not None:
+            n_live, sum_dl, gt, gdf = global_stats
+            d = dict(zip(np.asarray(gt).tolist(), np.asarray(gdf).tolist()))
+            st = (n_live, sum_dl, d.__getitem__)
+        return bm25_topk(self._corpus(), queries, k, allow=allow, stats=st)
 
     def hybrid(self, store, queries, query_terms, k, k_each=None, rank_const=1,
                min_score=float("-inf"), allow=None, mask_key=0):

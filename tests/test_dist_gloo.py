@@ -125,3 +125,115 @@ def test_sharded_passage_fetch_equals_replicated_table(world):
         ok = c >= 0
         np.testing.assert_array_equal(tq[idx[ok]], p_tok.numpy()[c[ok]])
         np.testing.assert_array_equal(lq[idx[ok]], p_len.numpy()[c[ok]])
+
+
+class ShardLexDouble:
+    """CPU double of NativeLexIndex's device-resident query path (query_stats_dev /
+    search_tok_dev) over one shard, on the oracle's BM25 (oracle/bm25.py) with the statistics
+    vector layout of sr_lex_query_stats_dev: [live rows, summed length, df per (query, pos)]."""
+
+    def __init__(self, off, terms, tf, dl):
+        from oracle.bm25 import LexCorpus
+        self.c = LexCorpus(off, terms, tf, dl)
+
+    def query_stats_dev(self, tok, qlen):
+        B, Lq = tok.shape
+        out = torch.zeros(2 + B * Lq, dtype=torch.int64)
+        out[0] = int(self.c.live.sum())
+        out[1] = int(self.c.dl[self.c.live].sum())
+        for q in range(B):
+            for i in range(int(qlen[q])):
+                t = int(tok[q, i])
+                out[2 + q * Lq + i] = int(self.c.df[t]) if 0 <= t < self.c.vocab else 0
+        return out
+
+    def search_tok_dev(self, tok, qlen, k, gstats=None, row_offset=0):
+        from oracle.bm25 import bm25_topk
+        B, Lq = tok.shape
+        queries = [tok[q, :int(qlen[q])].tolist() for q in range(B)]
+        stats = None
+        if gstats is not None:
+            g = gstats.tolist()
+            stats = []
+            for q in range(B):
+                d = {int(tok[q, i]): g[2 + q * Lq + i] for i in range(int(qlen[q]))}
+                stats.append((g[0], g[1], d.__getitem__))
+        sc, rows = bm25_topk(self.c, queries, k, stats=stats)
+        rows = np.where(rows >= 0, rows + row_offset, -1)
+        return torch.from_numpy(sc), torch.from_numpy(rows)
+
+
+def rrf_double(rows_a, rows_b, k, rank_const=1, min_score=float("-inf"), stream=None):
+    from oracle.bm25 import rrf_rows
+    sc, rows = rrf_rows(rows_a.numpy(), rows_b.numpy(), k, rank_const, min_score)
+    return torch.from_numpy(sc), torch.from_numpy(rows)
+
+
+def _lex_corpus(n, seed):
+    rng = np.random.default_rng(seed)
+    docs = [rng.zipf(1.3, rng.integers(1, 12)) % 60 for _ in range(n)]
+    from super_rag_amd.lexical import doc_arrays
+    return doc_arrays([d.tolist() for d in docs])
+
+
+def _hybrid_worker(rank, world, port, corpus, queries, qtok, qlen, k, out_q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "super-rag_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from super_rag_amd import lexical
+    from super_rag_amd.pipeline import SearchPipeline
+    lexical.rrf_fuse_dev = rrf_double
+    off, terms, tf, dl = _lex_corpus(corpus.shape[0], 5)
+    n = corpus.shape[0]
+    per = (n + world - 1) // world
+    r0, r1 = rank * per, min(n, (rank + 1) * per)
+    lo, hi = off[r0], off[r1]
+    lex = ShardLexDouble(off[r0:r1 + 1] - lo, terms[lo:hi], tf[lo:hi], dl[r0:r1])
+    pipe = SearchPipeline(None, None, ShardStoreDouble(corpus[r0:r1]), None, None, k_candidates=k,
+                          shard_offset=r0, merge_fn=merge_double, lexical=lex, k_each=k)
+    B = queries.shape[0] // world
+    sl = slice(rank * B, (rank + 1) * B)
+    score, rows = pipe.retrieve_hybrid(queries[sl], qtok[sl], qlen[sl])
+    out_q.put((rank, score.numpy(), rows.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_hybrid_retrieve_equals_single_index(world):
+    """Config-5 hybrid retrieval sharded: every shard scores BM25 with the corpus-wide statistics
+    (one all_reduce of the sr_lex_query_stats_dev vector), both per-shard lists take the same
+    all_to_all + merge and the rrf fusion of a rank's queries equals the single-index fusion."""
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "super-rag_amd")]
+    g = torch.Generator().manual_seed(4)
+    n, d, k = 503, 16, 9
+    corpus = torch.randn(n, d, generator=g)
+    queries = torch.randn(8, d, generator=g)
+    qtok = torch.randint(0, 70, (8, 6), generator=g, dtype=torch.int32)   # some terms unknown
+    qlen = torch.tensor([6, 3, 0, 5, 6, 1, 4, 2], dtype=torch.int32)
+    qtok[3, :3] = qtok[3, 0]                                             # repeated term
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000 + 13 * world
+    procs = [ctx.Process(target=_hybrid_worker,
+                         args=(r, world, port, corpus, queries, qtok, qlen, k, out_q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, rr)) for r, s, rr in (out_q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single index over the whole corpus, its own statistics
+    lex = ShardLexDouble(*_lex_corpus(n, 5))
+    _, drows = ShardStoreDouble(corpus).search_dev(queries, k)
+    _, lrows = lex.search_tok_dev(qtok, qlen, k)
+    want_s, want_r = rrf_double(drows, lrows, k)
+    assert (lrows >= 0).sum() > 8          # the lexical lists are not empty
+    B = queries.shape[0] // world
+    for r in range(world):
+        s, rows = res[r]
+        np.testing.assert_array_equal(rows, want_r[r * B:(r + 1) * B].numpy())
+        np.testing.assert_array_equal(s, want_s[r * B:(r + 1) * B].float().numpy())

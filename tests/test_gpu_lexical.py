@@ -205,3 +205,71 @@ def test_bm25_ties_beyond_the_lds_collect_capacity():
         np.testing.assert_array_equal(r, ro)
         np.testing.assert_array_equal(s, so)
     assert r[0, :3].tolist() == [20000, 20001, 20002] and r[0, 3] == 0
+
+
+def _pad(qs, Lq=None):
+    import torch
+    Lq = Lq or max(1, max(len(q) for q in qs))
+    tok = np.full((len(qs), Lq), -7, dtype=np.int32)     # padding past qlen is never read as a term
+    for i, q in enumerate(qs):
+        tok[i, :len(q)] = q
+    qlen = np.asarray([len(q) for q in qs], dtype=np.int32)
+    return torch.from_numpy(tok).cuda(), torch.from_numpy(qlen).cuda()
+
+
+@pytest.mark.parametrize("n,vocab,k", [(20000, 3000, 100), (5000, 50, 1024)])
+def test_device_resident_queries_equal_the_host_path(n, vocab, k):
+    """sr_lex_search_tok_dev (padded query tokens in HBM, term slots / idf / key offsets built on the
+    device) == sr_lex_search_dev (host-built slots) == the oracle, bit for bit, including repeated,
+    unknown and empty queries; no host synchronisation is needed for the launch."""
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(n + 1)
+    docs = _docs(rng, n, vocab)
+    lex = NativeLexIndex()
+    lex.add(docs)
+    dead = rng.choice(n, n // 20, replace=False)
+    lex.remove(dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    qs = _queries(rng, 300, vocab)           # > 256: two query groups would also work
+    tok, qlen = _pad(qs)
+    s, r = lex.search_tok_dev(tok, qlen, k, row_offset=1000)
+    so, ro = bm25_topk(_oracle(docs, live), qs, k)
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(np.where(r >= 0, r - 1000, -1), ro)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
+    sh, rh = lex.search(qs, k)
+    np.testing.assert_array_equal(rh, ro)
+
+
+def test_device_stats_of_two_shards_equal_one_index():
+    """Two shards scoring with the summed sr_lex_query_stats_dev vector (corpus-wide N, avgdl, df)
+    and merged on (score, row) == one index over all rows, bit for bit."""
+    import torch
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(9)
+    n, vocab, k = 12000, 800, 50
+    docs = _docs(rng, n, vocab)
+    qs = _queries(rng, 64, vocab)
+    tok, qlen = _pad(qs, 12)
+    halves = [(0, 5000), (5000, n)]
+    shards = []
+    for a, b in halves:
+        x = NativeLexIndex()
+        x.add(docs[a:b])
+        shards.append(x)
+    g = sum(x.query_stats_dev(tok, qlen) for x in shards)
+    assert int(g[0]) == n and int(g[1]) == sum(len(d) for d in docs)
+    parts = [x.search_tok_dev(tok, qlen, k, gstats=g, row_offset=a) for x, (a, _) in zip(shards, halves)]
+    s = torch.cat([p[0] for p in parts], 1).cpu().numpy()
+    r = torch.cat([p[1] for p in parts], 1).cpu().numpy()
+    so, ro = bm25_topk(_oracle(docs, np.ones(n, bool)), qs, k)
+    for i in range(len(qs)):
+        ok = r[i] >= 0
+        order = np.lexsort((r[i][ok], -s[i][ok]))[:k]
+        got_r, got_s = r[i][ok][order], s[i][ok][order]
+        m = int((ro[i] >= 0).sum())
+        np.testing.assert_array_equal(got_r, ro[i][:m])
+        np.testing.assert_array_equal(got_s, so[i][:m])

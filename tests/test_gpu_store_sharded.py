@@ -136,3 +136,50 @@ def test_native_store_set_equals_single_store(dtype):
     d, r = tiny.search(q[:2], 5)
     assert (r[:, 3:] == -1).all() and np.isinf(d[:, 3:]).all()
     assert sorted(r[0, :3].tolist()) == [0, 1, 2]
+
+
+@pytest.mark.parametrize("mode", ["fulltext", "hybrid"])
+def test_sharded_fulltext_hybrid_collection_equals_one_device(mode):
+    """ctx "devices" with "fulltext" / "hybrid" on the HIP path: per-shard BM25 (sr_lex_search_global
+    with the corpus-wide statistics) merged on (score, row) and rrf-fused with the sharded dense
+    list == the single-device collection (sr_lex_search / sr_hybrid_search), with a filter and
+    after deletes."""
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.lexical import ShardedLex
+    from super_rag_amd.models import QueryWithEmbedding, TextNode
+    rng = np.random.default_rng(5)
+    words = [f"w{i}" for i in range(300)]
+    V._collections.clear()
+    try:
+        base = {mode: True, "honor_filter": True}
+        one = V.MI355XVectorStoreConnector({**base, "collection": "lx1"})
+        many = V.MI355XVectorStoreConnector({**base, "collection": "lx2", "devices": [0, 0, 0]})
+        x = _data(3000, 64, 7)
+        ids1, ids2 = [], []
+        for s in range(0, 3000, 250):
+            nodes = [TextNode(text=" ".join(rng.choice(words, rng.integers(2, 30))),
+                              metadata={"i": i, "chat_id": f"c{i % 4}"}, embedding=x[i].tolist())
+                     for i in range(s, s + 250)]
+            ids1 += one.add(nodes)
+            ids2 += many.add(nodes)
+        assert isinstance(V._get("lx2").lex, ShardedLex)
+        qs = [" ".join(rng.choice(words, rng.integers(1, 6))) for _ in range(12)]
+        qv = _data(12, 64, 8)
+
+        def dump(con, flt=None):
+            kw = {"filter": flt} if flt else {}
+            if mode == "fulltext":
+                return [[(d.text, d.score) for d in con.fulltext_search(q, 20, **kw)] for q in qs]
+            return [[(d.text, d.score) for d in
+                     con.search(QueryWithEmbedding(query=q, top_k=20, embedding=v.tolist()), **kw).results]
+                    for q, v in zip(qs, qv)]
+        assert dump(one) == dump(many)
+        flt = {"chat_id": {"$in": ["c1", "c3"]}}
+        assert dump(one, flt) == dump(many, flt)
+        dead = rng.choice(3000, 700, replace=False)
+        one.delete(ids=[ids1[i] for i in dead])
+        many.delete(ids=[ids2[i] for i in dead])
+        a, b = dump(one), dump(many)
+        assert a == b and sum(len(r) for r in a) > 100
+    finally:
+        V._collections.clear()
