@@ -1,0 +1,159 @@
+"""Throughput of the DROP-IN per-request path on one GPU.
+
+The reference serves one query per request: POST /collections/{id}/searches (api/collections.py:
+272-279) -> CollectionService.execute_search_flow (service/collection_service.py:229-366):
+vector_search -> merge -> rerank.  Here C concurrent closed-loop callers each run that flow through
+this package's drop-in pieces exactly as the route would: super_rag_amd.flow.execute_search_flow
+with the pack's runners (nodeflow_pack.py), the collection's EmbeddingService (embed_query
+coalesced per encoder), ContextManager -> MI355XVectorStoreConnector.search (coalesced per
+collection), RerankService.async_rerank (pairs of concurrent requests coalesced per cross-encoder),
+12-layer bge-base-en embedder and bge-reranker-base cross-encoder (seeded synthetic weights, the
+hashing tokenizer: SUPER_RAG_AMD_SYNTHETIC), vector_topk = 100 candidates reranked at S_pair <= 128.
+
+Reported per concurrency: requests/s, mean coalesced batch per stage (items / device batches of
+each Coalescer), p50 / p99 request latency.  The batched SearchPipeline number (bench.py's headline)
+is the ceiling this path approaches as batches fill; the reference's own host orchestration costs
+5.1 ms per query (profiles/r02_reference_orchestration.json) before any model work.
+
+    python tools/bench_dropin.py [--rows 100000] [--concurrency 64 256] [--seconds 15]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import concurrent.futures
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "super-rag_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+os.environ.setdefault("SUPER_RAG_AMD_SYNTHETIC", "1")
+
+import numpy as np  # noqa: E402
+
+WORDS = [f"w{i:04d}" for i in range(20000)]
+EMBED_MODEL = "bge-base-en"
+RERANK_MODEL = "bge-reranker-base"
+
+
+def build_collection(col_id: str, rows: int, dim: int = 768, words_per_chunk: int = 90, seed: int = 0):
+    """A collection of `rows` chunks through the connector's add (texts + clustered vectors)."""
+    from super_rag_amd import nodeflow_pack as P
+    from super_rag_amd.models import TextNode
+    from super_rag_amd.vectorstore import VectorStoreConnectorAdaptor
+    P.register()
+    P.register_collection(P.LocalCollection(col_id, {"embedding": {"model": EMBED_MODEL}}))
+    con = VectorStoreConnectorAdaptor("mi355x", {"collection": P.collection_name_for(col_id)}).connector
+    con.create_collection(vector_size=dim)
+    rng = np.random.default_rng(seed)
+    centers = rng.standard_normal((256, dim)).astype(np.float32)
+    step = 20000
+    for a in range(0, rows, step):
+        n = min(step, rows - a)
+        v = centers[(np.arange(a, a + n)) % 256] + 0.5 * rng.standard_normal((n, dim)).astype(np.float32)
+        w = rng.integers(0, len(WORDS), (n, words_per_chunk))
+        nodes = [TextNode(text=" ".join(WORDS[j] for j in w[i]), metadata={"source": f"d{a + i}.md"},
+                          embedding=v[i].tolist()) for i in range(n)]
+        con.add(nodes)
+    return con
+
+
+def _coalescers():
+    """(name, Coalescer) of the embed / search / rerank stages, once they exist."""
+    from super_rag_amd import registry
+    from super_rag_amd import vectorstore as V
+    out = {}
+    for (name, _dir, _dev), (enc, _tok) in list(registry._models.items()):
+        c = getattr(enc, "_query_coalescer", None)
+        if c is not None:
+            out["embed"] = c
+        c = getattr(enc, "_pair_coalescer", None)
+        if c is not None:
+            out["rerank"] = c
+    for col in list(V._collections.values()):
+        if col.coalescer is not None:
+            out["search"] = col.coalescer
+    return out
+
+
+async def _closed_loop(n_callers: int, seconds: float, col_id: str, queries, lat: list):
+    from super_rag_amd.flow import execute_search_flow
+    t_end = time.perf_counter() + seconds
+    done = [0]
+
+    async def caller(i):
+        j = i
+        while time.perf_counter() < t_end:
+            q = queries[j % len(queries)]
+            j += n_callers
+            t0 = time.perf_counter()
+            items, _ = await execute_search_flow(q, col_id, "bench", vector_topk=100,
+                                                 rerank_config=(RERANK_MODEL, "local", "mi355x"))
+            lat.append(time.perf_counter() - t0)
+            if len(items) != 100:
+                raise RuntimeError(f"expected 100 reranked items, got {len(items)}")
+            done[0] += 1
+    await asyncio.gather(*[caller(i) for i in range(n_callers)])
+    return done[0]
+
+
+def measure(concurrency: int, seconds: float, col_id: str, queries) -> dict:
+    loop = asyncio.new_event_loop()
+    # one worker thread per concurrent request for the blocking device calls (asyncio.to_thread):
+    # the default executor's min(32, cpus + 4) threads would cap the coalesced batches at 32
+    loop.set_default_executor(concurrent.futures.ThreadPoolExecutor(max_workers=concurrency + 8))
+    try:
+        before = {k: (c.batches, c.items) for k, c in _coalescers().items()}
+        lat: list = []
+        t0 = time.perf_counter()
+        n = loop.run_until_complete(_closed_loop(concurrency, seconds, col_id, queries, lat))
+        dt = time.perf_counter() - t0
+        after = {k: (c.batches, c.items) for k, c in _coalescers().items()}
+    finally:
+        loop.close()
+    stages = {}
+    for k, (b, i) in after.items():
+        b0, i0 = before.get(k, (0, 0))
+        if b > b0:
+            stages[k] = {"batches": b - b0, "mean_batch": round((i - i0) / (b - b0), 2)}
+    lat_ms = np.asarray(lat) * 1e3
+    return {"concurrency": concurrency, "requests": n, "seconds": round(dt, 2),
+            "qps": round(n / dt, 1), "p50_ms": round(float(np.percentile(lat_ms, 50)), 1),
+            "p99_ms": round(float(np.percentile(lat_ms, 99)), 1), "coalesced": stages}
+
+
+def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16) -> dict:
+    col_id = "dropin"
+    t = time.time()
+    build_collection(col_id, rows)
+    setup = time.time() - t
+    rng = np.random.default_rng(7)
+    queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
+    # warm up: models resident, kernels compiled, coalescers created
+    measure(min(warmup, max(concurrency)), 3.0, col_id, queries)
+    out = {"path": ("execute_search_flow (collection_service.py:229-366) -> pack vector_search / "
+                    "merge / rerank runners -> EmbeddingService.embed_query + connector.search + "
+                    "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
+                    "(synthetic weights, hashing tokenizer); vector_topk 100, S_pair <= 128"),
+           "rows": rows, "setup_s": round(setup, 1),
+           "runs": [measure(c, seconds, col_id, queries) for c in concurrency],
+           "reference_orchestration_ms_per_query": 5.14}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=100000)
+    ap.add_argument("--concurrency", type=int, nargs="+", default=[64, 256])
+    ap.add_argument("--seconds", type=float, default=15.0)
+    a = ap.parse_args()
+    print(json.dumps(run(a.rows, a.concurrency, a.seconds)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
