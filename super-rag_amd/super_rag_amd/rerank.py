@@ -23,7 +23,7 @@ logger = logging.getLogger(__name__)
 class RerankService:
     def __init__(self, rerank_provider: str, rerank_model: str, rerank_service_url: str,
                  rerank_service_api_key: str, caching: bool = True, *, encoder=None,
-                 tokenizer=None, device: Optional[int] = None, device_batch: int = 1024,
+                 tokenizer=None, device: Optional[int] = None, device_batch: int = 4096,
                  coalesce: bool = True):
         self.rerank_provider = rerank_provider
         self.model = rerank_model

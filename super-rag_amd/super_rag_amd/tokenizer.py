@@ -71,13 +71,53 @@ class Tokenizer:
                 f"{spec.name}/tokenizer.json (or pass path=); the hashing tokenizer needs the "
                 f"explicit opt-in SUPER_RAG_AMD_SYNTHETIC=1")
         self.synthetic = self._hf is None
+        # caches: a search request re-scores passages the collection already holds, so the
+        # content ids of recently seen texts are kept (bounded; halved when full) and the hashing
+        # tokenizer memoises its word ids
+        self._cache: dict = {}
+        self._cache_cap = 1 << 18
+        self._words: dict = {}
 
     # -- content tokens (no specials) -------------------------------------------------------------
     def content_ids(self, text: str) -> List[int]:
+        hit = self._cache.get(text)
+        if hit is not None:
+            return hit
         if self._hf is not None:
-            return list(self._hf.encode(text, add_special_tokens=False).ids)
-        span = self.spec.vocab_size - _FIRST_ID
-        return [_FIRST_ID + _fnv1a(w.lower()) % span for w in _WORD.findall(text)]
+            ids = list(self._hf.encode(text, add_special_tokens=False).ids)
+        else:
+            ids = [self._word_id(w) for w in _WORD.findall(text)]
+        self._remember(text, ids)
+        return ids
+
+    def content_ids_many(self, texts: Sequence[str]) -> List[List[int]]:
+        """content_ids of many texts; the misses of an HF tokenizer go through one encode_batch
+        (the Rust tokenizer, parallel) instead of one call each."""
+        out: List = [self._cache.get(t) for t in texts]
+        miss = [i for i, o in enumerate(out) if o is None]
+        if miss and self._hf is not None and len(miss) > 1:
+            enc = self._hf.encode_batch([texts[i] for i in miss], add_special_tokens=False)
+            for i, e in zip(miss, enc):
+                out[i] = list(e.ids)
+                self._remember(texts[i], out[i])
+        else:
+            for i in miss:
+                out[i] = self.content_ids(texts[i])
+        return out
+
+    def _word_id(self, w: str) -> int:
+        i = self._words.get(w)
+        if i is None:
+            i = _FIRST_ID + _fnv1a(w.lower()) % (self.spec.vocab_size - _FIRST_ID)
+            if len(self._words) < (1 << 20):
+                self._words[w] = i
+        return i
+
+    def _remember(self, text: str, ids: List[int]) -> None:
+        if len(self._cache) >= self._cache_cap:
+            for k in list(self._cache)[: self._cache_cap // 2]:   # drop the older half
+                self._cache.pop(k, None)
+        self._cache[text] = ids
 
     def content_batch(self, texts: Sequence[str], max_len: int) -> Tuple[np.ndarray, np.ndarray]:
         """[N, max_len] int32 content tokens (truncated, zero padded) and [N] lengths."""
@@ -94,9 +134,8 @@ class Tokenizer:
         """(ids, mask) int32 [B, S], padded to the longest sequence (dynamic padding)."""
         L = min(max_length or self.max_length, self.max_length)
         seqs = []
-        for t in texts:
-            c = self.content_ids(t)[: L - 2]
-            seqs.append([self.spec.bos_id] + c + [self.spec.eos_id])
+        for c in self.content_ids_many(texts):
+            seqs.append([self.spec.bos_id] + c[: L - 2] + [self.spec.eos_id])
         S = max(len(s) for s in seqs)
         ids = np.full((len(seqs), S), self.spec.pad_id, dtype=np.int32)
         mask = np.zeros((len(seqs), S), dtype=np.int32)
@@ -117,8 +156,8 @@ class Tokenizer:
         nspec = 4 if style == 0 else 3
         bos, eos = self.spec.bos_id, self.spec.eos_id
         seqs, types = [], []
-        for p in passages:
-            a, b = list(q), self.content_ids(p)
+        for b in self.content_ids_many(passages):
+            a = q
             na, nb = longest_first(len(a), len(b), L - nspec)
             a, b = a[:na], b[:nb]
             if style == 0:
