@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--cpu-search-rows", type=int, default=0,
                     help="cpu_baseline: corpus rows scanned by the host search (0 = the whole corpus)")
     ap.add_argument("--batches", type=int, default=4, help="distinct resident query batches")
+    ap.add_argument("--dropin-seconds", type=float, default=8.0,
+                    help="drop_in field: seconds per concurrency (64, 256) of the per-request path "
+                         "(0 = skip)")
+    ap.add_argument("--dropin-rows", type=int, default=100000,
+                    help="drop_in field: chunks in the connector collection it searches")
     ap.add_argument("--workload", default="config4", choices=["config4", "config5"],
                     help="config4 (default, the BASELINE metric) or config5: bge-m3 embed, 6.25M x "
                          "1024 rows per GPU scanned in fp8, BM25 over the passage tokens fused by "
@@ -73,9 +78,10 @@ def parse():
     ap.add_argument("--fp8-ffn", action="store_true",
                     help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
                          "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
-    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2),
+    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3),
                     help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
-                         "e4m3 residual copies (dtype f16+fp8ffn / f16+fp8gemm)")
+                         "e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16 "
+                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp)")
     ap.add_argument("--replicate-passages", action="store_true",
                     help="N > 1: keep the whole passage token table on every rank (default: each "
                          "rank holds its shard's rows, the candidates' rows are fetched per batch, "
@@ -312,6 +318,14 @@ def main():
     if rank == 0 and not a.no_extras:
         fidelity = rerank_fidelity(rs, local)
 
+    # ---- the drop-in per-request path (not the headline): concurrent callers through the pack's
+    # runners, coalesced embed / search / rerank, one query per request (tools/bench_dropin.py) ----
+    drop_in = None
+    if rank == 0 and world == 1 and not a.no_extras and a.dropin_seconds > 0:
+        from tools.bench_dropin import run as dropin_run
+        drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds)
+        drop_in["pipeline_qps_same_box"] = round(value, 2)
+
     # ---- roofline of the dominant kernel -------------------------------------------------------
     dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
@@ -380,7 +394,7 @@ def main():
         "metric": metric,
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm")[a.fp8],
+        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm", "f16+fp8mlp")[a.fp8],
         "data": "synthetic",
         "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
@@ -390,6 +404,7 @@ def main():
         "recall_at_10": recall,
         **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
         "rerank_fidelity": fidelity,
+        "drop_in": drop_in,
         "roofline": roof,
         "search_roofline": search_roof,
         "search_b32": search32,
@@ -474,7 +489,7 @@ def rerank_fidelity(rs, device):
                    f"fp32 oracle (tests/golden/rerank_fidelity.npz)"),
            "logit_std_mean": round(float(std.mean()), 4)}
     try:
-        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2")):
+        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3")):
             enc.set_fp8(mode)
             lg = enc.cross_score_dev(dids, dmask)[:, 0].float().cpu().numpy().reshape(ref.shape)
             err = np.abs(lg - ref).max(1)

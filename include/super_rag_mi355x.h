@@ -287,8 +287,9 @@ int sr_cross_score_dev(sr_encoder* e, const int32_t* ids, const int32_t* mask,
  * e.g. the cross-encoders).  1: FFN1 stores OCP e4m3 activations and FFN2 runs the block-scaled
  * fp8 MFMA against an e4m3 copy of its weight (per-row power-of-two scales); 2: also FFN1 and the
  * QKV GEMMs of layers >= 1 on e4m3 copies of the residual sums (written by the residual
- * epilogues) and of the folded weights.  0 (default): fp16.  Opt-in: logits move by the fp8
- * rounding (tests/test_gpu_encoder.py). */
+ * epilogues) and of the folded weights; 3: FFN1 and FFN2 as in mode 2, the QKV projection and
+ * attention stay fp16 (fused).  0 (default): fp16.  Opt-in: logits move by the fp8 rounding
+ * (tests/test_gpu_encoder.py; ranking fidelity per mode: tests/test_gpu_rerank_fidelity.py). */
 int sr_encoder_set_fp8(sr_encoder* e, int mode);
 void sr_encoder_destroy(sr_encoder* e);
 

@@ -83,7 +83,7 @@ def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
     """Final hidden states [B, S, d] in fp32.  fp8 (the library's opt-in precision modes;
     fp8_ffn=True is fp8=1): 1 = the FFN activations 2 GELU(.) rounded to e4m3 and multiplied by
     fp8_rows(fp16(W2 / 2)); 2 = also FFN1 and the QKV of layers >= 1 as _fold8 on the pre-LN
-    residual sums."""
+    residual sums; 3 = FFN1 as in 2, QKV in fp16 (super-rag_amd/csrc/encoder.cpp ffn1_8 / qkv_8)."""
     fp8 = max(fp8, 1 if fp8_ffn else 0)
     # weights given as torch tensors on a device (e.g. fp32 on the GPU for the long-sequence
     # checks) run the same restatement there; numpy weights run on the CPU
@@ -105,7 +105,7 @@ def encode_hidden(cfg: RefConfig, w: dict, ids, mask, type_ids=None,
         p = f"encoder.layer.{l}."
         def lin(x, n):
             return x @ _t(w, p + n + ".weight").T + _t(w, p + n + ".bias")
-        if fp8 >= 2 and l > 0:
+        if fp8 == 2 and l > 0:
             pp = f"encoder.layer.{l - 1}.output.LayerNorm."
             wqkv = torch.cat([_t(w, p + f"attention.self.{n}.weight") for n in ("query", "key", "value")])
             bqkv = torch.cat([_t(w, p + f"attention.self.{n}.bias") for n in ("query", "key", "value")])

@@ -177,7 +177,7 @@ static bool fused_qkv_attention_enabled() {
 }
 
 void Encoder::set_fp8(int mode) {
-  SR_CHECK(mode >= 0 && mode <= 2, "encoder: fp8 mode must be 0, 1 or 2");
+  SR_CHECK(mode >= 0 && mode <= 3, "encoder: fp8 mode must be 0, 1, 2 or 3");
   if (mode) {
     SR_CHECK(fold_enabled(), "encoder: fp8 modes need the LN-folded fp16-residual path");
     SR_CHECK(cfg_.intermediate % 128 == 0 && cfg_.intermediate >= 256 &&
@@ -230,7 +230,7 @@ void Encoder::prepare_fold(hipStream_t s) {
     launch_fold_ln_weight(L.wqkv32.as<float>(), P.ln2g.as<float>(), P.ln2b.as<float>(),
                           L.bqkv.as<float>(), (int)(3 * D), (int)D, L.wqkv_f.as<half_t>(),
                           L.cqkv.as<float>(), L.dqkv.as<float>(), s);
-    if (fp8_ >= 2) {
+    if (fp8_ == 2) {
       L.wqkv8.reserve((size_t)3 * D * D);
       L.wqkve.reserve((size_t)3 * D);
       L.cqkv8.reserve((size_t)3 * D * sizeof(float));
@@ -338,7 +338,10 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       float* mB = mrB_.as<float>();
       uint8_t* u8 = u8_.as<uint8_t>();
       // K5c: QKV projection + attention in one kernel (the QKV activation stays in LDS)
-      const bool fuse_qa = fused_qkv_attention_enabled() && fp8_ < 2 && qkv_attention_supported(S, d, H);
+      // fp8 modes: 2 and 3 run FFN1 (and FFN2) on e4m3 copies of the residual sums, mode 2 also the
+      // QKV projection of layers >= 1 (then unfused); mode 3 keeps QKV + attention in fp16 (K5c)
+      const bool ffn1_8 = fp8_ >= 2, qkv_8 = fp8_ == 2;
+      const bool fuse_qa = fused_qkv_attention_enabled() && !qkv_8 && qkv_attention_supported(S, d, H);
       for (size_t l = 0; l < layers_.size(); ++l) {
         const Layer& L = layers_[l];
         const bool last = cls_only && l + 1 == layers_.size();
@@ -356,7 +359,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         } else if (l == 0) {
           launch_gemm(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
                       3 * d, M, 3 * d, d, s);
-        } else if (fp8_ >= 2) {  // A = e4m3 copy of u (written by the previous FFN2)
+        } else if (qkv_8) {  // A = e4m3 copy of u (written by the previous FFN2)
           LnFold lq;
           lq.mr = mB;
           lq.colsum = L.cqkv8.as<float>();
@@ -391,8 +394,8 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         lo.stat_ld = last ? S : 1;
         lo.gamma = P ? P->ln2g.as<float>() : nullptr;
         lo.stat_out = sA;
-        lo.y8 = fp8_ >= 2 ? u8 : nullptr;  // e4m3 copy of u1 for the fp8 FFN1
-        const int eo = fp8_ >= 2 ? (l == 0 ? EPI_RES16_STATS_Y8 : EPI_LNR16_STATS_Y8)
+        lo.y8 = ffn1_8 ? u8 : nullptr;  // e4m3 copy of u1 for the fp8 FFN1
+        const int eo = ffn1_8 ? (l == 0 ? EPI_RES16_STATS_Y8 : EPI_LNR16_STATS_Y8)
                                  : (l == 0 ? EPI_RES16_STATS : EPI_LNR16_STATS);
         launch_gemm(eo, ctx, d, L.wo.as<half_t>(),
                     (l == 0 ? L.bo : L.bo_f).as<float>(), U, last ? (int64_t)S * d : d, Uo, d, Mr,
@@ -402,7 +405,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         LnFold l1;
         l1.mr = mA;
         l1.colsum = L.c1.as<float>();
-        if (fp8_ >= 2) {
+        if (ffn1_8) {
           l1.colsum = L.c1_8.as<float>();
           l1.wexp = L.w1e.as<uint8_t>();
           launch_gemm_f8w(EPI_LNF_GELU_F8, u8, d, L.w1_8.as<uint8_t>(), L.d1.as<float>(), nullptr, 0,
@@ -416,7 +419,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         l2.gamma = L.ln1g.as<float>();
         l2.stat_out = sB;
         l2.wexp = L.w2e.as<uint8_t>();
-        l2.y8 = (fp8_ >= 2 && !last) ? u8 : nullptr;  // e4m3 copy of u2 for the next QKV
+        l2.y8 = (qkv_8 && !last) ? u8 : nullptr;  // e4m3 copy of u2 for the next fp8 QKV
         if (fp8_)  // ffn holds e4m3 bytes (F per row)
           launch_gemm_f8w(l2.y8 ? EPI_LNR16_STATS_Y8 : EPI_LNR16_STATS, reinterpret_cast<const uint8_t*>(ffn), F,
                           L.w2_8.as<uint8_t>(), L.b2_f.as<float>(), Uo, d, Uo, d, Mr, d, F, s, &l2);

@@ -270,6 +270,28 @@ def test_fp8_mode2_cross_encoder(S):
     np.testing.assert_array_equal(enc.cross_score(ids, mask), got1)
 
 
+@pytest.mark.parametrize("S", [16, 128, 130])
+def test_fp8_mode3_cross_encoder(S):
+    # fp8 mode 3: FFN1 and FFN2 on the block-scaled fp8 MFMA as in mode 2, the QKV projection and
+    # attention in fp16 (the fused K5c kernel where supported, S = 128 here): against the oracle
+    # restating that quantisation (fp8=3) the band is mode 2's
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("xlmr", d=256, H=4, F=512, L=3, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=37, style="test")
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 33, S, seed=S + 5)
+    enc.set_fp8(3)
+    got3 = enc.cross_score(ids, mask)
+    ref3 = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8=3)
+    ref2 = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8=2)
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)
+    scale = 1.0 + np.abs(ref).max()
+    assert np.abs(got3 - ref3).max() <= 8e-3 * scale
+    assert np.abs(got3 - ref).max() <= 5e-2 * scale
+    assert not np.array_equal(ref3, ref2)
+    enc.set_fp8(0)
+
+
 def test_fp8_mode2_persistent_tiles():
     # 143k tokens: the persistent fp8 QKV / FFN1 / FFN2 kernels and the _Y8 epilogues
     from super_rag_amd.encoder import Encoder, random_weights
