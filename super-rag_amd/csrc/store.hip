@@ -9,12 +9,25 @@
 // A per-query candidate list holds at most select_capacity() keys; if any list overflows (an
 // adversarial row order), the whole block is re-run in "safe" mode with chunks of
 // capacity - k rows, which can never overflow.  Results are exact either way.
+#include <cstdlib>
 #include <fstream>
 
 #include "sr_kernels.h"
 #include "sr_runtime.h"
 
 namespace sr {
+
+// Threshold-chunk growth cap of the K1 schedule (chunk = rows scanned so far x growth, growth <=
+// (cap - k) / 2k so the expected keys fit the candidate lists).  SR_SCAN_GROWTH overrides the cap
+// (schedule experiments).
+static int64_t scan_growth_max() {
+  static const int64_t g = [] {
+    const char* e = std::getenv("SR_SCAN_GROWTH");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return (int64_t)(v > 0 ? v : 8);
+  }();
+  return g;
+}
 
 namespace {
 constexpr int kDenseRows = 8192;
@@ -294,7 +307,7 @@ void Store::search_block8(const half_t* qn, int B, int k, float* out_sim, int64_
                                cap, s);
     }
     launch_topk_select(cand, cnt, cap, tau, B, kk, ovf, dense == n, asim, arow, 0, s, live);
-    const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(8, (cap - kk) / (2 * kk)));
+    const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(scan_growth_max(), (cap - kk) / (2 * kk)));
     int64_t r = dense;
     while (r < n) {
       const int64_t step = safe ? (int64_t)(cap - kk) : std::max<int64_t>(r * growth, kDenseRows);
@@ -340,7 +353,7 @@ void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t
   launch_cosine_scan(true, C, ld_, live, 0, dense, qn, B, tau, cand, cnt, cap, s);
   launch_fill_int(cnt, B, (int)dense, s);
   launch_topk_select(cand, cnt, cap, tau, B, k, ovf, dense == n, out_sim, out_rows, row_offset, s, live);
-  const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(8, (cap - k) / (2 * k)));
+  const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(scan_growth_max(), (cap - k) / (2 * k)));
   int64_t r = dense;
   while (r < n) {
     const int64_t step = safe ? (int64_t)(cap - k) : std::max<int64_t>(r * growth, kDenseRows);
