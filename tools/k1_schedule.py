@@ -13,23 +13,32 @@ import os
 import sys
 
 
+def _rows(trace_dir):
+    """(name, start, end) of every dispatch: the CSV kernel trace, or the rocpd database
+    (rocprofv3's default output format on ROCm 7.2)."""
+    f = glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"), recursive=True)
+    if f:
+        return [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                for r in csv.DictReader(open(f[0]))]
+    import sqlite3
+    db = glob.glob(os.path.join(trace_dir, "**", "*.db"), recursive=True)[0]
+    return list(sqlite3.connect(db).execute("select name, start, end from kernels"))
+
+
 def calls(trace_dir):
-    f = glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
-    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    """Per search call (dispatches after a normalize_rows): the scan dispatches (the dense first
+    chunk, then the threshold chunks on the GEMM main loop) as (kind, microseconds)."""
     out, cur = [], None
-    for r in rows:
-        name = r["Kernel_Name"]
-        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    for name, t0, t1 in sorted(_rows(trace_dir), key=lambda r: r[1]):
+        us = (t1 - t0) / 1e3
         if "normalize_rows" in name:
             cur = []
             out.append(cur)
-        elif cur is not None and ("cosine_scan" in name or "topk_select" in name or "rescore" in name):
-            short = ("scan8" if "scan8" in name or "f8" in name else "scan") if "scan" in name else \
-                    ("select" if "select" in name else "rescore")
-            cur.append((short, round(us, 1)))
+        elif cur is not None and ("cosine_scan" in name or "gemm_pipe" in name):
+            cur.append(("dense" if "cosine_scan" in name else "chunk", round(us, 1)))
     return out
 
 
 if __name__ == "__main__":
-    res = {d: calls(d)[-4:] for d in sys.argv[1:]}
+    res = {d: calls(d) for d in sys.argv[1:]}
     print(json.dumps(res, indent=1))
