@@ -20,6 +20,14 @@ namespace sr {
 // Threshold-chunk growth cap of the K1 schedule (chunk = rows scanned so far x growth, growth <=
 // (cap - k) / 2k so the expected keys fit the candidate lists).  SR_SCAN_GROWTH overrides the cap
 // (schedule experiments).
+static int64_t scan_fixed_chunk() {  // SR_SCAN_CHUNK: fixed threshold-chunk rows (experiments)
+  static const int64_t c = [] {
+    const char* e = std::getenv("SR_SCAN_CHUNK");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return (int64_t)(v > 0 ? v : 0);
+  }();
+  return c;
+}
 static int64_t scan_growth_max() {
   static const int64_t g = [] {
     const char* e = std::getenv("SR_SCAN_GROWTH");
@@ -356,7 +364,8 @@ void Store::search_block(const half_t* qn, int B, int k, float* out_sim, int64_t
   const int64_t growth = std::max<int64_t>(1, std::min<int64_t>(scan_growth_max(), (cap - k) / (2 * k)));
   int64_t r = dense;
   while (r < n) {
-    const int64_t step = safe ? (int64_t)(cap - k) : std::max<int64_t>(r * growth, kDenseRows);
+    const int64_t step = safe ? (int64_t)(cap - k)
+                              : (scan_fixed_chunk() ? scan_fixed_chunk() : std::max<int64_t>(r * growth, kDenseRows));
     const int64_t next = std::min(n, r + step);
     launch_cosine_scan(false, C, ld_, live, r, next, qn, B, tau, cand, cnt, cap, s);
     launch_topk_select(cand, cnt, cap, tau, B, k, ovf, next == n, out_sim, out_rows, row_offset, s, live);
