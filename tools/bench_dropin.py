@@ -102,11 +102,23 @@ async def _closed_loop(n_callers: int, seconds: float, col_id: str, queries, lat
     return done[0]
 
 
-def measure(concurrency: int, seconds: float, col_id: str, queries) -> dict:
+_PROFILES: list = []
+
+
+def _profiled_worker_init():
+    """(--profile) one cProfile.Profile per worker thread, merged at the end."""
+    import cProfile
+    pr = cProfile.Profile()
+    _PROFILES.append(pr)
+    pr.enable()
+
+
+def measure(concurrency: int, seconds: float, col_id: str, queries, profile: bool = False) -> dict:
     loop = asyncio.new_event_loop()
     # one worker thread per concurrent request for the blocking device calls (asyncio.to_thread):
     # the default executor's min(32, cpus + 4) threads would cap the coalesced batches at 32
-    loop.set_default_executor(concurrent.futures.ThreadPoolExecutor(max_workers=concurrency + 8))
+    loop.set_default_executor(concurrent.futures.ThreadPoolExecutor(
+        max_workers=concurrency + 8, initializer=_profiled_worker_init if profile else None))
     try:
         before = {k: (c.batches, c.items) for k, c in _coalescers().items()}
         lat: list = []
@@ -151,7 +163,29 @@ def main():
     ap.add_argument("--rows", type=int, default=100000)
     ap.add_argument("--concurrency", type=int, nargs="+", default=[64, 256])
     ap.add_argument("--seconds", type=float, default=15.0)
+    ap.add_argument("--profile", action="store_true",
+                    help="cProfile the event loop and every worker thread of one C = 64 run (host "
+                         "time per request by function), printed after the JSON line")
     a = ap.parse_args()
+    if a.profile:
+        import cProfile
+        import pstats
+        build_collection("dropin", a.rows)
+        rng = np.random.default_rng(7)
+        queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
+        measure(16, 3.0, "dropin", queries)
+        main_pr = cProfile.Profile()
+        main_pr.enable()
+        r = measure(64, a.seconds, "dropin", queries, profile=True)
+        main_pr.disable()
+        print(json.dumps(r), flush=True)
+        for pr in _PROFILES:
+            pr.disable()
+        st = pstats.Stats(main_pr)
+        for pr in _PROFILES:
+            st.add(pr)
+        st.sort_stats("tottime").print_stats(45)
+        return
     print(json.dumps(run(a.rows, a.concurrency, a.seconds)), flush=True)
 
 
