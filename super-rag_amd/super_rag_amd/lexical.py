@@ -376,8 +376,9 @@ class ShardedLex:
         scores, rows = [], []
         for s, sh in enumerate(self.shards):
             a = None if allow is None else np.asarray(allow, dtype=np.uint8)[self.tables[s]]
-            sc, r = sh.search(queries, k, allow=a, mask_key=(int(mask_key) << 6) | s if a is not None else 0,
-                              global_stats=st)
+            # a shard's device mask cache is keyed per shard (0 = never cached)
+            mk = (int(mask_key) << 6) | s if (a is not None and mask_key) else 0
+            sc, r = sh.search(queries, k, allow=a, mask_key=mk, global_stats=st)
             t = self.tables[s]
             g = np.where(r >= 0, t[np.clip(r, 0, None)] if len(t) else -1, -1)
             scores.append(np.where(g >= 0, np.asarray(sc, np.float32), -np.inf))
