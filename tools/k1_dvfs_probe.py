@@ -18,11 +18,18 @@ from super_rag_amd.store import NativeStore  # noqa: E402
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--predummy-gb", type=float, default=0.0,
+                    help="allocate (and keep) this many GB before the store (other physical memory)")
+    ap.add_argument("--capacity", type=int, default=10_000_000)
+    a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rows, dim, B, k = 10_000_000, 768, 256, 100
     g = torch.Generator(device="cpu").manual_seed(0)
     centers = torch.randn((1024, dim), generator=g).to(dev)
-    st = NativeStore(dim, capacity=rows)
+    dummy = torch.empty(int(a.predummy_gb * 1e9), dtype=torch.uint8, device=dev) if a.predummy_gb else None
+    st = NativeStore(dim, capacity=max(rows, a.capacity))
     for c0 in range(0, rows, 1 << 20):
         st.add_dev(bench.gen_corpus_chunk(c0, min(rows, c0 + (1 << 20)), dim, centers, dev))
     gq = torch.Generator(device=dev).manual_seed(3)
@@ -37,7 +44,7 @@ def main():
             a @ a
         st.search_dev(q, k)
     torch.cuda.synchronize()
-    print("done", flush=True)
+    print("done", dummy is not None, flush=True)
 
 
 if __name__ == "__main__":
