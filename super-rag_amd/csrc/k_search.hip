@@ -158,6 +158,209 @@ __global__ __launch_bounds__(STHREADS, 1) void cosine_scan_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// K1s cosine_stream (threshold chunks, 65..256 queries): the query block lives in LDS for the whole
+// launch and the corpus streams from HBM straight into the MFMA A-operand registers, so the main
+// loop has no LDS-DMA staging and no barrier.
+//   * a workgroup holds 64 queries (64 x ld fp16 in LDS, 16-byte chunks XOR-swizzled by the query's
+//     low 4 bits: the B-fragment reads are conflict-free); B > 64 takes G = ceil(B / 64) workgroups
+//     on ONE XCD (a "team": blocks b, b + 8, ... share an XCD) walking the same tiles, so a corpus
+//     tile comes from HBM once and the team's other members read it from that XCD's L2
+//   * a tile = 512 rows; each of the 8 waves owns 64 of them (4 blocks of 16 rows in the A
+//     fragment layout: lane (c, g) holds row c, dims 32 j + 8 g .. + 8 of slice j) and keeps D
+//     slices (D x 4 buffer_load_dwordx4) in flight, refilled as each slice is consumed, across
+//     tile boundaries; rows past the chunk read as zero (buffer bounds) and are masked
+//   * epilogue per wave and tile: v_max3 fast rejection per query column (no memory traffic), hits
+//     append to per-query LDS lists (LDS atomics: nothing waits on the streaming loads); the lists
+//     are flushed to the candidate lists once per launch with one global atomic per query.  An LDS
+//     list that fills up spills keys to the global list directly (per-key atomics).
+// Same key set and counts as cosine_scan's threshold mode (cnt[q] = keys appended, > cap means the
+// list overflowed and the search re-runs in safe mode).
+constexpr int KS_QB = 64;     // queries per workgroup
+constexpr int KS_RB = 4;      // 16-row blocks per wave
+constexpr int KS_TROWS = 8 * KS_RB * 16;  // rows per tile (512)
+
+template <int NS>
+struct KsGeom {
+  static constexpr int LD = NS * 32;                       // halfs per row
+  static constexpr int QHALFS = KS_QB * LD;
+  static constexpr int KSLOT_FIT = (163840 - QHALFS * 2 - 2 * KS_QB * 4) / (KS_QB * 8);
+  static constexpr int KSLOT = KSLOT_FIT > 128 ? 128 : (KSLOT_FIT & ~1);
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int NS, int D>
+__global__ __launch_bounds__(512, 1) void cosine_stream_kernel(
+    const half_t* __restrict__ corpus, int64_t r0, int64_t r1, const half_t* __restrict__ Q, int B,
+    const float* __restrict__ tau, uint64_t* __restrict__ cand, int* __restrict__ cnt, int cap,
+    int G) {
+  using Geo = KsGeom<NS>;
+  constexpr int LD = Geo::LD, KSLOT = Geo::KSLOT;
+  static_assert(NS % D == 0, "the load ring must divide the slices of a row");
+  __shared__ __attribute__((aligned(16))) half_t qlds[Geo::QHALFS];
+  __shared__ __attribute__((aligned(16))) uint64_t klds[KS_QB * KSLOT];
+  __shared__ int kcnt[KS_QB], kbase[KS_QB];
+
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int T = (int)(gridDim.x >> 3) / G;  // teams per XCD
+  if (jb >= T * G) return;                  // (whole workgroup: no barrier is skipped by a part)
+  const int team = xcd * T + jb / G, qg = jb % G, NT = 8 * T;
+  const int64_t n = r1 - r0;
+  const int64_t ntiles = (n + KS_TROWS - 1) / KS_TROWS;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, g = lane >> 4;
+
+  // query block -> LDS (chunk ch of query q at ch ^ (q & 15)); rows >= B are never keys (tau inf)
+  for (int i = tid; i < KS_QB * NS * 4; i += 512) {
+    const int q = i / (NS * 4), ch = i - q * (NS * 4);
+    const half8 v = *reinterpret_cast<const half8*>(Q + (int64_t)(qg * KS_QB + q) * LD + ch * 8);
+    *reinterpret_cast<half8*>(qlds + q * LD + ((ch ^ (q & 15)) * 8)) = v;
+  }
+  if (tid < KS_QB) kcnt[tid] = 0;
+  float t[4];
+#pragma unroll
+  for (int qb = 0; qb < 4; ++qb) {
+    const int q = qg * KS_QB + 16 * qb + c;
+    t[qb] = q < B ? tau[q] : INFINITY;
+  }
+  __syncthreads();
+
+  // B fragment of (query block qb, slice j): query 16 qb + c, chunk 4 j + g, stored at
+  // (4 j + g) ^ c = 16 (j >> 2) + (4 (j & 3) ^ (g ^ c)): four lane offsets cover every slice
+  int qoff[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) qoff[m] = c * LD + ((4 * m) ^ (g ^ c)) * 8;
+  const uint32_t voff = (uint32_t)((c * LD + 8 * g) * 2);  // lane's row / dims in a 16-row block
+
+  auto tile_rsrc = [&](int64_t tl) {
+    const int64_t row0 = tl * KS_TROWS + wave * 64;  // chunk-relative
+    const int64_t left = n - row0;
+    const int64_t bytes = left <= 0 ? 0 : (left >= 64 ? 64 : left) * (int64_t)LD * 2;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(corpus + (r0 + row0) * LD), (short)0,
+                                             (int)bytes, 0x00020000);
+  };
+  auto load = [&](__amdgpu_buffer_rsrc_t rs, int rb, int j) {
+    return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rs, voff + 64 * j, rb * 16 * LD * 2, 0));
+  };
+
+  int64_t tile = team;
+  half8 buf[D][KS_RB];
+  auto bfrag = [&](int j, int qb) {
+    return *reinterpret_cast<const half8*>(qlds + qb * 16 * LD + (j >> 2) * 128 + qoff[j & 3]);
+  };
+  half8 bc[4];  // B fragments of the slice being multiplied (slice 0 of every tile: the same)
+  if (tile < ntiles) {
+    const auto rs = tile_rsrc(tile);
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int rb = 0; rb < KS_RB; ++rb) buf[d][rb] = load(rs, rb, d);
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) bc[qb] = bfrag(0, qb);
+  }
+  while (tile < ntiles) {
+    const int64_t next = tile + NT;
+    // (past the last tile: a zero-byte resource, so the ring's refills read nothing)
+    const auto rs = tile_rsrc(tile), rn = tile_rsrc(next);
+    float4v acc[KS_RB][4];
+#pragma unroll
+    for (int rb = 0; rb < KS_RB; ++rb)
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) acc[rb][qb] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int s = j % D;
+      // next slice's B fragments (LDS), then this slice's 16 MFMAs with the refill of its ring slot
+      // (slice j + D of this tile or the next) spread among them
+      half8 bn[4];
+      const int jn = j + 1 < NS ? j + 1 : 0;
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) bn[qb] = bfrag(jn, qb);
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+        for (int rb = 0; rb < KS_RB; ++rb)
+          acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(buf[s][rb], bc[qb], acc[rb][qb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < KS_RB; ++rb)
+        buf[s][rb] = j + D < NS ? load(rs, rb, j + D) : load(rn, rb, j + D - NS);
+      // schedule: 4 x {MFMA, DS read}, 4 x {2 MFMA, VMEM read}, 4 MFMA
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) bc[qb] = bn[qb];
+    }
+    // epilogue: acc[rb][qb][r] = sim(row tile*512 + 64 wave + 16 rb + 4 g + r, query 16 qb + c)
+    const int64_t rw = tile * KS_TROWS + wave * 64;  // chunk-relative first row of the wave
+    const int valid = (int)(n - rw < 64 ? n - rw : 64);  // rows of the wave in the chunk (may be <= 0)
+    bool hit = false;
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int rb = 0; rb < KS_RB; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          mx = fmaxf(mx, (16 * rb + 4 * g + r < valid) ? acc[rb][qb][r] : -INFINITY);
+      hit |= mx >= t[qb];
+    }
+    if (__builtin_amdgcn_ballot_w64(hit) != 0) {
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+        for (int rb = 0; rb < KS_RB; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rr = 16 * rb + 4 * g + r;
+            const float sim = acc[rb][qb][r];
+            if (rr < valid && sim >= t[qb]) {
+              const int ql = 16 * qb + c;
+              const uint64_t key = make_key(sim, (uint32_t)(r0 + rw + rr));
+              const int rank = atomicAdd(&kcnt[ql], 1);  // LDS atomic
+              if (rank < KSLOT) {
+                klds[ql * KSLOT + rank] = key;
+              } else {  // the query's LDS list is full: straight to the global list
+                const int q = qg * KS_QB + ql;
+                const int pos = atomicAdd(&cnt[q], 1);
+                if (pos < cap) cand[(int64_t)q * cap + pos] = key;
+              }
+            }
+          }
+    }
+    tile = next;
+  }
+  // flush the LDS lists: one reservation per query, then the keys
+  __syncthreads();
+  if (tid < KS_QB) {
+    const int q = qg * KS_QB + tid;
+    const int m = min(kcnt[tid], KSLOT);
+    kcnt[tid] = m;
+    kbase[tid] = (m > 0 && q < B) ? atomicAdd(&cnt[q], m) : 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < KS_QB * KSLOT; i += 512) {
+    const int ql = i / KSLOT, e = i - ql * KSLOT;
+    if (e < kcnt[ql]) {
+      const int pos = kbase[ql] + e;
+      if (pos < cap) cand[(int64_t)(qg * KS_QB + ql) * cap + pos] = klds[i];
+    }
+  }
+}
+
 struct SelectSmem {
   uint64_t keys[SEL_CAP];
   SelShared sh;
@@ -339,6 +542,48 @@ int scan_query_tiles(int B) {
 
 static bool g_scan_legacy = std::getenv("SR_SCAN_LEGACY") != nullptr;
 
+// SR_SCAN_STREAM (read per launch: parity tests switch it): 0 (default) = threshold chunks of 65..256
+// queries on the GEMM main loop (launch_cosine_scan_gemm), 1 = on cosine_stream, 2 = cosine_stream for
+// every threshold chunk (also B <= 64).  Measured (10M x 768, B = 256, k = 100): cosine_stream
+// 8.4 ms vs 4.4 ms for the GEMM scan: the team members do not stay close enough for the XCD's L2 to
+// serve 3 of the 4 reads of a tile (8 teams x 786 KB in flight per XCD > 4 MB), so the corpus
+// streams ~4x from the Infinity Cache / HBM.
+static int scan_stream_mode() {
+  const char* e = std::getenv("SR_SCAN_STREAM");
+  return e ? (int)std::strtol(e, nullptr, 10) : 0;
+}
+
+template <int NS, int D>
+static void stream_ns(dim3 grid, hipStream_t s, const half_t* corpus, int64_t r0, int64_t r1,
+                      const half_t* Q, int B, const float* tau, uint64_t* cand, int* cnt, int cap,
+                      int G) {
+  hipLaunchKernelGGL((cosine_stream_kernel<NS, D>), grid, dim3(512), 0, s, corpus, r0, r1, Q, B, tau,
+                     cand, cnt, cap, G);
+}
+
+// K1s for a threshold chunk; false when the row width has no instantiation (then the caller's
+// other kernels run).  Q holds >= 64 * ceil(B / 64) rows of ldc halfs (the store's query buffer is
+// 256 rows per block).
+static bool launch_cosine_stream(const half_t* corpus, int64_t ldc, int64_t r0, int64_t r1,
+                                 const half_t* Q, int B, const float* tau, uint64_t* cand, int* cnt,
+                                 int cap, hipStream_t s) {
+  if (ldc != 384 && ldc != 512 && ldc != 768 && ldc != 1024) return false;
+  const int64_t n = r1 - r0;
+  const int G = (B + KS_QB - 1) / KS_QB;
+  const int64_t ntiles = ceil_div(n, KS_TROWS);
+  const int per_xcd = (int)std::min<int64_t>(32, G * ceil_div(ntiles, 8));
+  const dim3 grid((unsigned)(8 * per_xcd));
+  ProfScope prof("cosine_scan", s, 2.0 * (double)n * ldc * B, (double)n * ldc * 2.0 + (double)B * ldc * 2.0);
+  switch (ldc) {
+    case 384: stream_ns<12, 4>(grid, s, corpus, r0, r1, Q, B, tau, cand, cnt, cap, G); break;
+    case 512: stream_ns<16, 4>(grid, s, corpus, r0, r1, Q, B, tau, cand, cnt, cap, G); break;
+    case 768: stream_ns<24, 4>(grid, s, corpus, r0, r1, Q, B, tau, cand, cnt, cap, G); break;
+    default: stream_ns<32, 4>(grid, s, corpus, r0, r1, Q, B, tau, cand, cnt, cap, G); break;
+  }
+  SR_LAUNCH_CHECK();
+  return true;
+}
+
 void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uint8_t* live,
                         int64_t r0, int64_t r1, const half_t* Q, int B, const float* tau,
                         uint64_t* cand, int* cnt, int cap, hipStream_t s) {
@@ -346,6 +591,11 @@ void launch_cosine_scan(bool dense, const half_t* corpus, int64_t ldc, const uin
   SR_CHECK(ldc % SBK == 0, "cosine_scan: padded dim must be a multiple of 64");
   if (r1 <= r0) return;
   SR_CHECK(!dense || r1 - r0 <= cap, "cosine_scan: dense chunk larger than the candidate list");
+  if (!dense && !g_scan_legacy) {
+    const int mode = scan_stream_mode();
+    if ((mode == 1 && B > 64) || mode == 2)
+      if (launch_cosine_stream(corpus, ldc, r0, r1, Q, B, tau, cand, cnt, cap, s)) return;
+  }
   const int qt = scan_query_tiles(B);
   if (!dense && qt == 16 && ldc >= 2 * SBK && r1 - r0 >= 8 * SROWS && !g_scan_legacy) {
     // large query blocks: the pipelined 256 x 256 GEMM main loop with the threshold epilogue

@@ -317,3 +317,31 @@ def test_gemm_scan_key_buffer_overflow_near_identical_queries(scan):
         assert recall_at_k(r[pick], r_ref) >= 0.9
         sims = stored[r[pick]] @ qq[:, :, None]
         np.testing.assert_allclose(d[pick], 1.0 - sims[..., 0], atol=EPS)
+
+
+@pytest.mark.parametrize("dim,B,n,k", [(768, 256, 200_000, 100), (768, 65, 70_001, 10),
+                                       (384, 200, 150_000, 20), (1024, 130, 100_003, 50),
+                                       (512, 192, 90_000, 1), (768, 32, 120_000, 10)])
+def test_stream_scan_equals_gemm_scan(dim, B, n, k, monkeypatch):
+    # K1s (cosine_stream: queries resident in LDS, corpus streamed into registers) against the
+    # GEMM-main-loop scan on the same store: the same MFMA over the same 32-dim slices in the same
+    # order, so sims, rows and order must be identical; ragged row counts (partial 512-row tiles),
+    # tombstones, 1..4 query groups per team (B = 32 runs with SR_SCAN_STREAM=2); the oracle
+    # checks the first case.
+    x = _clustered(n, dim, seed=dim + B, centers=512)
+    s = _store(dim)
+    s.add(x)
+    dead = np.arange(3, n, 11)
+    s.remove(dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    q = _queries(x, B, seed=B + 7)
+    monkeypatch.setenv("SR_SCAN_STREAM", "0")
+    d0, r0 = s.search(q, k)
+    monkeypatch.setenv("SR_SCAN_STREAM", "2")
+    d1, r1 = s.search(q, k)
+    np.testing.assert_array_equal(r1, r0)
+    np.testing.assert_array_equal(d1, d0)
+    assert not np.isin(r1, dead).any()
+    if dim == 768 and B == 256:
+        _check(s, q, k, live=live)

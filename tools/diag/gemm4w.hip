@@ -226,6 +226,116 @@ __global__ __launch_bounds__(256, 1) void v4(const half_t* __restrict__ W, const
   out[(size_t)blockIdx.x * 512 + 256 + tid] = 0.f;
 }
 
+// ---- V3: 8 waves, wave tile 256 (W rows) x 32 (X rows), X straight into registers ----------------
+// Only W is staged by LDS-DMA (32 pieces per K-step, 4 per wave, 3-stage ring of 32 KiB); every
+// wave's 32 X rows are exclusive to it, so their B fragments are loaded with buffer_load_dwordx4
+// into a 3-K-step register ring (4 loads per wave and K-step).  A K-step = 8 phases of 4 W blocks
+// x 2 X blocks (8 MFMAs); phase q + 1's A fragments are read during phase q; the barrier sits
+// before phase 7, after which the next K-step's phase-0 fragments are read and the DMA of K-step
+// kt + 2 is issued.
+template <int XD>
+__global__ __launch_bounds__(512) void v3(const half_t* __restrict__ W, const half_t* __restrict__ X,
+                                          float* __restrict__ out, int M, int N, int K) {
+  constexpr int WST = 256 * BK;
+  __shared__ __attribute__((aligned(16))) half_t lds[3 * WST];
+  int n0, m0;
+  tile_of(blockIdx.x, gridDim.x, N / 256, n0, m0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nk = K / BK;
+  const int c = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * K), (short)0, 256 * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)(m0 + 32 * wave) * K), (short)0, 32 * K * 2, 0x00020000);
+  int voff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par)
+    voff[par] = ((lane >> 3) * K + ((lane & 7) ^ ((4 * par + (lane >> 4)) & 7)) * 8) * 2;
+  const int xoff = (c * K + 8 * g) * 2;
+  auto dma = [&](int kt) __attribute__((always_inline)) {
+    half_t* dst = lds + (kt % 3) * WST;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = wave * 4 + i;  // rows 8p .. 8p + 7; swizzle parity p & 1 = i & 1
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, LDSP(dst + p * 8 * BK), 16, voff[i & 1], (8 * p * K + kt * BK) * 2, 0, 0);
+    }
+  };
+  h8 xb[XD][2][2];  // [ring slot][X block][k half]
+  auto xload = [&](int slot, int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        xb[slot][mb][h] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rx, xoff, (mb * 16 * K + kt * BK + 32 * h) * 2, 0));
+  };
+  f4 acc[16][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // phase q: W blocks 4 (q & 3) .. + 3, k half q >> 2
+  auto afrag = [&](const half_t* st, int q, int i) __attribute__((always_inline)) {
+    return frag(st, 16 * (4 * (q & 3) + i) + c, 4 * (q >> 2) + g);
+  };
+  dma(0);
+  if (nk > 1) dma(1);
+#pragma unroll
+  for (int d = 0; d < XD; ++d) xload(d, d);
+  WAITCNT(0, 0);
+  __builtin_amdgcn_s_barrier();
+  h8 A[2][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) A[0][i] = afrag(lds, 0, i);
+  for (int kt0 = 0; kt0 < nk; kt0 += 6) {
+#pragma unroll
+    for (int u6 = 0; u6 < 6; ++u6) {
+      const int kt = kt0 + u6;  // (nk % 6 == 0: K = 768 / 3072)
+      const int u = u6 % 3, xs = u6 % XD;
+      const half_t* cur = lds + u * WST;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        if (q < 6) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) A[(q + 1) & 1][i] = afrag(cur, q + 1, i);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) A[1][i] = afrag(cur, 7, i);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * (q & 3) + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[q & 1][i], xb[xs][j][q >> 2], acc[4 * (q & 3) + i][j], 0, 0, 0);
+      }
+      // K-step kt + 1's W stage has landed (younger: X(kt - 1 + XD) only) -> barrier
+      if (kt - 1 + XD < nk)
+        WAITCNT(4, 0);
+      else
+        WAITCNT(0, 0);
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) dma(kt + 2);
+      const half_t* nxt = lds + ((u + 1) % 3) * WST;
+      if (kt + 1 < nk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A[0][i] = afrag(nxt, 0, i);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[12 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[1][i], xb[xs][j][1], acc[12 + i][j], 0, 0, 0);
+      if (kt + XD < nk) xload(xs, kt + XD);
+    }
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum += acc[i][j][r];
+  out[(size_t)blockIdx.x * 512 + tid] = sum;
+}
+
 template <class Kern>
 static double run(Kern k, int threads, const half_t* W, const half_t* X, float* out, int M, int N, int K,
                   int reps) {
@@ -286,8 +396,13 @@ int main(int argc, char** argv) {
     const double s1 = total(out, M, N);
     const double t2 = run(v4<2>, 256, W, X, out, M, N, K, reps);
     const double s2 = total(out, M, N);
-    printf("M=%d N=%d K=%d  V0 8w: %7.1f  V1 4w dma: %7.1f  V2 4w reg: %7.1f TF/s  totals %s %s\n", M, N,
-           K, t0, t1, t2, s0 == s1 ? "eq" : "DIFF", s0 == s2 ? "eq" : "DIFF");
+    const double t3 = run(v3<3>, 512, W, X, out, M, N, K, reps);
+    const double s3 = total(out, M, N);
+    const double t4 = run(v3<2>, 512, W, X, out, M, N, K, reps);
+    const double s4 = total(out, M, N);
+    printf("M=%d N=%d K=%d  V0 8w: %7.1f  V1 4w dma: %7.1f  V2 4w reg: %7.1f  V3 8w Xreg3: %7.1f  Xreg2: %7.1f TF/s  totals %s %s %s %s\n", M, N,
+           K, t0, t1, t2, t3, t4, s0 == s1 ? "eq" : "DIFF", s0 == s2 ? "eq" : "DIFF", s0 == s3 ? "eq" : "DIFF",
+           s0 == s4 ? "eq" : "DIFF");
     fflush(stdout);
   }
   return 0;

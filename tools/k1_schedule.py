@@ -34,7 +34,7 @@ def calls(trace_dir):
         if "normalize_rows" in name:
             cur = []
             out.append(cur)
-        elif cur is not None and ("cosine_scan" in name or "gemm_pipe" in name):
+        elif cur is not None and ("cosine_scan" in name or "gemm_pipe" in name or "cosine_stream" in name):
             cur.append(("dense" if "cosine_scan" in name else "chunk", round(us, 1)))
     return out
 
