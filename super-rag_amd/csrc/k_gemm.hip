@@ -30,6 +30,14 @@
 #ifndef SR_GEMM_LINE_GELU
 #define SR_GEMM_LINE_GELU 0  // whole-line stores for the GELU epilogues too (A/B builds)
 #endif
+#ifndef SR_GEMM_GELU_LUT
+#define SR_GEMM_GELU_LUT 1  // FFN1 epilogues: erf from an LDS table (0: A&S 7.1.26, A/B builds)
+#endif
+#ifndef SR_GEMM_LATE_STAGE
+#define SR_GEMM_LATE_STAGE 0  // 1: persistent wide epilogues stage the next tile after the epilogue's
+                              // constant loads (A/B build; measured -0.3 % end to end,
+                              // profiles/r03_gemm_epilogue_ab/)
+#endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
@@ -147,6 +155,32 @@ __device__ __forceinline__ f2v gelu2_erf2(f2v x) {
   return pk_fma(ax, pk_fma(-p, w, splat2(1.0f)), x);
 }
 
+// 2 * GELU(x) = x + |x| erf(|x| / sqrt 2) with erf from a 1024-entry LDS table over [0, 4) (step
+// 1/256, entries (erf(z_i), erf(z_i+1) - erf(z_i)), linear interpolation; z >= 4 takes the last
+// entry: erf(4) = 1 - 1.5e-8): one LDS read and 5 VALU per element instead of a v_rcp, a v_exp and
+// 9 VALU.  |error| <= 2.5e-6 (rms 1.0e-6 on N(0, 2) inputs) against fp16 output rounding of rms
+// 5.8e-4 (A&S 7.1.26: 4.2e-7).  Used by the FFN1 epilogues of the pipelined kernels
+// (EPI_LNF_GELU_F16 / _F8), whose GELU math was ~36 % of the kernel (profiles/r02_pmc_gemm_study).
+constexpr int GELU_TAB = 1024;
+__device__ __forceinline__ float gelu2_lut(float x, const float2* __restrict__ tab) {
+  const float ax = fabsf(x);
+  const float az = ax * (256.0f * 0.70710678118654752f);
+  const uint32_t i = min((uint32_t)az, (uint32_t)(GELU_TAB - 1));
+  const float2 t = tab[i];
+  return fmaf(ax, fmaf(__builtin_amdgcn_fractf(az), t.y, t.x), x);
+}
+__device__ __forceinline__ f2v gelu2_lut2(f2v x, const float2* __restrict__ tab) {
+  return f2v{gelu2_lut(x.x, tab), gelu2_lut(x.y, tab)};
+}
+// the table, written by a workgroup's threads before its first barrier
+__device__ __forceinline__ void gelu_tab_init(float2* __restrict__ tab, int tid, int nthreads) {
+  for (int i = tid; i < GELU_TAB; i += nthreads) {
+    const float z0 = (float)i * (1.0f / 256.0f);
+    const float e0 = erff(z0), e1 = erff(z0 + (1.0f / 256.0f));
+    tab[i] = make_float2(e0, e1 - e0);
+  }
+}
+
 __device__ __forceinline__ f2v gelu_erf2(f2v x) {
   const f2v z = __builtin_elementwise_abs(x) * splat2(0.70710678118654752f);
   const f2v d = pk_fma(splat2(0.3275911f), z, splat2(1.0f));
@@ -161,6 +195,10 @@ __device__ __forceinline__ f2v gelu_erf2(f2v x) {
   const f2v s = {copysignf(e.x, x.x), copysignf(e.y, x.y)};
   return splat2(0.5f) * x * (splat2(1.0f) + s);
 }
+
+struct NoPre {
+  __device__ __forceinline__ void operator()() const {}
+};
 
 // Epilogue: lane owns D[n = nw0 + 16i + 4(lane>>4) + r][m = mw0 + 16j + (lane&15)] of the wave's
 // FN x FM 16x16 tiles; bias (+ residual) (+ activation), one 8/16-byte store per tile.
@@ -275,12 +313,18 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
 // from mr (launch_ln_stats_finalize of the producer's partials).  The *_STATS epilogues write the
 // Chan partials of their own fp16-rounded outputs: per 128-column wave span the sum over the 4
 // lane groups (xor-shuffles 16 / 32), then M2 around that span's mean.
-template <int EPI, bool CHECK, bool LINE_ST = false>
+// pre(): called once the epilogue's constant loads (bias, column sums / LayerNorm weight, row
+// statistics) are issued: the persistent kernel stages the next tile's first K-steps there, so
+// those loads are older than the staging pieces and their wait (vmcnt counts in order) does not
+// also wait for the staging.
+template <int EPI, bool CHECK, bool LINE_ST = false, bool GLUT = false, class Pre = NoPre>
 __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, int mw0, int lane,
                                                 int M, int N, const float* __restrict__ bias,
                                                 const void* __restrict__ R, int64_t ldr,
                                                 void* __restrict__ Y, int64_t ldy,
-                                                const LnFold& lf, half_t* __restrict__ scr = nullptr) {
+                                                const LnFold& lf, half_t* __restrict__ scr = nullptr,
+                                                const float2* __restrict__ gtab = nullptr,
+                                                const Pre& pre = Pre{}) {
   constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;  // e4m3 bytes instead of fp16
   constexpr bool Y8 = EPI == EPI_RES16_STATS_Y8 || EPI == EPI_LNR16_STATS_Y8;  // + e4m3 copy
   constexpr bool LNF = EPI == EPI_LNF_F16 || EPI == EPI_LNF_GELU_F16 || OUT8;
@@ -325,6 +369,11 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       m = (CHECK && m >= M) ? M - 1 : m;
       mrj[j] = *reinterpret_cast<const float2*>(lf.mr + (int64_t)m * lf.stat_ld * 2);
     }
+  }
+  if constexpr (!std::is_same<Pre, NoPre>::value) {
+    __builtin_amdgcn_sched_barrier(0);
+    pre();
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -396,7 +445,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       }
       if constexpr (GELU2) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = gelu2_erf2(x[q]);
+        for (int q = 0; q < 4; ++q) {
+          if constexpr (GLUT)
+            x[q] = gelu2_lut2(x[q], gtab);
+          else
+            x[q] = gelu2_erf2(x[q]);
+        }
       }
       if constexpr (OUT8) {
         uint2 q8;
@@ -467,7 +521,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       }
       if constexpr (GELU2) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = gelu2_erf(v[r]);
+        for (int r = 0; r < 8; ++r) {
+          if constexpr (GLUT)
+            v[r] = gelu2_lut(v[r], gtab);
+          else
+            v[r] = gelu2_erf(v[r]);
+        }
       }
       if constexpr (OUT8) {
         uint2 q8;
@@ -545,16 +604,21 @@ template <int EPI>
 struct PipeEpi {
   static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
   static constexpr int NSTORE = WIDE ? 16 : 32;
-  template <bool CHECK, bool LINE = false>
+  template <bool CHECK, bool LINE = false, bool GLUT = false, class Pre = NoPre>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
                                              int N, const float* __restrict__ bias,
                                              const void* __restrict__ R, int64_t ldr,
                                              void* __restrict__ Y, int64_t ldy, const LnFold& lf,
-                                             half_t* __restrict__ scr = nullptr) {
+                                             half_t* __restrict__ scr = nullptr,
+                                             const float2* __restrict__ gtab = nullptr,
+                                             const Pre& pre = Pre{}) {
     if constexpr (WIDE)
-      store_tile_wide<EPI, CHECK, LINE>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr);
+      store_tile_wide<EPI, CHECK, LINE, GLUT, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
     else
+    {
+      pre();
       store_tile_fast<EPI, CHECK, 8, 4>(acc, nw0, mw0, lane, M, bias, R, ldr, Y, ldy);
+    }
   }
 };
 
@@ -726,10 +790,19 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr int EPI_OUT = EPI;
   // whole-line epilogue stores: a 4 KiB LDS scratch per wave after the two 64 KiB stages (one
   // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
+  // (the e4m3-output epilogues never take the line path: no scratch for them)
   constexpr bool LINE = SR_GEMM_LINE_STORE && PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 &&
+                        EPI != EPI_LNF_GELU_F8 && EPI != EPI_RES16_STATS_Y8 && EPI != EPI_LNR16_STATS_Y8 &&
                         (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (SCAN ? 512 : 0)];
+  // GLUT: the FFN1 epilogues' 8 KiB erf table (gelu2_lut) past the stages / line scratch
+  constexpr bool GLUT = SR_GEMM_GELU_LUT && DIAG == 0 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (SCAN ? 512 : 0) +
+                                                     (GLUT ? 4 * GELU_TAB : 0)];
+  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0));
+  // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
+  // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
+  constexpr bool LATE = SR_GEMM_LATE_STAGE && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -836,6 +909,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
                          // barrier publishes it
     for (int q = tid; q < 256; q += blockDim.x) tau_lds[q] = q < M ? bias[q] : INFINITY;
   }
+  if constexpr (GLUT) gelu_tab_init(gtab, tid, blockDim.x);  // published by the prologue's barrier
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
     stage(0, lds, m0, n0);
@@ -898,7 +972,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     // (group (kt & 1) stages K-step kt + 2 in one burst while the partner wave of every SIMD,
     // from the other group, runs its MFMAs)
     if (SN == 1 && DIAG != 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
-    if (SN == 2) {
+    if (SN == 2 && !LATE) {
       if (more_) {
         if (grp == 0)
           stage(0, lds, mn, nn);
@@ -949,7 +1023,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (SN == 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
-    if (SN == 2) {
+    if (SN == 2 && !LATE) {
       if (more_) {
         if (grp == 0)
           stage(0, lds, mn, nn);
@@ -1084,12 +1158,27 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       scan_tau(tq, m0 + wm * 64, lane, tau_lds);
       scan_epilogue(acc, tq, n0 + wn * 128, m0 + wm * 64, lane, N, reinterpret_cast<uint64_t*>(Y),
                     (int)ldy, lf);
+    } else if constexpr (LATE) {
+      auto pre = [&]() __attribute__((always_inline)) {
+        if (more) {
+          if (grp == 0)
+            stage(0, lds, m0n, n0n);
+          else
+            stage(1, lds + STAGE, m0n, n0n);
+        }
+      };
+      if (full)
+        PipeEpi<EPI_OUT>::template run<false, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                          R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab, pre);
+      else
+        PipeEpi<EPI_OUT>::template run<true, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                         R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab, pre);
     } else if (full) {
-      PipeEpi<EPI_OUT>::template run<false, LINE>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                  R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048);
+      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                        R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab);
     } else {
-      PipeEpi<EPI_OUT>::template run<true, LINE>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                 R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048);
+      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                       R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab);
     }
     if (!more) break;
     // next tile: K-step 0 (group 0's 16 glds) landed; younger: the epilogue's NSTORE stores
