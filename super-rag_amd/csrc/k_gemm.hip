@@ -341,7 +341,8 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   // 71 vs 19 B/clk of store throughput per CU (tools/diag/store_rate.hip)
   // (not for the GELU epilogues: there the exchange measured slower, FFN1 932 -> 881 TF/s, while
   // QKV gained 1005 -> 1044 and the residual + statistics GEMMs 1072 -> 1078, ab_line3)
-  constexpr bool LINE = LINE_ST && !OUT8 && !Y8 && (SR_GEMM_LINE_GELU || (!GELU && !GELU2));
+  // (Y8: the e4m3 copy leaves from the line read-back too, as whole 128-B row segments)
+  constexpr bool LINE = LINE_ST && !OUT8 && (SR_GEMM_LINE_GELU || (!GELU && !GELU2));
   static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
@@ -470,7 +471,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         }
         else
           *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
-        if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+        if constexpr (Y8 && !LINE) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
           {
             uint2 q8;
             q8.x = e4m3x4((float)hv[p][0], (float)hv[p][1], (float)hv[p][2], (float)hv[p][3]);
@@ -543,7 +544,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         }
         else
           *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
-        if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+        if constexpr (Y8 && !LINE) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
           {
             uint2 q8;
             q8.x = e4m3x4((float)hv[p][0], (float)hv[p][1], (float)hv[p][2], (float)hv[p][3]);
@@ -563,8 +564,15 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       for (int q = 0; q < 4; ++q) {
         const int ln = lane_id_here(), c = ln & 15, rr = 4 * q + (ln >> 4);
         const half8 o = *reinterpret_cast<const half8*>(scr + rr * 128 + ((c ^ rr) << 3));
-        if (!CHECK || mw0 + j * 16 + rr < M)
+        if (!CHECK || mw0 + j * 16 + rr < M) {
           *reinterpret_cast<half8*>(yw + (int64_t)rr * ldy + c * 8) = o;
+          if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+            uint2 q8;
+            q8.x = e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
+            q8.y = e4m3x4((float)o[4], (float)o[5], (float)o[6], (float)o[7]);
+            *reinterpret_cast<uint2*>(lf.y8 + (int64_t)(mw0 + j * 16 + rr) * ldy + nw0 + c * 8) = q8;
+          }
+        }
       }
     }
     if constexpr (STATS) {
@@ -792,7 +800,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
   // (the e4m3-output epilogues never take the line path: no scratch for them)
   constexpr bool LINE = SR_GEMM_LINE_STORE && PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 &&
-                        EPI != EPI_LNF_GELU_F8 && EPI != EPI_RES16_STATS_Y8 && EPI != EPI_LNR16_STATS_Y8 &&
+                        EPI != EPI_LNF_GELU_F8 &&
                         (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
   // GLUT: the FFN1 epilogues' 8 KiB erf table (gelu2_lut) past the stages / line scratch
