@@ -176,6 +176,13 @@ static bool fused_qkv_attention_enabled() {
   return !(e && e[0] == '0');
 }
 
+// K/V-free CLS-only last layer of the folded cross-encoders (cls_attn_fold, k_encoder_misc.hip):
+// no K / V projection of the S tokens; SR_KVFREE_CLS=0 keeps the K, V GEMM + CLS attention (A/B).
+static bool kvfree_cls_enabled() {
+  const char* e = std::getenv("SR_KVFREE_CLS");
+  return !(e && e[0] == '0');
+}
+
 void Encoder::set_fp8(int mode) {
   SR_CHECK(mode >= 0 && mode <= 3, "encoder: fp8 mode must be 0, 1, 2 or 3");
   if (mode) {
@@ -222,6 +229,8 @@ void Encoder::prepare_fold(hipStream_t s) {
     launch_vec_add(L.b2.as<float>(), L.ln1b.as<float>(), L.b2_f.as<float>(), (int)D, s);
     if (l == 0) continue;  // layer 0 reads the (normalised) embedding LayerNorm output
     const Layer& P = layers_[l - 1];
+    const bool kvfree_prep = l + 1 == layers_.size() && kvfree_cls_enabled() &&
+                             cls_attn_fold_supported(128, (int)D, cfg_.heads);
     L.bo_f.reserve((size_t)D * sizeof(float));  // O-proj bias + beta of the previous LN2
     launch_vec_add(L.bo.as<float>(), P.ln2b.as<float>(), L.bo_f.as<float>(), (int)D, s);
     L.wqkv_f.reserve((size_t)3 * D * D * sizeof(half_t));
@@ -230,6 +239,15 @@ void Encoder::prepare_fold(hipStream_t s) {
     launch_fold_ln_weight(L.wqkv32.as<float>(), P.ln2g.as<float>(), P.ln2b.as<float>(),
                           L.bqkv.as<float>(), (int)(3 * D), (int)D, L.wqkv_f.as<half_t>(),
                           L.cqkv.as<float>(), L.dqkv.as<float>(), s);
+    if (kvfree_prep) {
+      const int64_t HD = (int64_t)cfg_.heads * D;
+      L.wk_bd.reserve((size_t)HD * D * sizeof(half_t));
+      L.wv_bd.reserve((size_t)D * 2 * HD * sizeof(half_t));
+      L.zb.reserve((size_t)HD * sizeof(float));
+      SR_HIP(hipMemsetAsync(L.zb.p, 0, (size_t)HD * sizeof(float), s));
+      launch_kv_blockdiag(L.wqkv_f.as<half_t>(), (int)D, cfg_.heads, L.wk_bd.as<half_t>(),
+                          L.wv_bd.as<half_t>(), s);
+    }
     if (fp8_ == 2) {
       L.wqkv8.reserve((size_t)3 * D * D);
       L.wqkve.reserve((size_t)3 * D);
@@ -342,6 +360,9 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       // QKV projection of layers >= 1 (then unfused); mode 3 keeps QKV + attention in fp16 (K5c)
       const bool ffn1_8 = fp8_ >= 2, qkv_8 = fp8_ == 2;
       const bool fuse_qa = fused_qkv_attention_enabled() && !qkv_8 && qkv_attention_supported(S, d, H);
+      // (qkv_8: mode 2 keeps the e4m3 QKV path in every layer)
+      const bool kvfree = cls_only && !qkv_8 && kvfree_cls_enabled() && layers_.size() > 1 &&
+                          cls_attn_fold_supported(S, d, H) && layers_.back().wk_bd.p != nullptr;
       for (size_t l = 0; l < layers_.size(); ++l) {
         const Layer& L = layers_[l];
         const bool last = cls_only && l + 1 == layers_.size();
@@ -366,6 +387,25 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
           lq.wexp = L.wqkve.as<uint8_t>();
           launch_gemm_f8w(EPI_LNF_F16, u8, d, L.wqkv8.as<uint8_t>(), L.dqkv.as<float>(), nullptr, 0,
                           qkv, 3 * d, M, 3 * d, d, s, &lq);
+        } else if (last && kvfree) {
+          // K/V-free CLS-only last layer: q of the CLS rows, w_h = W'_{k,h}^T q_h (one GEMM on the
+          // block-diagonal weight), scores / softmax / z' per sequence (as an fp16 hi + lo pair),
+          // ctx = W'_v z' + d_v (one GEMM, K = 2 H d)
+          LnFold lc;  // A = row b*S of each sequence (stride S*d), its statistics at row b*S
+          lc.mr = mB;
+          lc.stat_ld = S;
+          lc.colsum = L.cqkv.as<float>();
+          const int64_t HD = (int64_t)H * d;
+          half_t* qc = ffn;
+          half_t* wq = ffn + (int64_t)nb * d;
+          half_t* zq = wq + (int64_t)nb * HD;
+          launch_gemm(EPI_LNF_F16, U, (int64_t)S * d, L.wqkv_f.as<half_t>(), L.dqkv.as<float>(), nullptr,
+                      0, qc, d, nb, d, d, s, &lc);
+          launch_gemm(EPI_BIAS_F16, qc, d, L.wk_bd.as<half_t>(), L.zb.as<float>(), nullptr, 0, wq, HD, nb,
+                      (int)HD, d, s);
+          launch_cls_attn_fold(wq, U, mB, cmask, nb, S, d, H, zq, s);
+          launch_gemm(EPI_BIAS_F16, zq, 2 * HD, L.wv_bd.as<half_t>(), L.dqkv.as<float>() + 2 * d, nullptr,
+                      0, ctx, d, nb, d, (int)(2 * HD), s);
         } else if (last && d % 256 == 0) {  // CLS-only last layer: K, V for all rows, Q for CLS rows
           LnFold lq;
           lq.mr = mB;
@@ -386,7 +426,8 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
                       3 * d, M, 3 * d, d, s, &lq);
         }
         const int Mr = last ? nb : M;
-        if (!(fuse_qa && !last)) launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
+        if (!(fuse_qa && !last) && !(last && kvfree))
+          launch_attention(qkv, cmask, ctx, nb, S, last ? 1 : S, d, H, s);
         // O-projection + residual LN2(l-1)(u) -> u1 (in place, or compact rows) + partials sA
         half_t* Uo = last ? Uc : U;
         LnFold lo;

@@ -475,6 +475,187 @@ void launch_copy16(const void* src, void* dst, int64_t bytes, hipStream_t s) {
   SR_LAUNCH_CHECK();
 }
 
+// ---- K/V-free CLS-only last layer of an LN-folded cross-encoder (encoder.cpp) ---------------------
+// With LN folded, K_j = rstd_j (W'_k u_j - mu_j c_k) + d_k and V_j likewise, so for the CLS query q
+//   score_h(j) = q_h . K_{j,h} = rstd_j (w_h . u_j - mu_j sum(w_h)) + const_h,   w_h = W'_{k,h}^T q_h
+//   ctx_h      = sum_j p_j V_{j,h} = W'_{v,h} z'_h + d_{v,h},   z'_h = sum_j p_j rstd_j (u_j - mu_j)
+// (const_h cancels in the softmax; sum_j p_j = 1).  w for all heads is ONE GEMM against a
+// block-diagonal [H*D x D] weight, ctx ONE GEMM against a block-diagonal [D x H*D] weight; this
+// kernel does the rest per sequence: scores on MFMA (A = u rows straight from HBM, B = w_h from
+// LDS), the masked softmax, and z' on VALU (a second, L2 / Infinity-Cache-served read of u).
+// U is never projected to K and V: at the bge-reranker-base shape that is 2 x D x D x S FLOP and
+// 4 x D x S bytes of K / V per sequence the last layer no longer spends.
+template <int D, int HH>
+__global__ __launch_bounds__(512) void cls_attn_fold_kernel(const half_t* __restrict__ w,
+                                                            const half_t* __restrict__ U,
+                                                            const float* __restrict__ mr,
+                                                            const int32_t* __restrict__ mask, int S,
+                                                            int H, float scale, half_t* __restrict__ z) {
+  constexpr int NCH = D / 8;  // 16-byte chunks per row
+  __shared__ __attribute__((aligned(16))) half_t wl[16 * D];
+  __shared__ __attribute__((aligned(16))) float sc[16 * 512];
+  __shared__ float2 mrl[512];
+  __shared__ float alpha[16], sig[16];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const half_t* wb = w + (int64_t)b * H * D;
+  const half_t* Ub = U + (int64_t)b * S * D;
+  // w_h rows (h >= H: zero), chunk ch of row r at ch ^ (r & 15) (conflict-free B-fragment reads)
+  for (int i = tid; i < 16 * NCH; i += 512) {
+    const int r = i / NCH, ch = i - r * NCH;
+    half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < H) v = *reinterpret_cast<const half8*>(wb + (int64_t)r * D + ch * 8);
+    *reinterpret_cast<half8*>(wl + r * D + ((ch & ~15) | ((ch ^ r) & 15)) * 8) = v;
+  }
+  for (int j = tid; j < S; j += 512) {
+    const float2 m = *reinterpret_cast<const float2*>(mr + ((int64_t)b * S + j) * 2);
+    mrl[j] = mask[(int64_t)b * S + j] ? m : make_float2(0.f, 0.f);
+  }
+  // alpha_h = sum_i w_h[i] (the fp16 w the scores use)
+  for (int h = wave; h < H; h += 8) {
+    float a = 0.f;
+    for (int i = lane; i < D; i += 64) a += (float)wb[(int64_t)h * D + i];
+    a = wave_sum(a);
+    if (lane == 0) alpha[h] = a;
+  }
+  __syncthreads();
+  // scores: token block tb (16 tokens) per wave; lane (c, g): A = token 16 tb + c, dims 32 k + 8 g
+  for (int tb = wave; tb * 16 < S; tb += 8) {
+    const half_t* ur = Ub + (int64_t)(16 * tb + c) * D + 8 * g;
+    half8 a[D / 32];
+#pragma unroll
+    for (int k = 0; k < D / 32; ++k) a[k] = *reinterpret_cast<const half8*>(ur + 32 * k);
+    float4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < D / 32; ++k) {
+      const int ch = 4 * k + g;
+      const half8 bf = *reinterpret_cast<const half8*>(wl + c * D + ((ch & ~15) | ((ch ^ c) & 15)) * 8);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], bf, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // acc[r] = w_c . u_j, j = 16 tb + 4 g + r
+      const int j = 16 * tb + 4 * g + r;
+      const float2 m = mrl[j];
+      const bool live = mask[(int64_t)b * S + j] != 0;
+      if (c < H) sc[c * S + j] = live ? m.y * (acc[r] - m.x * alpha[c]) * scale : -INFINITY;
+    }
+  }
+  __syncthreads();
+  // softmax per head; p'_j = p_j rstd_j (masked tokens: rstd 0), sig_h = sum_j p'_j mu_j
+  for (int h = wave; h < H; h += 8) {
+    float mx = -INFINITY;
+    for (int j = lane; j < S; j += 64) mx = fmaxf(mx, sc[h * S + j]);
+    mx = wave_max(mx);
+    float l = 0.f;
+    for (int j = lane; j < S; j += 64) l += __expf(sc[h * S + j] - mx);
+    l = wave_sum(l);
+    const float inv = 1.f / l;
+    float sg = 0.f;
+    for (int j = lane; j < S; j += 64) {
+      const float2 m = mrl[j];
+      const float pj = __expf(sc[h * S + j] - mx) * inv * m.y;
+      sc[h * S + j] = pj;
+      sg = fmaf(pj, m.x, sg);
+    }
+    sg = wave_sum(sg);
+    if (lane == 0) sig[h] = sg;
+  }
+  __syncthreads();
+  // z'_h[i] = sum_j p'_j u_j[i] - sig_h: thread t owns dims 2t, 2t + 1
+  if (tid < D / 2) {
+    float zx[HH], zy[HH];
+#pragma unroll
+    for (int h = 0; h < HH; ++h) zx[h] = zy[h] = 0.f;
+    const half_t* up = Ub + 2 * tid;
+    // 16 tokens per step: their 16 loads are in flight together (the loop is latency-bound on
+    // the second read of u otherwise)
+    for (int j = 0; j < S; j += 16) {
+      half2_t u[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) u[e] = *reinterpret_cast<const half2_t*>(up + (int64_t)(j + e) * D);
+#pragma unroll
+      for (int h = 0; h < HH; ++h) {
+        if (h >= H) break;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const float4v p = *reinterpret_cast<const float4v*>(sc + h * S + j + 4 * e4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            zx[h] = fmaf(p[e], (float)u[4 * e4 + e][0], zx[h]);
+            zy[h] = fmaf(p[e], (float)u[4 * e4 + e][1], zy[h]);
+          }
+        }
+      }
+    }
+    // z' as an fp16 pair hi + lo (row [hi(H*D) | lo(H*D)]; the ctx GEMM's weight repeats): z' is
+    // rounded once per head, not once per token as V was, so it keeps ~22 bits instead of 11
+    half_t* zb = z + (int64_t)b * 2 * H * D + 2 * tid;
+#pragma unroll
+    for (int h = 0; h < HH; ++h) {
+      if (h >= H) break;
+      const float vx = zx[h] - sig[h], vy = zy[h] - sig[h];
+      half2_t hi, lo;
+      hi[0] = (half_t)vx;
+      hi[1] = (half_t)vy;
+      lo[0] = (half_t)(vx - (float)hi[0]);
+      lo[1] = (half_t)(vy - (float)hi[1]);
+      *reinterpret_cast<half2_t*>(zb + (int64_t)h * D) = hi;
+      *reinterpret_cast<half2_t*>(zb + (int64_t)(H + h) * D) = lo;
+    }
+  }
+}
+
+// Block-diagonal weights of the K/V-free last layer from the folded QKV weight W' [3D x D]:
+//   wk_bd [H*D x D]: row h*D + i, column k = W'_k[k][i] for k in head h, else 0
+//   wv_bd [D x 2*H*D]: row n, column c*H*D + h*D + i (c = 0, 1: the z' hi / lo halves)
+//                      = W'_v[n][i] for h = head of n, else 0
+__global__ void kv_blockdiag_kernel(const half_t* __restrict__ wqkv_f, int D, int H,
+                                    half_t* __restrict__ wk_bd, half_t* __restrict__ wv_bd) {
+  const int dh = D / H;
+  const int64_t r = blockIdx.x;  // 0 .. H*D-1 (wk_bd rows), then D rows of wv_bd
+  if (r < (int64_t)H * D) {
+    const int h = (int)(r / D), i = (int)(r % D);
+    for (int k = threadIdx.x; k < D; k += blockDim.x)
+      wk_bd[r * D + k] = (k / dh == h) ? wqkv_f[(int64_t)(D + k) * D + i] : (half_t)0.f;
+  } else {
+    const int n = (int)(r - (int64_t)H * D), h = n / dh;
+    const int64_t HD = (int64_t)H * D;
+    for (int64_t col = threadIdx.x; col < 2 * HD; col += blockDim.x) {
+      const int64_t cm = col % HD;
+      wv_bd[(int64_t)n * 2 * HD + col] = (cm / D == h) ? wqkv_f[(int64_t)(2 * D + n) * D + cm % D]
+                                                      : (half_t)0.f;
+    }
+  }
+}
+
+bool cls_attn_fold_supported(int S, int D, int H) {
+  return (D == 768 || D == 1024) && H >= 1 && H <= 16 && D % H == 0 && D / H == 64 && S % 16 == 0 &&
+         S >= 16 && S <= 512;
+}
+
+void launch_kv_blockdiag(const half_t* wqkv_f, int D, int H, half_t* wk_bd, half_t* wv_bd,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(kv_blockdiag_kernel, dim3((unsigned)((int64_t)H * D + D)), dim3(256), 0, s,
+                     wqkv_f, D, H, wk_bd, wv_bd);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_cls_attn_fold(const half_t* w, const half_t* U, const float* mr, const int32_t* mask,
+                          int B, int S, int D, int H, half_t* z, hipStream_t s) {
+  SR_CHECK(cls_attn_fold_supported(S, D, H), "cls_attn_fold: unsupported shape");
+  if (B <= 0) return;
+  ProfScope prof("cls_attn_fold", s, 4.0 * B * (double)S * D * H,
+                 2.0 * 2.0 * B * (double)S * D + 2.0 * 2.0 * B * (double)H * D);
+  const float scale = 0.125f;  // 1 / sqrt(64)
+  if (D == 768)
+    hipLaunchKernelGGL((cls_attn_fold_kernel<768, 12>), dim3((unsigned)B), dim3(512), 0, s, w, U, mr,
+                       mask, S, H, scale, z);
+  else
+    hipLaunchKernelGGL((cls_attn_fold_kernel<1024, 16>), dim3((unsigned)B), dim3(512), 0, s, w, U, mr,
+                       mask, S, H, scale, z);
+  SR_LAUNCH_CHECK();
+}
+
 void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(vec_add_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, a, b, out, n);

@@ -138,6 +138,13 @@ void launch_ln_stats_finalize(const float* stat, int nparts, float eps, int M, f
 void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float* gamma,
                      const float* beta, int M, int d, half_t* h16, hipStream_t s);
 void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s);
+// K/V-free CLS-only last layer (k_encoder_misc.hip): block-diagonal K / V weights from the folded
+// QKV weight, and per sequence scores + softmax + z' = sum_j p_j rstd_j (u_j - mu_j)
+bool cls_attn_fold_supported(int S, int D, int H);
+void launch_kv_blockdiag(const half_t* wqkv_f, int D, int H, half_t* wk_bd, half_t* wv_bd,
+                         hipStream_t s);
+void launch_cls_attn_fold(const half_t* w, const half_t* U, const float* mr, const int32_t* mask,
+                          int B, int S, int D, int H, half_t* z, hipStream_t s);
 void launch_scale_f16(const half_t* in, float scale, half_t* out, int64_t n, hipStream_t s);
 
 // k_search.hip

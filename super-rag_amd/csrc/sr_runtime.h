@@ -199,6 +199,8 @@ class Encoder {
     // fp8 modes: e4m3 copies of w2h (FFN) and of the folded w1_f / wqkv_f (all), their per-row
     // exponents and the folded column sums of the quantised weights
     DevBuf w2_8, w2e, w1_8, w1e, c1_8, wqkv8, wqkve, cqkv8;
+    // K/V-free CLS-only last layer: block-diagonal K / V weights, zero bias (H*D)
+    DevBuf wk_bd, wv_bd, zb;
   };
   bool fold_enabled() const;
   void prepare_fold(hipStream_t s);

@@ -326,3 +326,34 @@ def test_fp8_ffn_persistent_tiles():
     got8 = enc.cross_score(ids, mask)
     ref8 = R.cross_logits(_ref_cfg(spec), w, ids, mask, fp8_ffn=True)
     assert np.abs(got8 - ref8).max() <= 8e-3 * (1.0 + np.abs(ref8).max())
+
+
+@pytest.mark.parametrize("S,L", [(16, 2), (64, 3), (128, 2)])
+def test_kvfree_cls_last_layer(S, L, monkeypatch):
+    # K/V-free CLS-only last layer (cls_attn_fold): with LN folded the CLS query's scores are
+    # rstd_j (w_h . u_j - mu_j sum w_h) with w_h = W'_{k,h}^T q_h and its context W'_v z' + d_v, so
+    # no token is projected to K / V.  Ragged masks, non-trivial LayerNorm affine parameters, the
+    # bge-reranker head geometry (d 768, 12 heads of 64): against the fp32 oracle within the fp16
+    # residual band, and against the K, V GEMM + CLS attention path (SR_KVFREE_CLS=0).
+    from super_rag_amd.encoder import Encoder, random_weights
+    spec = _tiny("xlmr", d=768, H=12, F=3072, L=L, classifier=1, P=200, res16=True)
+    w = random_weights(spec, seed=41 + S, style="test")
+    rng = np.random.default_rng(S)
+    for k in list(w):
+        if k.endswith("LayerNorm.weight"):
+            w[k] = (1.0 + 0.3 * rng.standard_normal(w[k].shape)).astype(np.float32)
+        elif k.endswith("LayerNorm.bias"):
+            w[k] = (0.2 * rng.standard_normal(w[k].shape)).astype(np.float32)
+    w["classifier.out_proj.weight"] *= 20.0
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 40, S, seed=7 + S, ragged=True)
+    got = enc.cross_score(ids, mask)[:, 0]
+    monkeypatch.setenv("SR_KVFREE_CLS", "0")
+    kv = enc.cross_score(ids, mask)[:, 0]
+    ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)[:, 0]
+    tol = 1e-2 * (1.0 + np.abs(ref).max())
+    assert np.abs(got - ref).max() <= tol
+    assert np.abs(kv - ref).max() <= tol
+    # the two paths differ only by where fp16 rounding happens (K / V vs w / z')
+    assert np.abs(got - kv).max() <= tol
+    assert not np.array_equal(got, kv)
