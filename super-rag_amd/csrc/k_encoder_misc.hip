@@ -567,12 +567,19 @@ __global__ __launch_bounds__(512) void cls_attn_fold_kernel(const half_t* __rest
 #pragma unroll
     for (int h = 0; h < HH; ++h) zx[h] = zy[h] = 0.f;
     const half_t* up = Ub + 2 * tid;
-    // 16 tokens per step: their 16 loads are in flight together (the loop is latency-bound on
-    // the second read of u otherwise)
+    // 16 tokens per step, the next step's 16 loads in flight while this step's FMAs run (the loop
+    // is latency-bound on the second read of u otherwise)
+    half2_t un[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) un[e] = *reinterpret_cast<const half2_t*>(up + (int64_t)e * D);
     for (int j = 0; j < S; j += 16) {
       half2_t u[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) u[e] = *reinterpret_cast<const half2_t*>(up + (int64_t)(j + e) * D);
+      for (int e = 0; e < 16; ++e) u[e] = un[e];
+      if (j + 16 < S) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) un[e] = *reinterpret_cast<const half2_t*>(up + (int64_t)(j + 16 + e) * D);
+      }
 #pragma unroll
       for (int h = 0; h < HH; ++h) {
         if (h >= H) break;
