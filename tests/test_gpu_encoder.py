@@ -328,15 +328,16 @@ def test_fp8_ffn_persistent_tiles():
     assert np.abs(got8 - ref8).max() <= 8e-3 * (1.0 + np.abs(ref8).max())
 
 
-@pytest.mark.parametrize("S,L", [(16, 2), (64, 3), (128, 2)])
-def test_kvfree_cls_last_layer(S, L, monkeypatch):
+@pytest.mark.parametrize("S,L,d,H", [(16, 2, 768, 12), (64, 3, 768, 12), (128, 2, 768, 12),
+                                     (64, 2, 1024, 16)])
+def test_kvfree_cls_last_layer(S, L, d, H, monkeypatch):
     # K/V-free CLS-only last layer (cls_attn_fold): with LN folded the CLS query's scores are
     # rstd_j (w_h . u_j - mu_j sum w_h) with w_h = W'_{k,h}^T q_h and its context W'_v z' + d_v, so
     # no token is projected to K / V.  Ragged masks, non-trivial LayerNorm affine parameters, the
-    # bge-reranker head geometry (d 768, 12 heads of 64): against the fp32 oracle within the fp16
-    # residual band, and against the K, V GEMM + CLS attention path (SR_KVFREE_CLS=0).
+    # bge-reranker-base / -v2-m3 head geometries (d 768 / 1024, heads of 64): against the fp32 oracle
+    # within the fp16 residual band, and against the K, V GEMM + CLS attention path (SR_KVFREE_CLS=0).
     from super_rag_amd.encoder import Encoder, random_weights
-    spec = _tiny("xlmr", d=768, H=12, F=3072, L=L, classifier=1, P=200, res16=True)
+    spec = _tiny("xlmr", d=d, H=H, F=4 * d, L=L, classifier=1, P=200, res16=True)
     w = random_weights(spec, seed=41 + S, style="test")
     rng = np.random.default_rng(S)
     for k in list(w):
