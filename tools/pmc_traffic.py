@@ -45,6 +45,7 @@ def logical(name):
         return base
     m = re.search(r"\d+([a-z0-9_]+?)_kernel", name) or re.search(r"::(\w+?)_kernel", name)
     base = m.group(1) if m else name
+    base = re.sub(r"^sr\d+", "", base)  # kernels in namespace sr itself (not the anonymous one)
     if base.startswith("attention"):
         return "attention"
     if base == "qkv_attn":

@@ -4,6 +4,8 @@
 #   2. FETCH_SIZE and WRITE_SIZE in separate PMC passes (MI355X_MICROARCH.md: one TCC counter
 #      group per pass) over a 1-step bench
 #   3. MFMA busy cycles + GRBM_GUI_ACTIVE (matrix-pipe utilisation and the clock actually held)
+# All with --no-extras: the extras (drop-in flow, peaks, B = 32 search) launch the same kernels at
+# other shapes, which would mix into the per-launch means of the timed step's kernels.
 # Summaries: python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles/<tag>_pmc_traffic.json
 # Outputs under gpurun_out/prof_<tag>/.
 set -e
@@ -12,10 +14,10 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_trace.log 2>&1
+  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras > $OUT/bench_trace.log 2>&1
 timeout -k 10 600 rocprofv3 -i tools/pmc_fetch.txt -d $OUT/fetch -o run --output-format csv -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_fetch.log 2>&1
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_fetch.log 2>&1
 timeout -k 10 600 rocprofv3 -i tools/pmc_write.txt -d $OUT/write -o run --output-format csv -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_write.log 2>&1
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_write.log 2>&1
 timeout -k 10 600 rocprofv3 -i tools/pmc_mfma.txt -d $OUT/mfma -o run --output-format csv -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_mfma.log 2>&1
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_mfma.log 2>&1
