@@ -63,9 +63,10 @@ async def execute_search_flow(query: str, collection_id: str, search_user_id: st
     rr, _ = await NODE_RUNNER_REGISTRY["rerank"]["runner"].run(
         RerankInput(use_rerank_service=use_service, model=model, model_service_provider=msp,
                     custom_llm_provider=provider, docs=merged.docs), si)
-    items = [SearchResultItem(rank=i + 1, score=d.score, content=d.text,
-                              source=(d.metadata or {}).get("source", ""),
-                              recall_type=(d.metadata or {}).get("recall_type", ""),
-                              metadata=d.metadata)
+    # (typed values from the runners: constructed without re-validation, 100 per request)
+    items = [SearchResultItem.model_construct(rank=i + 1, score=d.score, content=d.text,
+                                              source=(d.metadata or {}).get("source", ""),
+                                              recall_type=(d.metadata or {}).get("recall_type", ""),
+                                              metadata=d.metadata)
              for i, d in enumerate(rr.docs)]
     return items, "rerank"

@@ -62,12 +62,16 @@ class RerankService:
         enc = [tokenizer.encode_pairs(q, t) for q, t in items]
         n = [e[0].shape[0] for e in enc]
         S = max(e[0].shape[1] for e in enc)
-
-        def pad(a, v):
-            return np.pad(a, ((0, 0), (0, S - a.shape[1])), constant_values=v)
-        ids = np.concatenate([pad(e[0], encoder.spec.pad_id) for e in enc])
-        mask = np.concatenate([pad(e[1], 0) for e in enc])
-        tt = np.concatenate([pad(e[2], 0) for e in enc])
+        ids = np.full((sum(n), S), encoder.spec.pad_id, dtype=np.int32)
+        mask = np.zeros((sum(n), S), dtype=np.int32)
+        tt = np.zeros((sum(n), S), dtype=np.int32)
+        o = 0
+        for (ei, em, et), k in zip(enc, n):
+            w = ei.shape[1]
+            ids[o:o + k, :w] = ei
+            mask[o:o + k, :w] = em
+            tt[o:o + k, :w] = et
+            o += k
         out = np.empty(ids.shape[0], dtype=np.float32)
         for s in range(0, ids.shape[0], device_batch):
             sl = slice(s, s + device_batch)

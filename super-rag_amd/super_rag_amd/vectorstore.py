@@ -98,6 +98,23 @@ def _load_store(path: str, device: int, devices: Optional[List[int]]):
     return _store_loader(path, devices[0] if devices else device)
 
 
+
+def _json_copy(v):
+    """Deep copy of JSON-like metadata (dict / list / scalars), ~10x cheaper than copy.deepcopy:
+    every returned document owns its metadata, as SeekDB's JSON-decoded results did."""
+    if isinstance(v, dict):
+        return {k: _json_copy(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_json_copy(x) for x in v]
+    if isinstance(v, (str, int, float, bool)) or v is None:
+        return v
+    return copy.deepcopy(v)
+
+
+# DocumentWithScore without re-validation for the connector's own, already typed values (text str,
+# score float, metadata dict): 100 per request on the per-request path
+_make_doc = getattr(DocumentWithScore, "model_construct", DocumentWithScore)
+
 class _Collection:
     def __init__(self, name: str, dim: int, device: int, store=None,
                  devices: Optional[List[int]] = None):
@@ -446,8 +463,8 @@ class MI355XVectorStoreConnector:
                     dist, rows = c.store.search(Q, kmax, allow=allow, mask_key=mkey)
                 for j, i in enumerate(idx):
                     k = items[i][1]
-                    out[i] = [DocumentWithScore(text=c.texts[r], score=float(d),
-                                                metadata=copy.deepcopy(c.metadatas[r]))
+                    out[i] = [_make_doc(text=c.texts[r], score=float(d),
+                                        metadata=_json_copy(c.metadatas[r]))
                               for d, r in zip(dist[j, :k].tolist(), rows[j, :k].tolist()) if r >= 0]
         return out
 
@@ -464,8 +481,7 @@ class MI355XVectorStoreConnector:
                 mkey, allow = self._allow_mask(c, flt)
             scores, rows = c.lex.hybrid(c.store, q.reshape(1, -1), [terms], k, k_each,
                                         self.rrf_rank_const, allow=allow, mask_key=mkey)
-            return [DocumentWithScore(text=c.texts[r], score=float(s),
-                                      metadata=copy.deepcopy(c.metadatas[r]))
+            return [_make_doc(text=c.texts[r], score=float(s), metadata=_json_copy(c.metadatas[r]))
                     for s, r in zip(scores[0].tolist(), rows[0].tolist()) if r >= 0]
 
     def fulltext_search(self, query_text: str, top_k: int, keywords: Optional[List[str]] = None,
@@ -489,8 +505,7 @@ class MI355XVectorStoreConnector:
             if flt is not None:
                 mkey, allow = self._allow_mask(c, flt)
             scores, rows = c.lex.search([terms], min(int(top_k), 1024), allow=allow, mask_key=mkey)
-            return [DocumentWithScore(text=c.texts[r], score=float(s),
-                                      metadata=copy.deepcopy(c.metadatas[r]))
+            return [_make_doc(text=c.texts[r], score=float(s), metadata=_json_copy(c.metadatas[r]))
                     for s, r in zip(scores[0].tolist(), rows[0].tolist()) if r >= 0]
 
     def get_vectors(self, ids: List[str]) -> np.ndarray:
