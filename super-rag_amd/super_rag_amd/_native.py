@@ -145,6 +145,23 @@ SIGNATURES = {
 }
 
 _lib = None
+
+_gates: dict = {}
+_gates_lock = threading.Lock()
+
+
+def device_gate(device: int) -> threading.Lock:
+    """One lock per device, held by the coalesced request paths (embed_query, connector search,
+    rerank scoring) around their device calls.  Without it, a concurrent small batch (a 12-layer
+    embed of a few queries: ~100 short kernels) interleaves kernel by kernel with a large rerank
+    batch on the same GPU, so each of its kernels waits for a ~1 ms rerank kernel and the stage
+    takes ~100x its own time; with it, each stage's batch runs back to back and the waiting
+    requests join the next, larger batch (profiles/r03_dropin/)."""
+    g = _gates.get(device)
+    if g is None:
+        with _gates_lock:
+            g = _gates.setdefault(device, threading.Lock())
+    return g
 _lock = threading.Lock()
 
 

@@ -14,6 +14,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
+from ._native import device_gate
 from .errors import (BatchProcessingError, EmbeddingError, EmptyTextError,
                      InvalidConfigurationError)
 
@@ -53,7 +54,8 @@ class EmbeddingService:
             idx = order[s:s + device_batch]
             try:
                 ids, mask = tokenizer.encode_batch([texts[i] for i in idx])
-                out[idx] = encoder.embed(ids, mask)
+                with device_gate(getattr(encoder, "device", 0)):
+                    out[idx] = encoder.embed(ids, mask)
             except Exception as e:  # noqa: BLE001 - a failed device batch, as in :94-99
                 raise BatchProcessingError(batch_size=len(idx), reason=f"device batch failed: {e}") from e
         return out

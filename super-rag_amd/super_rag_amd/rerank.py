@@ -15,6 +15,7 @@ from typing import List, Optional
 
 import numpy as np
 
+from ._native import device_gate
 from .errors import InvalidConfigurationError, InvalidDocumentError, RerankError, TooManyDocumentsError
 
 logger = logging.getLogger(__name__)
@@ -41,7 +42,9 @@ class RerankService:
 
     def score(self, query: str, texts: List[str]) -> np.ndarray:
         """Raw cross-encoder logits, one per text.  Concurrent calls (one per search request)
-        are coalesced into shared device batches per cross-encoder (coalesce.py)."""
+        are coalesced into shared device batches per cross-encoder (coalesce.py).  The batch
+        leader packs every caller's pairs: packing in the callers, concurrently, measured slower
+        (GIL contention; 210.7 vs 228.1 q/s, profiles/r03_dropin/)."""
         if not self.coalesce:
             return self._score_many(self.encoder, self.tokenizer, self.device_batch, [(query, texts)])[0]
         coal = getattr(self.encoder, "_pair_coalescer", None)
@@ -55,13 +58,22 @@ class RerankService:
 
     @staticmethod
     def _score_many(encoder, tokenizer, device_batch: int, items) -> List[np.ndarray]:
-        """[(query, texts)] -> per item logits; the pairs of all items share device batches
-        (each batch padded to its longest pair; the padding is masked, so logits do not depend on
-        the batch composition)."""
+        """[(query, texts)] -> per item logits."""
+        return RerankService._score_encoded(
+            encoder, device_batch, [tokenizer.encode_pairs(q, t) for q, t in items])
+
+    @staticmethod
+    def _score_encoded(encoder, device_batch: int, enc) -> List[np.ndarray]:
+        """[(ids, mask, type_ids)] of encode_pairs -> per item logits; the pairs of all items
+        share device batches (padded to a common width; the padding is masked, so logits do not
+        depend on the batch composition)."""
         with_types = encoder.spec.pair_style == 1
-        enc = [tokenizer.encode_pairs(q, t) for q, t in items]
         n = [e[0].shape[0] for e in enc]
         S = max(e[0].shape[1] for e in enc)
+        # bucketed width: up to 128 tokens -> 128 (the fused QKV + attention kernel and the K/V-free
+        # last layer take S = 128 / S % 16 == 0), longer -> a multiple of 16 within max_length
+        cap = max(S, int(getattr(encoder.spec, "max_length", S)))
+        S = min(128 if S <= 128 else -(-S // 16) * 16, cap)
         ids = np.full((sum(n), S), encoder.spec.pad_id, dtype=np.int32)
         mask = np.zeros((sum(n), S), dtype=np.int32)
         tt = np.zeros((sum(n), S), dtype=np.int32)
@@ -73,9 +85,10 @@ class RerankService:
             tt[o:o + k, :w] = et
             o += k
         out = np.empty(ids.shape[0], dtype=np.float32)
-        for s in range(0, ids.shape[0], device_batch):
-            sl = slice(s, s + device_batch)
-            out[sl] = encoder.cross_score(ids[sl], mask[sl], tt[sl] if with_types else None)[:, 0]
+        with device_gate(getattr(encoder, "device", 0)):
+            for s in range(0, ids.shape[0], device_batch):
+                sl = slice(s, s + device_batch)
+                out[sl] = encoder.cross_score(ids[sl], mask[sl], tt[sl] if with_types else None)[:, 0]
         res, o = [], 0
         for k in n:
             res.append(out[o:o + k])

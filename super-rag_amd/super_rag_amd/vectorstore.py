@@ -33,6 +33,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
 
+from ._native import device_gate
 from .models import DocumentWithScore, QueryResult
 
 logger = logging.getLogger(__name__)
@@ -457,10 +458,12 @@ class MI355XVectorStoreConnector:
                 Q = np.stack([np.asarray(items[i][0], dtype=np.float32).reshape(-1) for i in idx])
                 kmax = max(items[i][1] for i in idx)
                 if key == "":
-                    dist, rows = c.store.search(Q, kmax)
+                    with device_gate(getattr(c.store, "device", 0)):
+                        dist, rows = c.store.search(Q, kmax)
                 else:
                     mkey, allow = MI355XVectorStoreConnector._allow_mask(c, items[idx[0]][2])
-                    dist, rows = c.store.search(Q, kmax, allow=allow, mask_key=mkey)
+                    with device_gate(getattr(c.store, "device", 0)):
+                        dist, rows = c.store.search(Q, kmax, allow=allow, mask_key=mkey)
                 for j, i in enumerate(idx):
                     k = items[i][1]
                     out[i] = [_make_doc(text=c.texts[r], score=float(d),

@@ -164,8 +164,11 @@ def main():
     ap.add_argument("--concurrency", type=int, nargs="+", default=[64, 256])
     ap.add_argument("--seconds", type=float, default=15.0)
     ap.add_argument("--profile", action="store_true",
-                    help="cProfile the event loop and every worker thread of one C = 64 run (host "
-                         "time per request by function), printed after the JSON line")
+                    help="cProfile the event loop and every worker thread of one run at "
+                         "--profile-concurrency (host time per request by function), printed after "
+                         "the JSON line")
+    ap.add_argument("--profile-concurrency", type=int, default=64,
+                    help="1: no GIL contention, so the per-function times are the host CPU cost")
     a = ap.parse_args()
     if a.profile:
         import cProfile
@@ -176,7 +179,7 @@ def main():
         measure(16, 3.0, "dropin", queries)
         main_pr = cProfile.Profile()
         main_pr.enable()
-        r = measure(64, a.seconds, "dropin", queries, profile=True)
+        r = measure(a.profile_concurrency, a.seconds, "dropin", queries, profile=True)
         main_pr.disable()
         print(json.dumps(r), flush=True)
         for pr in _PROFILES:
