@@ -6,9 +6,11 @@ every compute entry point raises :class:`NativeUnavailableError`.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
+import time
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_void_p
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsrmi.so")
@@ -150,18 +152,45 @@ _gates: dict = {}
 _gates_lock = threading.Lock()
 
 
-def device_gate(device: int) -> threading.Lock:
-    """One lock per device, held by the coalesced request paths (embed_query, connector search,
-    rerank scoring) around their device calls.  Without it, a concurrent small batch (a 12-layer
-    embed of a few queries: ~100 short kernels) interleaves kernel by kernel with a large rerank
-    batch on the same GPU, so each of its kernels waits for a ~1 ms rerank kernel and the stage
-    takes ~100x its own time; with it, each stage's batch runs back to back and the waiting
-    requests join the next, larger batch (profiles/r03_dropin/)."""
+class _DeviceGate:
+    """The per-device lock of device_gate and the time it was held, per stage."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.busy: dict = {}    # stage -> [seconds held, holds]
+
+    @contextlib.contextmanager
+    def hold(self, stage: str):
+        with self.lock:
+            t0 = time.perf_counter()
+            try:
+                yield
+            finally:
+                b = self.busy.setdefault(stage, [0.0, 0])
+                b[0] += time.perf_counter() - t0
+                b[1] += 1
+
+
+def device_gate(device: int, stage: str = "device"):
+    """Context manager: one lock per device, held by the coalesced request paths (embed_query,
+    connector search, rerank scoring) around their device calls.  Without it, a concurrent small
+    batch (a 12-layer embed of a few queries: ~100 short kernels) interleaves kernel by kernel with
+    a large rerank batch on the same GPU, so each of its kernels waits for a ~1 ms rerank kernel;
+    with it, each stage's batch runs back to back and the waiting requests join the next, larger
+    batch.  The time held is kept per stage (gate_busy: the device's busy time by stage, since the
+    calls synchronise before they return)."""
     g = _gates.get(device)
     if g is None:
         with _gates_lock:
-            g = _gates.setdefault(device, threading.Lock())
-    return g
+            g = _gates.setdefault(device, _DeviceGate())
+    return g.hold(stage)
+
+
+def gate_busy() -> dict:
+    """{device: {stage: (seconds held, holds)}} accumulated by device_gate."""
+    return {d: {k: (v[0], v[1]) for k, v in g.busy.items()} for d, g in list(_gates.items())}
+
+
 _lock = threading.Lock()
 
 

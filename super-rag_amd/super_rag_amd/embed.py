@@ -54,7 +54,7 @@ class EmbeddingService:
             idx = order[s:s + device_batch]
             try:
                 ids, mask = tokenizer.encode_batch([texts[i] for i in idx])
-                with device_gate(getattr(encoder, "device", 0)):
+                with device_gate(getattr(encoder, "device", 0), "embed"):
                     out[idx] = encoder.embed(ids, mask)
             except Exception as e:  # noqa: BLE001 - a failed device batch, as in :94-99
                 raise BatchProcessingError(batch_size=len(idx), reason=f"device batch failed: {e}") from e

@@ -85,7 +85,7 @@ class RerankService:
             tt[o:o + k, :w] = et
             o += k
         out = np.empty(ids.shape[0], dtype=np.float32)
-        with device_gate(getattr(encoder, "device", 0)):
+        with device_gate(getattr(encoder, "device", 0), "rerank"):
             for s in range(0, ids.shape[0], device_batch):
                 sl = slice(s, s + device_batch)
                 out[sl] = encoder.cross_score(ids[sl], mask[sl], tt[sl] if with_types else None)[:, 0]

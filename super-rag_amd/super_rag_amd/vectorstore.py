@@ -458,11 +458,11 @@ class MI355XVectorStoreConnector:
                 Q = np.stack([np.asarray(items[i][0], dtype=np.float32).reshape(-1) for i in idx])
                 kmax = max(items[i][1] for i in idx)
                 if key == "":
-                    with device_gate(getattr(c.store, "device", 0)):
+                    with device_gate(getattr(c.store, "device", 0), "search"):
                         dist, rows = c.store.search(Q, kmax)
                 else:
                     mkey, allow = MI355XVectorStoreConnector._allow_mask(c, items[idx[0]][2])
-                    with device_gate(getattr(c.store, "device", 0)):
+                    with device_gate(getattr(c.store, "device", 0), "search"):
                         dist, rows = c.store.search(Q, kmax, allow=allow, mask_key=mkey)
                 for j, i in enumerate(idx):
                     k = items[i][1]

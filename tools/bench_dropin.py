@@ -11,7 +11,8 @@ collection), RerankService.async_rerank (pairs of concurrent requests coalesced 
 hashing tokenizer: SUPER_RAG_AMD_SYNTHETIC), vector_topk = 100 candidates reranked at S_pair <= 128.
 
 Reported per concurrency: requests/s, mean coalesced batch per stage (items / device batches of
-each Coalescer), p50 / p99 request latency.  The batched SearchPipeline number (bench.py's headline)
+each Coalescer), the device time per stage (device_gate hold time: fraction of the run, ms per
+device batch), p50 / p99 request latency.  The batched SearchPipeline number (bench.py's headline)
 is the ceiling this path approaches as batches fill; the reference's own host orchestration costs
 5.1 ms per query (profiles/r02_reference_orchestration.json) before any model work.
 
@@ -120,12 +121,15 @@ def measure(concurrency: int, seconds: float, col_id: str, queries, profile: boo
     loop.set_default_executor(concurrent.futures.ThreadPoolExecutor(
         max_workers=concurrency + 8, initializer=_profiled_worker_init if profile else None))
     try:
+        from super_rag_amd._native import gate_busy
         before = {k: (c.batches, c.items) for k, c in _coalescers().items()}
+        busy0 = gate_busy()
         lat: list = []
         t0 = time.perf_counter()
         n = loop.run_until_complete(_closed_loop(concurrency, seconds, col_id, queries, lat))
         dt = time.perf_counter() - t0
         after = {k: (c.batches, c.items) for k, c in _coalescers().items()}
+        busy1 = gate_busy()
     finally:
         loop.close()
     stages = {}
@@ -133,6 +137,15 @@ def measure(concurrency: int, seconds: float, col_id: str, queries, profile: boo
         b0, i0 = before.get(k, (0, 0))
         if b > b0:
             stages[k] = {"batches": b - b0, "mean_batch": round((i - i0) / (b - b0), 2)}
+    # device time by stage: the device_gate hold times (each stage's calls synchronise), as a
+    # fraction of the run and per device batch
+    for d, st in busy1.items():
+        for k, (sec, holds) in st.items():
+            s0, h0 = busy0.get(d, {}).get(k, (0.0, 0))
+            if holds > h0:
+                e = stages.setdefault(k, {})
+                e["device_busy_frac"] = round((sec - s0) / dt, 3)
+                e["device_ms_per_batch"] = round((sec - s0) / (holds - h0) * 1e3, 2)
     lat_ms = np.asarray(lat) * 1e3
     return {"concurrency": concurrency, "requests": n, "seconds": round(dt, 2),
             "qps": round(n / dt, 1), "p50_ms": round(float(np.percentile(lat_ms, 50)), 1),
