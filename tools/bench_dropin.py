@@ -152,7 +152,8 @@ def measure(concurrency: int, seconds: float, col_id: str, queries, profile: boo
             "p99_ms": round(float(np.percentile(lat_ms, 99)), 1), "coalesced": stages}
 
 
-def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16) -> dict:
+def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16,
+        start_at: float = 0.0) -> dict:
     col_id = "dropin"
     t = time.time()
     build_collection(col_id, rows)
@@ -161,6 +162,8 @@ def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup
     queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
     # warm up: models resident, kernels compiled, coalescers created
     measure(min(warmup, max(concurrency)), 3.0, col_id, queries)
+    if start_at > time.time():  # several serving processes on one GPU: measure together
+        time.sleep(start_at - time.time())
     out = {"path": ("execute_search_flow (collection_service.py:229-366) -> pack vector_search / "
                     "merge / rerank runners -> EmbeddingService.embed_query + connector.search + "
                     "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
@@ -176,6 +179,9 @@ def main():
     ap.add_argument("--rows", type=int, default=100000)
     ap.add_argument("--concurrency", type=int, nargs="+", default=[64, 256])
     ap.add_argument("--seconds", type=float, default=15.0)
+    ap.add_argument("--start-at", type=float, default=0.0,
+                    help="wall-clock time (time.time()) to start the measured runs at, after "
+                         "setup and warmup: several processes serving from one GPU measure together")
     ap.add_argument("--profile", action="store_true",
                     help="cProfile the event loop and every worker thread of one run at "
                          "--profile-concurrency (host time per request by function), printed after "
@@ -202,7 +208,7 @@ def main():
             st.add(pr)
         st.sort_stats("tottime").print_stats(45)
         return
-    print(json.dumps(run(a.rows, a.concurrency, a.seconds)), flush=True)
+    print(json.dumps(run(a.rows, a.concurrency, a.seconds, start_at=a.start_at)), flush=True)
 
 
 if __name__ == "__main__":
