@@ -3,7 +3,7 @@
 # models, collection and coalescers; C = 64 callers each), measured over the same 10 s window.
 # Summary: python tools/dropin_mp_summary.py gpurun_out/dropin_mp
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/dropin_mp
-for np_ in 1 2 4; do
+for np_ in ${DROPIN_PROCS:-1 2 4}; do
   t0=$(python3 -c "import time; print(time.time() + 75)")
   pids=()
   for i in $(seq 0 $((np_ - 1))); do
