@@ -119,3 +119,44 @@ def test_rerank_scores_coalesced_equal_one_by_one():
     for (q, ts), g in zip(items, got):
         np.testing.assert_allclose(g, [relevance(q, t) for t in ts], rtol=1e-6)
     assert enc._pair_coalescer.items == 40
+
+
+def test_rerank_batch_width_is_bucketed_and_padding_is_masked():
+    # _score_many pads a device batch to 128 (<= 128 tokens) or a multiple of 16 within the model's
+    # max_length, so per-request batches take the S = 128 fused attention and the K/V-free last
+    # layer; the padding is masked, so the logits equal the unpadded ones.  The device calls are
+    # counted under the "rerank" stage of device_gate.
+    from types import SimpleNamespace
+    from super_rag_amd._native import gate_busy
+    from super_rag_amd.rerank import RerankService
+
+    class Tok:
+        def encode_pairs(self, q, texts):
+            w = len(q)
+            ids = np.arange(len(texts) * w, dtype=np.int32).reshape(len(texts), w) + 3
+            mask = np.ones_like(ids)
+            mask[:, w - 2:] = np.arange(len(texts))[:, None] % 2  # ragged rows
+            return ids, mask, np.zeros_like(ids)
+
+    class Enc:
+        spec = SimpleNamespace(pad_id=1, pair_style=0, max_length=512)
+        device = 0
+
+        def __init__(self):
+            self.widths = []
+
+        def cross_score(self, ids, mask, types=None):
+            self.widths.append(ids.shape[1])
+            return ((ids * mask).sum(1, dtype=np.int64) % 10007).astype(np.float32)[:, None]
+
+    tok = Tok()
+    for w, want in [(7, 128), (100, 128), (128, 128), (130, 144), (505, 512), (512, 512)]:
+        enc = Enc()
+        before = gate_busy().get(0, {}).get("rerank", (0.0, 0))[1]
+        items = [("q" * w, ["a", "b", "c"]), ("q" * max(1, w - 5), ["d"])]
+        got = RerankService._score_many(enc, tok, 4096, items)
+        assert enc.widths == [want]
+        for (q, ts), g in zip(items, got):
+            ids, mask, _ = tok.encode_pairs(q, ts)
+            np.testing.assert_array_equal(g, ((ids * mask).sum(1, dtype=np.int64) % 10007).astype(np.float32))
+        assert gate_busy()[0]["rerank"][1] == before + 1
