@@ -2,6 +2,9 @@
 // LayerNorm, pooling + L2 normalisation, classification logits, row normalisation.
 // All are HBM-bound row kernels: one wave per row, 16-byte vector accesses, fp32 statistics with
 // wave shuffles (two-pass mean / variance held in registers).
+#include <algorithm>
+#include <cstdlib>
+
 #include "sr_common.h"
 #include "sr_kernels.h"
 
@@ -612,6 +615,175 @@ __global__ __launch_bounds__(512) void cls_attn_fold_kernel(const half_t* __rest
   }
 }
 
+// Single-read form (S <= 128): the score phase keeps each wave's 16 token rows of u in registers
+// (its MFMA A fragments, 16 tokens x D); after the softmax the rows go through LDS 32 tokens at a
+// time ([token][D + 4] halfs: the 4 k-groups of a B fragment land on distinct banks) and
+// z'[16 heads x D] = p' . u runs on MFMA (A = p' as an fp16 hi + lo pair, so z' keeps fp32-like
+// precision; B = 8 tokens of one dim per lane).  u is read from HBM once (the two-pass form reads
+// it twice and accumulates z' on VALU with 4-byte loads); z' leaves through LDS as 16-byte stores.
+constexpr int CF_T = 32;  // tokens per LDS round
+// persistent: one workgroup per CU (175 / 239 VGPRs) walks sequences b, b + grid, ...; a wave
+// loads its rows of the NEXT sequence as soon as its own round has put this sequence's rows into
+// LDS, so the HBM reads overlap the remaining rounds, the z' store and the next sequence's prologue
+template <int D, int HH>
+__global__ __launch_bounds__(512) void cls_attn_fold1_kernel(const half_t* __restrict__ w,
+                                                             const half_t* __restrict__ U,
+                                                             const float* __restrict__ mr,
+                                                             const int32_t* __restrict__ mask, int B,
+                                                             int S, int H, float scale,
+                                                             half_t* __restrict__ z) {
+  constexpr int NCH = D / 8, KD = D / 32, LDU = D + 4;
+  constexpr int NT = D / 16 / 8;  // z' column tiles (16 dims) per wave
+  // D = 1024 (128 VGPRs of rows + 32 of z') loads its rows at the top of each sequence instead:
+  // the early prefetch spills there
+  constexpr bool PF = D <= 768;
+  static_assert(CF_T * LDU >= 2 * 16 * D, "the stage area holds z' (hi, lo) on the way out");
+  __shared__ __attribute__((aligned(16))) half_t wl[16 * D];
+  __shared__ __attribute__((aligned(16))) half_t ust[CF_T * LDU];
+  __shared__ __attribute__((aligned(16))) float sc[16 * 128];
+  __shared__ float2 mrl[128];
+  __shared__ float alpha[16], sig[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  // this wave's token rows (tb = wave) of sequence bb, all loads in flight before any wait
+  const bool has = 16 * wave < S;
+  half8 a[KD];
+  auto load_rows = [&](int bb) __attribute__((always_inline)) {
+    if (has) {
+      const half_t* ur = U + ((int64_t)bb * S + 16 * wave + c) * D + 8 * g;
+#pragma unroll
+      for (int k = 0; k < KD; ++k) a[k] = *reinterpret_cast<const half8*>(ur + 32 * k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < KD; ++k) a[k] = half8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  int b = blockIdx.x;
+  if (b >= B) return;
+  if (PF) load_rows(b);
+  const int rounds = (S + CF_T - 1) / CF_T;
+  for (; b < B; b += gridDim.x) {
+    const int nb = b + (int)gridDim.x;
+    if (!PF) load_rows(b);
+    const half_t* wb = w + (int64_t)b * H * D;
+    for (int i = tid; i < 16 * NCH; i += 512) {
+      const int r = i / NCH, ch = i - r * NCH;
+      half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (r < H) v = *reinterpret_cast<const half8*>(wb + (int64_t)r * D + ch * 8);
+      *reinterpret_cast<half8*>(wl + r * D + ((ch & ~15) | ((ch ^ r) & 15)) * 8) = v;
+    }
+    for (int j = tid; j < S; j += 512) {
+      const float2 m = *reinterpret_cast<const float2*>(mr + ((int64_t)b * S + j) * 2);
+      mrl[j] = mask[(int64_t)b * S + j] ? m : make_float2(0.f, 0.f);
+    }
+    for (int i = tid; i < 16 * 128; i += 512) sc[i] = 0.f;  // heads >= H, tokens >= S: p' = 0
+    for (int h = wave; h < H; h += 8) {
+      float s = 0.f;
+      for (int i = lane; i < D; i += 64) s += (float)wb[(int64_t)h * D + i];
+      s = wave_sum(s);
+      if (lane == 0) alpha[h] = s;
+    }
+    __syncthreads();
+    if (has) {
+      float4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int ch = 4 * k + g;
+        const half8 bf = *reinterpret_cast<const half8*>(wl + c * D + ((ch & ~15) | ((ch ^ c) & 15)) * 8);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], bf, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // acc[r] = w_c . u_j, j = 16 wave + 4 g + r
+        const int j = 16 * wave + 4 * g + r;
+        const float2 m = mrl[j];
+        const bool live = mask[(int64_t)b * S + j] != 0;
+        if (c < H) sc[c * 128 + j] = live ? m.y * (acc[r] - m.x * alpha[c]) * scale : -INFINITY;
+      }
+    }
+    __syncthreads();
+    // softmax per head; p'_j = p_j rstd_j (masked tokens: rstd 0), sig_h = sum_j p'_j mu_j
+    for (int h = wave; h < H; h += 8) {
+      float mx = -INFINITY;
+      for (int j = lane; j < S; j += 64) mx = fmaxf(mx, sc[h * 128 + j]);
+      mx = wave_max(mx);
+      float l = 0.f;
+      for (int j = lane; j < S; j += 64) l += __expf(sc[h * 128 + j] - mx);
+      l = wave_sum(l);
+      const float inv = 1.f / l;
+      float sg = 0.f;
+      for (int j = lane; j < S; j += 64) {
+        const float2 m = mrl[j];
+        const float pj = __expf(sc[h * 128 + j] - mx) * inv * m.y;
+        sc[h * 128 + j] = pj;
+        sg = fmaf(pj, m.x, sg);
+      }
+      sg = wave_sum(sg);
+      if (lane == 0) sig[h] = sg;
+    }
+    // z' on MFMA, 32 tokens per round: waves 2r, 2r + 1 put their rows into the stage area, then
+    // start loading their rows of the next sequence
+    float4v zacc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) zacc[t] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < rounds; ++r) {
+      __syncthreads();  // the softmax is done (r = 0) / every wave is past round r - 1's reads
+      const bool mine = (wave >> 1) == r;
+      if (mine) {
+        half_t* dst = ust + (16 * (wave & 1) + c) * LDU + 8 * g;
+#pragma unroll
+        for (int k = 0; k < KD; ++k) *reinterpret_cast<half8*>(dst + 32 * k) = a[k];
+      }
+      __syncthreads();
+      if (PF && mine && nb < B) load_rows(nb);
+      // A = p' (row: head c, k: tokens 32 r + 8 g .. + 7) as fp16 hi + lo
+      half8 ph, pl;
+      {
+        const float4v p0 = *reinterpret_cast<const float4v*>(sc + c * 128 + CF_T * r + 8 * g);
+        const float4v p1 = *reinterpret_cast<const float4v*>(sc + c * 128 + CF_T * r + 8 * g + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ph[e] = (half_t)p0[e];
+          pl[e] = (half_t)(p0[e] - (float)ph[e]);
+          ph[4 + e] = (half_t)p1[e];
+          pl[4 + e] = (half_t)(p1[e] - (float)ph[4 + e]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = 16 * (wave * NT + t) + c;  // this lane's dim
+        half8 bu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bu[e] = ust[(8 * g + e) * LDU + n];
+        zacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, bu, zacc[t], 0, 0, 0);
+        zacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, bu, zacc[t], 0, 0, 0);
+      }
+    }
+    // waves without a round of their own (S <= 96: no rows, or rounds < 4) load the next rows here
+    if (PF && (wave >> 1) >= rounds && nb < B) load_rows(nb);
+    __syncthreads();  // the stage area becomes z' (hi rows 0 .. H-1, lo rows H .. 2H-1)
+    half_t* zo = ust;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = 16 * (wave * NT + t) + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // zacc[t][q] = z'[head 4 g + q][dim n]
+        const int h = 4 * g + q;
+        if (h < H) {
+          const float v = zacc[t][q] - sig[h];
+          const half_t hi = (half_t)v;
+          zo[h * D + n] = hi;
+          zo[(H + h) * D + n] = (half_t)(v - (float)hi);
+        }
+      }
+    }
+    __syncthreads();
+    half_t* zb = z + (int64_t)b * 2 * H * D;
+    for (int i = tid; i < 2 * H * NCH; i += 512)
+      *reinterpret_cast<half8*>(zb + 8 * i) = *reinterpret_cast<const half8*>(zo + 8 * i);
+    __syncthreads();  // every wave is done with zo, wl, sc, mrl before the next sequence's prologue
+  }
+}
+
 // Block-diagonal weights of the K/V-free last layer from the folded QKV weight W' [3D x D]:
 //   wk_bd [H*D x D]: row h*D + i, column k = W'_k[k][i] for k in head h, else 0
 //   wv_bd [D x 2*H*D]: row n, column c*H*D + h*D + i (c = 0, 1: the z' hi / lo halves)
@@ -654,6 +826,19 @@ void launch_cls_attn_fold(const half_t* w, const half_t* U, const float* mr, con
   ProfScope prof("cls_attn_fold", s, 4.0 * B * (double)S * D * H,
                  2.0 * 2.0 * B * (double)S * D + 2.0 * 2.0 * B * (double)H * D);
   const float scale = 0.125f;  // 1 / sqrt(64)
+  // the single-read form for S <= 128 (SR_CLS_FOLD_1READ=0: the two-pass form; read per launch)
+  const char* e1 = std::getenv("SR_CLS_FOLD_1READ");
+  if (S <= 128 && !(e1 && e1[0] == '0')) {
+    const unsigned grid = (unsigned)std::min(B, 256);  // one workgroup per CU (registers), persistent
+    if (D == 768)
+      hipLaunchKernelGGL((cls_attn_fold1_kernel<768, 12>), dim3(grid), dim3(512), 0, s, w, U, mr, mask, B,
+                         S, H, scale, z);
+    else
+      hipLaunchKernelGGL((cls_attn_fold1_kernel<1024, 16>), dim3(grid), dim3(512), 0, s, w, U, mr, mask, B,
+                         S, H, scale, z);
+    SR_LAUNCH_CHECK();
+    return;
+  }
   if (D == 768)
     hipLaunchKernelGGL((cls_attn_fold_kernel<768, 12>), dim3((unsigned)B), dim3(512), 0, s, w, U, mr,
                        mask, S, H, scale, z);

@@ -328,9 +328,10 @@ def test_fp8_ffn_persistent_tiles():
     assert np.abs(got8 - ref8).max() <= 8e-3 * (1.0 + np.abs(ref8).max())
 
 
-@pytest.mark.parametrize("S,L,d,H", [(16, 2, 768, 12), (64, 3, 768, 12), (128, 2, 768, 12),
-                                     (512, 2, 768, 12), (64, 2, 1024, 16)])
-def test_kvfree_cls_last_layer(S, L, d, H, monkeypatch):
+@pytest.mark.parametrize("S,L,d,H,nb", [(16, 2, 768, 12, 40), (64, 3, 768, 12, 40), (128, 2, 768, 12, 40),
+                                        (512, 2, 768, 12, 12), (64, 2, 1024, 16, 40),
+                                        (128, 2, 768, 12, 600), (96, 2, 1024, 16, 300)])
+def test_kvfree_cls_last_layer(S, L, d, H, nb, monkeypatch):
     # K/V-free CLS-only last layer (cls_attn_fold): with LN folded the CLS query's scores are
     # rstd_j (w_h . u_j - mu_j sum w_h) with w_h = W'_{k,h}^T q_h and its context W'_v z' + d_v, so
     # no token is projected to K / V.  Ragged masks, non-trivial LayerNorm affine parameters, the
@@ -347,14 +348,22 @@ def test_kvfree_cls_last_layer(S, L, d, H, monkeypatch):
             w[k] = (0.2 * rng.standard_normal(w[k].shape)).astype(np.float32)
     w["classifier.out_proj.weight"] *= 20.0
     enc = Encoder(spec, weights=w)
-    ids, mask = _batch(spec, 40 if S < 512 else 12, S, seed=7 + S, ragged=True)
+    # nb > 256: the single-read kernel's persistent workgroups take several sequences each
+    ids, mask = _batch(spec, nb, S, seed=7 + S, ragged=True)
     got = enc.cross_score(ids, mask)[:, 0]
+    # S <= 128 takes the single-read kernel (u once from HBM, z' on MFMA); the two-pass form too
+    monkeypatch.setenv("SR_CLS_FOLD_1READ", "0")
+    two = enc.cross_score(ids, mask)[:, 0]
+    monkeypatch.delenv("SR_CLS_FOLD_1READ")
     monkeypatch.setenv("SR_KVFREE_CLS", "0")
     kv = enc.cross_score(ids, mask)[:, 0]
     ref = R.cross_logits(_ref_cfg(spec), w, ids, mask)[:, 0]
     tol = 1e-2 * (1.0 + np.abs(ref).max())
     assert np.abs(got - ref).max() <= tol
+    assert np.abs(two - ref).max() <= tol
     assert np.abs(kv - ref).max() <= tol
+    # single-read vs two-pass: z' in fp32 either way (MFMA with p' as fp16 hi + lo vs VALU)
+    assert np.abs(got - two).max() <= 2e-3 * (1.0 + np.abs(ref).max())
     # the two paths differ only by where fp16 rounding happens (K / V vs w / z')
     assert np.abs(got - kv).max() <= tol
     assert not np.array_equal(got, kv)
