@@ -617,10 +617,16 @@ __global__ __launch_bounds__(512) void cls_attn_fold_kernel(const half_t* __rest
 
 // Single-read form (S <= 128): the score phase keeps each wave's 16 token rows of u in registers
 // (its MFMA A fragments, 16 tokens x D); after the softmax the rows go through LDS 32 tokens at a
-// time ([token][D + 4] halfs: the 4 k-groups of a B fragment land on distinct banks) and
-// z'[16 heads x D] = p' . u runs on MFMA (A = p' as an fp16 hi + lo pair, so z' keeps fp32-like
-// precision; B = 8 tokens of one dim per lane).  u is read from HBM once (the two-pass form reads
+// time ([token][D + 16] halfs: the 8 rows of a half-wave's transposed read start 32 bytes apart,
+// one bank slot each) and z'[16 heads x D] = p' . u runs on MFMA (A = p' as an fp16 hi + lo pair,
+// so z' keeps fp32-like precision; B = 8 tokens of one dim per lane by two ds_read_b64_tr_b16, token
+// order 4g + j then 16 + 4g + j, which p' follows).  u is read from HBM once (the two-pass form reads
 // it twice and accumulates z' on VALU with 4-byte loads); z' leaves through LDS as 16-byte stores.
+__device__ __forceinline__ half4 cf_tr_read_b64(const half_t* p) {
+  typedef short short4_t __attribute__((ext_vector_type(4)));
+  const short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
+  return __builtin_bit_cast(half4, v);
+}
 constexpr int CF_T = 32;  // tokens per LDS round
 // persistent: one workgroup per CU (175 / 239 VGPRs) walks sequences b, b + grid, ...; a wave
 // loads its rows of the NEXT sequence as soon as its own round has put this sequence's rows into
@@ -632,7 +638,7 @@ __global__ __launch_bounds__(512) void cls_attn_fold1_kernel(const half_t* __res
                                                              const int32_t* __restrict__ mask, int B,
                                                              int S, int H, float scale,
                                                              half_t* __restrict__ z) {
-  constexpr int NCH = D / 8, KD = D / 32, LDU = D + 4;
+  constexpr int NCH = D / 8, KD = D / 32, LDU = D + 16;
   constexpr int NT = D / 16 / 8;  // z' column tiles (16 dims) per wave
   // D = 1024 (128 VGPRs of rows + 32 of z') loads its rows at the top of each sequence instead:
   // the early prefetch spills there
@@ -735,11 +741,11 @@ __global__ __launch_bounds__(512) void cls_attn_fold1_kernel(const half_t* __res
       }
       __syncthreads();
       if (PF && mine && nb < B) load_rows(nb);
-      // A = p' (row: head c, k: tokens 32 r + 8 g .. + 7) as fp16 hi + lo
+      // A = p' (row: head c, k: tokens 32 r + 4 g + j, then 32 r + 16 + 4 g + j) as fp16 hi + lo
       half8 ph, pl;
       {
-        const float4v p0 = *reinterpret_cast<const float4v*>(sc + c * 128 + CF_T * r + 8 * g);
-        const float4v p1 = *reinterpret_cast<const float4v*>(sc + c * 128 + CF_T * r + 8 * g + 4);
+        const float4v p0 = *reinterpret_cast<const float4v*>(sc + c * 128 + CF_T * r + 4 * g);
+        const float4v p1 = *reinterpret_cast<const float4v*>(sc + c * 128 + CF_T * r + 16 + 4 * g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           ph[e] = (half_t)p0[e];
@@ -748,12 +754,15 @@ __global__ __launch_bounds__(512) void cls_attn_fold1_kernel(const half_t* __res
           pl[4 + e] = (half_t)(p1[e] - (float)ph[4 + e]);
         }
       }
+      // B = u tokens (as ph) x dims 16 (wave NT + t) ..: lane 4q + pp of group g addresses token
+      // 4 g + q (16 + 4 g + q), dims + 4 pp .. + 3; the transposed read hands lane c its dim's 4 tokens
+      const int q = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const int n = 16 * (wave * NT + t) + c;  // this lane's dim
-        half8 bu;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bu[e] = ust[(8 * g + e) * LDU + n];
+        const half_t* col = ust + 16 * (wave * NT + t) + 4 * pp;
+        const half4 lo = cf_tr_read_b64(col + (4 * g + q) * LDU);
+        const half4 hi = cf_tr_read_b64(col + (16 + 4 * g + q) * LDU);
+        const half8 bu = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         zacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, bu, zacc[t], 0, 0, 0);
         zacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, bu, zacc[t], 0, 0, 0);
       }
