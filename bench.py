@@ -180,6 +180,8 @@ def main():
         if dist.get_world_size() != world:
             sys.exit(f"bench: backend world_size {dist.get_world_size()} != WORLD_SIZE {world}")
 
+    comm = comm_record(dist, world, a.dist_backend)
+
     from super_rag_amd import _native as N
     from super_rag_amd.encoder import MODELS, Encoder, random_weights
     from super_rag_amd.pipeline import SearchPipeline
@@ -342,14 +344,7 @@ def main():
                  "per_launch": (f"{dom['flops'] / dom['launches']:.4g} FLOP" if roof["bound"] == "mfma"
                                 else f"{dom['bytes'] / dom['launches']:.4g} B"),
                  "algorithmic_B_per_launch": round(dom["bytes"] / dom["launches"])})
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(dom_name)
-    pmc = pmc_record(dom_name)
-    if pmc and pmc.get("clock_ghz") and roof["bound"] == "mfma":
-        # the clock the chip holds under this MFMA load (DVFS) and the matrix-pipe utilisation
-        # measured by the PMC pass: frac of the spec peak vs of the peak at the held clock
-        roof["pmc_clock_ghz"] = pmc["clock_ghz"]
-        roof["pmc_mfma_util"] = pmc.get("mfma_util")
-        roof["peak_at_held_clock"] = round(roof["peak"] * pmc["clock_ghz"] / 2.4, 1)
+    apply_pmc(roof, dom_name, prof.keys())
     step_ms = dt / a.steps * 1e3
     kern = {k: {"ms_per_step": round(v["total_ms"] / a.steps, 3), "launches": v["launches"],
                 ("tflops" if v["flops"] > 0 else "gbs"):
@@ -362,7 +357,8 @@ def main():
         search_roof = {"bound": "hbm", "achieved": round(sb / (sm * 1e-3) / 1e9, 1),
                        "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
-        search_roof["traffic"], search_roof["traffic_source"] = pmc_traffic("cosine_scan")
+        apply_pmc(search_roof, "cosine_scan", prof.keys())
+        search_roof.pop("pmc_provenance", None)  # (the same record as roofline's)
         # at B = 256 the scan's intensity (2 B flop per row byte) sits at the ridge: its ceiling is
         # the slower of the HBM time and the MFMA time at spec peak
         mfma_s = sum(v["flops"] / ((PEAK_F8_TFLOPS if k.startswith("cosine_scan8") else PEAK_F16_TFLOPS) * 1e12)
@@ -400,7 +396,8 @@ def main():
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
                    "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
                    "parallelism": f"corpus row-shard x{world}, query DP x{world}",
-                   "passages": "sharded (C3 fetch)" if shard_p else "replicated"},
+                   "passages": "sharded (C3 fetch)" if shard_p else "replicated",
+                   "comm": comm},
         "recall_at_10": recall,
         **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
         "rerank_fidelity": fidelity,
@@ -417,6 +414,22 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def comm_record(dist, world, backend):
+    """The communicator as the ranks see it (config.comm of the JSON line): the process group's
+    backend and world size as torch.distributed reports them (None / 1 without a group at N = 1)
+    and the RCCL version torch links (torch.cuda.nccl.version(): RCCL on ROCm)."""
+    try:
+        ver = torch.cuda.nccl.version()
+        rccl = ".".join(str(x) for x in ver) if isinstance(ver, tuple) else str(ver)
+    except Exception as e:  # noqa: BLE001 - reported, not fatal
+        rccl = f"unavailable ({type(e).__name__})"
+    init = dist.is_available() and dist.is_initialized()
+    return {"backend": dist.get_backend() if init else None,
+            "world_size": dist.get_world_size() if init else 1,
+            "launched_world_size": world, "requested_backend": backend if world > 1 else None,
+            "rccl_version": rccl}
 
 
 def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
@@ -556,31 +569,99 @@ def measured_peaks(dev):
     return out
 
 
-def pmc_record(kernel):
-    """The kernel's record in the newest committed PMC summary (tools/pmc_traffic.py), or None."""
+def source_fingerprint(root=ROOT):
+    """sha256 over the native sources (super-rag_amd/csrc/*, include/*.h) in name order: names the
+    kernel code a PMC summary was collected on (tools/profile_round.sh writes it beside the passes)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(root, "super-rag_amd", "csrc", "*")) +
+                   glob.glob(os.path.join(root, "include", "*.h")))
+    for fn in files:
+        if os.path.isfile(fn):
+            h.update(os.path.relpath(fn, root).encode())
+            with open(fn, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
+
+
+def pmc_file(root=ROOT):
+    """(relative path, parsed summary) of the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, tools/pmc_traffic.py), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(root, "profiles", "*_pmc_traffic.json")))
     if not files:
-        return None
+        return None, None
     with open(files[-1]) as f:
-        return json.load(f)["kernels"].get(kernel)
+        return os.path.relpath(files[-1], root), json.load(f)
 
 
-def pmc_traffic(kernel):
+def pmc_provenance(run_kernels, root=ROOT):
+    """Which PMC summary the roofline's `traffic` / `pmc_*` fields come from and whether it
+    describes THIS run: the summary's commit and native-source fingerprint (recorded on the box by
+    tools/profile_round.sh) against the running tree's, and its kernel set against the kernels
+    timed here.  stale = the sources differ, or the kernel sets differ (another workload / precision
+    mode, or kernels added or removed since): the counters then describe other code, so the
+    roofline reports traffic null and keeps the stale numbers beside it."""
+    path, d = pmc_file(root)
+    if d is None:
+        return None
+    mine = set(run_kernels)
+    theirs = set(d.get("kernels", {}))
+    fp = d.get("source_sha256")
+    src_match = None if fp is None else fp == source_fingerprint(root)
+    reasons = []
+    if src_match is False:
+        reasons.append("native sources differ from the profiled tree")
+    if mine != theirs:
+        reasons.append(f"kernel sets differ (only here: {sorted(mine - theirs)}, only in the "
+                       f"summary: {sorted(theirs - mine)})")
+    return {"file": path, "commit": d.get("commit"), "source_sha256": fp,
+            "source_match": src_match, "kernel_set_match": mine == theirs,
+            "stale": bool(reasons), "stale_reasons": reasons}
+
+
+def pmc_record(kernel, root=ROOT):
+    """The kernel's record in the newest committed PMC summary (tools/pmc_traffic.py), or None."""
+    _, d = pmc_file(root)
+    return None if d is None else d["kernels"].get(kernel)
+
+
+def pmc_traffic(kernel, root=ROOT):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes over this same bench command, gfx950 fetch correction applied).
     Counters cannot be read live inside the timed region, so the value is the profiled run's."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
+    path, d = pmc_file(root)
+    if d is None:
         return None, None
-    with open(files[-1]) as f:
-        k = json.load(f)["kernels"].get(kernel)
+    k = d["kernels"].get(kernel)
     if not k:
         return None, None
-    return k["traffic_B"], (f"{os.path.relpath(files[-1], ROOT)}: fetch {k['fetch_B']} B + write "
+    return k["traffic_B"], (f"{path}: fetch {k['fetch_B']} B + write "
                             f"{k['write_B']} B per launch (mean over {k['launches']} launches)")
+
+
+def apply_pmc(roof, kernel, run_kernels, root=ROOT):
+    """Fill roof["traffic"] (+ pmc clock / utilisation) from the PMC summary, with its provenance;
+    a stale summary's numbers move to roof["stale_pmc"] and traffic stays null."""
+    traffic, src = pmc_traffic(kernel, root)
+    rec = pmc_record(kernel, root)
+    prov = pmc_provenance(run_kernels, root)
+    roof["pmc_provenance"] = prov
+    fields = {"traffic": traffic, "traffic_source": src}
+    if rec and rec.get("clock_ghz") and roof.get("bound") == "mfma":
+        # the clock the chip holds under this MFMA load (DVFS) and the matrix-pipe utilisation
+        # measured by the PMC pass: frac of the spec peak vs of the peak at the held clock
+        fields["pmc_clock_ghz"] = rec["clock_ghz"]
+        fields["pmc_mfma_util"] = rec.get("mfma_util")
+        fields["peak_at_held_clock"] = round(roof["peak"] * rec["clock_ghz"] / 2.4, 1)
+    if prov and prov["stale"]:
+        roof["traffic"] = None
+        roof["stale_pmc"] = fields
+    else:
+        roof.update(fields)
+    return roof
 
 
 def cpu_cores() -> int:

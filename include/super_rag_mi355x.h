@@ -341,6 +341,16 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, int device,
                  void* stream);
 
+/* Diagnostic: the LayerNorm-folded FFN1 GEMM Y = 2 GELU(rstd_m (X W^T - mu_m colsum) + bias) on
+ * device buffers (the cross-encoders' FFN1 epilogue), fp16 (f8 = 0: X M x K, W N x K fp16, Y fp16)
+ * or fp8 (f8 = 1: X, W OCP e4m3 bytes, wexp the E8M0 exponent byte of each W row, Y e4m3 bytes);
+ * mr = (mu, rstd) per X row, colsum / bias N fp32.  diag: 0 the product kernel, 2 the main loop
+ * without an epilogue, 5 the epilogue math without its stores, 6 the stores of the raw
+ * accumulators without the math (2 / 5 / 6: timing only, wrong results). */
+int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
+                 const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
+                 int N, int K, int device, void* stream);
+
 /* Diagnostic: device-to-device copy of `bytes` (multiple of 16) with 16-byte lanes, the HBM
  * yardstick bench.py reports beside the spec peak (no reference counterpart). */
 int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream);

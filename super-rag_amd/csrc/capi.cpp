@@ -800,6 +800,23 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
   SR_API_END
 }
 
+int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
+                 const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
+                 int N, int K, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(colsum);
+  SR_NONNULL(mr);
+  SR_NONNULL(Y);
+  SR_CHECK(!f8 || wexp, "diag_ffn1: fp8 needs wexp");
+  sr::DeviceGuard g(device);
+  sr::launch_ffn1_diag(diag, f8 != 0, X, lda, W, wexp, bias, colsum, mr, Y, ldy, M, N, K,
+                       reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
 int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream) {
   SR_API_BEGIN
   SR_NONNULL(src);

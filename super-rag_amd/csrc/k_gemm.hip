@@ -38,6 +38,13 @@
                               // constant loads (A/B build; measured -0.3 % end to end,
                               // profiles/r03_gemm_epilogue_ab/)
 #endif
+#ifndef SR_GEMM_PERMW
+#define SR_GEMM_PERMW 1  // wide epilogues: W rows staged in the perm32 order, no permlane16_swap
+#endif
+#ifndef SR_GEMM_GELU_V2
+#define SR_GEMM_GELU_V2 1  // FFN1 epilogues: 2 GELU(x) = x * T(x), T = erfc(-x / sqrt 2) from a
+                           // 2049-entry LDS table over [-4 sqrt 2, 4 sqrt 2] (0: gelu2_lut)
+#endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
@@ -181,6 +188,43 @@ __device__ __forceinline__ void gelu_tab_init(float2* __restrict__ tab, int tid,
   }
 }
 
+// 2 GELU(x) = x * T(x), T(x) = 1 + erf(x / sqrt 2) = erfc(-x / sqrt 2), linearly interpolated
+// from an LDS table of GELU_NT + 1 nodes x_i = -XMAX + i h over [-XMAX, XMAX] (XMAX = 4 sqrt 2,
+// h = 2 XMAX / GELU_NT; entries (T(x_i), T(x_i+1) - T(x_i))); x outside the range takes the end
+// nodes (T(-XMAX) = 1.5e-8, T(XMAX) = 2 - 1.5e-8).  |T error| <= h^2 / 8 max|T''| = 1.9e-6.  Per
+// element: v_fma + v_med3 (index space, clamped), v_cvt_u32 + v_fract, one address op, one
+// ds_read_b64, v_fma + v_mul: 7 VALU against gelu2_lut's 9-10 (and no abs / sign handling).
+constexpr int GELU_NT = 2048;
+constexpr float GELU_XMAX = 5.6568542494923802f;  // 4 sqrt 2
+// (index space through [0, 1] (the clamp modifier) and an exact ldexp)
+__device__ __forceinline__ float gelu2_t(float x, const float2* __restrict__ tab) {
+  static_assert(GELU_NT == 2048, "ldexp by 11");
+  const float zc = __builtin_amdgcn_fmed3f(fmaf(x, 1.0f / (2.0f * GELU_XMAX), 0.5f), 0.0f, 1.0f);
+  const float az = __builtin_amdgcn_ldexpf(zc, 11);
+  const float2 t = tab[(uint32_t)az];
+  return x * fmaf(__builtin_amdgcn_fractf(az), t.y, t.x);
+}
+__device__ __forceinline__ void gelu_t_tab_init(float2* __restrict__ tab, int tid, int nthreads) {
+  constexpr float h = 2.0f * GELU_XMAX / (float)GELU_NT;
+  for (int i = tid; i <= GELU_NT; i += nthreads) {
+    const double x0 = -(double)GELU_XMAX + (double)i * (double)h;
+    const float t0 = (float)erfc(-x0 * 0.70710678118654752);
+    const float t1 = i < GELU_NT ? (float)erfc(-(x0 + (double)h) * 0.70710678118654752) : t0;
+    tab[i] = make_float2(t0, t1 - t0);
+  }
+}
+
+// W-row order of the wide epilogues (PERMW): inside each 32-row block, LDS row k holds W row
+// perm32(k), so that MFMA tile 2p's rows 4g .. 4g+3 (lane group g) and tile 2p+1's rows 4g ..
+// 4g+3 are the 8 CONSECUTIVE output columns 32p + 16(g & 1) + 4(g & 2) + 0..7 -- the layout the
+// permlane16_swap exchange used to build (one swap per two outputs, no longer issued).
+__device__ __forceinline__ int perm32(int k) {
+  const int h = k >> 4, g = (k >> 2) & 3, r = k & 3;
+  return 16 * (g & 1) + 4 * (g & 2) + 4 * h + r;
+}
+// the piece-dependent (uniform) part of perm32 for staging piece i (rows 8i + lane / 8 of a band)
+__host__ __device__ constexpr int perm_row_off(int i) { return 32 * (i >> 2) + 8 * (i & 1) + 4 * ((i >> 1) & 1); }
+
 __device__ __forceinline__ f2v gelu_erf2(f2v x) {
   const f2v z = __builtin_elementwise_abs(x) * splat2(0.70710678118654752f);
   const f2v d = pk_fma(splat2(0.3275911f), z, splat2(1.0f));
@@ -317,7 +361,8 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
 // statistics) are issued: the persistent kernel stages the next tile's first K-steps there, so
 // those loads are older than the staging pieces and their wait (vmcnt counts in order) does not
 // also wait for the staging.
-template <int EPI, bool CHECK, bool LINE_ST = false, bool GLUT = false, class Pre = NoPre>
+template <int EPI, bool CHECK, bool LINE_ST = false, bool GLUT = false, bool PERM = false,
+          class Pre = NoPre>
 __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, int mw0, int lane,
                                                 int M, int N, const float* __restrict__ bias,
                                                 const void* __restrict__ R, int64_t ldr,
@@ -409,6 +454,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     for (int p = 0; p < 4; ++p) {
       // columns nb .. nb+7 as 4 packed pairs: x[q] = (col 2q, col 2q + 1)
       f2v x[4];
+      if constexpr (PERM) {  // W rows staged in perm32 order: the lane's 8 columns as they are
+        x[0] = f2v{acc[2 * p][j][0], acc[2 * p][j][1]};
+        x[1] = f2v{acc[2 * p][j][2], acc[2 * p][j][3]};
+        x[2] = f2v{acc[2 * p + 1][j][0], acc[2 * p + 1][j][1]};
+        x[3] = f2v{acc[2 * p + 1][j][2], acc[2 * p + 1][j][3]};
+      } else {
 #pragma unroll
       for (int r = 0; r < 4; r += 2) {
         const auto s0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
@@ -417,6 +468,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
                                                          __float_as_uint(acc[2 * p + 1][j][r + 1]), false, false);
         x[r / 2] = f2v{__uint_as_float(s0[0]), __uint_as_float(s1[0])};
         x[2 + r / 2] = f2v{__uint_as_float(s0[1]), __uint_as_float(s1[1])};
+      }
       }
       const f2v bb[4] = {b0[p].xy, b0[p].zw, b1[p].xy, b1[p].zw};
       if constexpr (LNF) {
@@ -447,7 +499,9 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       if constexpr (GELU2) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if constexpr (GLUT)
+          if constexpr (GLUT && SR_GEMM_GELU_V2)
+            x[q] = f2v{gelu2_t(x[q].x, gtab), gelu2_t(x[q].y, gtab)};
+          else if constexpr (GLUT)
             x[q] = gelu2_lut2(x[q], gtab);
           else
             x[q] = gelu2_erf2(x[q]);
@@ -487,10 +541,15 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
-                                                         __float_as_uint(acc[2 * p + 1][j][r]), false, false);
-        v[r] = __uint_as_float(sw[0]);
-        v[4 + r] = __uint_as_float(sw[1]);
+        if constexpr (PERM) {
+          v[r] = acc[2 * p][j][r];
+          v[4 + r] = acc[2 * p + 1][j][r];
+        } else {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                           __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
       }
       if constexpr (LNF) {
 #pragma unroll
@@ -523,7 +582,9 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       if constexpr (GELU2) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          if constexpr (GLUT)
+          if constexpr (GLUT && SR_GEMM_GELU_V2)
+            v[r] = gelu2_t(v[r], gtab);
+          else if constexpr (GLUT)
             v[r] = gelu2_lut(v[r], gtab);
           else
             v[r] = gelu2_erf(v[r]);
@@ -605,6 +666,117 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   }
 }
 
+// The LayerNorm-folded FFN1 epilogues (EPI_LNF_GELU_F16 / _F8) column-group outer: the bias and
+// column sums of ONE 8-column group p live at a time (16 VGPRs, the next group's loaded while this
+// one is processed) instead of all four (64 VGPRs), which left no room for the 2 GELU(x) = x T(x)
+// table form without spilling the K-loop's LDS bases.  Same outputs, same stores (16 per wave),
+// in (p, j) instead of (j, p) order.
+// DMODE (timing diagnostics, wrong results): 5 = the math without the stores, 6 = the stores of the
+// raw accumulators without the math.
+template <int EPI, bool CHECK, bool PERM, class Pre = NoPre, int DMODE = 0>
+__device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, int mw0, int lane,
+                                                int M, const float* __restrict__ bias,
+                                                void* __restrict__ Y, int64_t ldy, const LnFold& lf,
+                                                const float2* __restrict__ gtab, const Pre& pre = Pre{}) {
+  constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;
+  static_assert(EPI == EPI_LNF_GELU_F16 || OUT8, "store_tile_gelu: LN-folded FFN1 epilogues");
+  const int g = lane >> 4, odd = g & 1;
+  const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
+  float2 mrj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int m = mw0 + j * 16 + (lane & 15);
+    m = (CHECK && m >= M) ? M - 1 : m;
+    mrj[j] = *reinterpret_cast<const float2*>(lf.mr + (int64_t)m * lf.stat_ld * 2);
+  }
+  float4v bc[2][4];  // [buffer][b0, b1, c0, c1] of column group p
+  auto load_consts = [&](float4v (&d)[4], int p) __attribute__((always_inline)) {
+    d[0] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p);
+    d[1] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p + 4);
+    d[2] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p);
+    d[3] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p + 4);
+  };
+  load_consts(bc[0], 0);
+  if constexpr (!std::is_same<Pre, NoPre>::value) {
+    __builtin_amdgcn_sched_barrier(0);
+    pre();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (p < 3) load_consts(bc[(p + 1) & 1], p + 1);
+    const float4v(&cst)[4] = bc[p & 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = mw0 + j * 16 + (lane & 15);
+      if (CHECK && m >= M) continue;
+      const float mu = mrj[j].x, rstd = mrj[j].y;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (PERM) {
+          v[r] = acc[2 * p][j][r];
+          v[4 + r] = acc[2 * p + 1][j][r];
+        } else {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                           __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
+      }
+      // (each value through an empty asm: kept scalar -- SLP packing it into v_pk_fma_f32 cost
+      // two v_mov per packed pair here, and packed f32 VALU issues no faster than two scalar ops)
+      if constexpr (DMODE != 6) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = fmaf(rstd, fmaf(-mu, cst[2][r], v[r]), cst[0][r]);
+        v[4 + r] = fmaf(rstd, fmaf(-mu, cst[3][r], v[4 + r]), cst[1][r]);
+        asm("" : "+v"(v[r]));
+        asm("" : "+v"(v[4 + r]));
+      }
+      // the 8 table reads issued together, consumed after a scheduling fence (left to the
+      // scheduler, each read was awaited right behind its own issue)
+      float fr[8];
+      float2 tv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float az = __builtin_amdgcn_ldexpf(
+            __builtin_amdgcn_fmed3f(fmaf(v[r], 1.0f / (2.0f * GELU_XMAX), 0.5f), 0.0f, 1.0f), 11);
+        fr[r] = __builtin_amdgcn_fractf(az);
+        tv[r] = gtab[(uint32_t)az];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v[r] *= fmaf(fr[r], tv[r].y, tv[r].x);
+        // e4m3: 2 GELU >= -0.34, so only the upper saturation bound can apply (e4m3x4's clamp)
+        if constexpr (OUT8) v[r] = fminf(v[r], 448.f);
+        asm("" : "+v"(v[r]));
+      }
+      }  // DMODE != 6
+      if constexpr (DMODE == 5) {
+        float z = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) z += v[r];
+        if (z == 12345.678f) reinterpret_cast<float*>(Y)[lane] = z;
+      } else if constexpr (OUT8) {
+        uint2 q8;
+        q8.x = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
+            v[2], v[3], __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false), true);
+        q8.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
+            v[6], v[7], __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false), true);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+      } else {
+        half8 h;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) h[r] = (half_t)v[r];
+        *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = h;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the next groups' constant loads where they are
+  }
+}
+
 // One epilogue for the pipelined kernels; NSTORE = global store instructions per wave on the
 // unchecked path (the persistent kernel's counted vmcnt relies on it: extra stores, such as the
 // statistics of the *_STATS epilogues, only make its waits stricter).
@@ -612,7 +784,7 @@ template <int EPI>
 struct PipeEpi {
   static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
   static constexpr int NSTORE = WIDE ? 16 : 32;
-  template <bool CHECK, bool LINE = false, bool GLUT = false, class Pre = NoPre>
+  template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
                                              int N, const float* __restrict__ bias,
                                              const void* __restrict__ R, int64_t ldr,
@@ -620,8 +792,10 @@ struct PipeEpi {
                                              half_t* __restrict__ scr = nullptr,
                                              const float2* __restrict__ gtab = nullptr,
                                              const Pre& pre = Pre{}) {
-    if constexpr (WIDE)
-      store_tile_wide<EPI, CHECK, LINE, GLUT, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
+    if constexpr (WIDE && GLUT && SR_GEMM_GELU_V2 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
+      store_tile_gelu<EPI, CHECK, PERM, Pre>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, pre);
+    else if constexpr (WIDE)
+      store_tile_wide<EPI, CHECK, LINE, GLUT, PERM, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
     else
     {
       pre();
@@ -804,9 +978,14 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
                         (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
   // GLUT: the FFN1 epilogues' 8 KiB erf table (gelu2_lut) past the stages / line scratch
-  constexpr bool GLUT = SR_GEMM_GELU_LUT && DIAG == 0 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
+  constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6) &&
+                        (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
+  constexpr int GTAB = SR_GEMM_GELU_V2 ? GELU_NT + 1 : GELU_TAB;  // float2 entries
+  // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
+  // and the 32-bit-output epilogues index the rows as staged)
+  constexpr bool PERMW = SR_GEMM_PERMW && PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (SCAN ? 512 : 0) +
-                                                     (GLUT ? 4 * GELU_TAB : 0)];
+                                                     (GLUT ? 4 * GTAB : 0)];
   float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0));
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
   // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
@@ -864,12 +1043,18 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // swizzle parity p & 1, so a lane keeps 2 offsets per operand.
   const int grp = wave >> 2, w4 = wave & 3;
   (void)w4;
+  // PERMW: piece i of a wave fills LDS rows 8i + (lane >> 3) of its 64-row band, i.e. row
+  // k = 8 (i & 3) + l3 (l3 = lane >> 3) of the band's 32-row block i >> 2, which takes W row
+  // perm32(k) = [16 (l3 >> 2) + (l3 & 3)] + 8 (i & 1) + 4 ((i >> 1) & 1): the lane part stays in
+  // the 2 offsets per operand, the piece part joins the uniform soffset (perm_row_off)
   uint32_t vbw[2], vbx[2];
 #pragma unroll
   for (int par = 0; par < 2; ++par) {
     const int ch = (lane & 7) ^ ((lane >> 4) + 4 * par);
-    vbw[par] = (uint32_t)(((int64_t)(lane >> 3) * K + ch * 8) * 2);
-    vbx[par] = (uint32_t)(((int64_t)(lane >> 3) * lda + ch * 8) * 2);
+    const int l3 = lane >> 3;
+    const int wr = PERMW ? 16 * (l3 >> 2) + (l3 & 3) : l3;
+    vbw[par] = (uint32_t)(((int64_t)wr * K + ch * 8) * 2);
+    vbx[par] = (uint32_t)(((int64_t)l3 * lda + ch * 8) * 2);
   }
   // tile panels: W rows [nn, nn+256) and X rows [mm, min(M, mm+256)) (a lambda may not carry the
   // buffer-resource type through its signature: hipcc then drops the host stubs of this template)
@@ -889,7 +1074,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       asm volatile("" : "+s"(sw));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, SR_LDS(s + (w4 * 8 + i) * 8 * GBK), 16,
                                                vbw[i & 1], sw, 0, 0);
-      sw += 16 * K;
+      // next piece's row offset (bytes = rows x 2K): PERMW rows 0 8 4 12 32 40 36 44
+      if (i < 7) sw += (PERMW ? perm_row_off(i + 1) - perm_row_off(i) : 8) * 2 * K;
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -917,7 +1103,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
                          // barrier publishes it
     for (int q = tid; q < 256; q += blockDim.x) tau_lds[q] = q < M ? bias[q] : INFINITY;
   }
-  if constexpr (GLUT) gelu_tab_init(gtab, tid, blockDim.x);  // published by the prologue's barrier
+  if constexpr (GLUT) {  // published by the prologue's barrier
+    if constexpr (SR_GEMM_GELU_V2)
+      gelu_t_tab_init(gtab, tid, blockDim.x);
+    else
+      gelu_tab_init(gtab, tid, blockDim.x);
+  }
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
     stage(0, lds, m0, n0);
@@ -1079,7 +1270,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       const uint8_t* wexp = lf.wexp;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int n = n0 + arow + 16 * i;
+        const int n = PERMW ? n0 + wn * 128 + 32 * (i >> 1) + 4 * (i & 1) + perm32(lane & 15)
+                            : n0 + arow + 16 * i;
         sa[i] = wexp[n < N ? n : N - 1];
       }
     }
@@ -1116,7 +1308,13 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 
     // (EPI_SCAN issues a data-dependent number of atomics / stores: never counted as pending)
     const bool full = !SCAN && m0 + BM <= M;
-    if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
+    if constexpr (DIAG == 5 || DIAG == 6) {  // FFN1 epilogue without its stores / its math
+      static_assert(GLUT && SR_GEMM_GELU_V2, "DIAG 5 / 6: the FFN1 epilogue");
+      if (full)
+        store_tile_gelu<EPI, false, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab);
+      else
+        store_tile_gelu<EPI, true, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab);
+    } else if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
       const int g = lane >> 4, odd = g & 1;
       const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
 #pragma unroll
@@ -1176,16 +1374,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         }
       };
       if (full)
-        PipeEpi<EPI_OUT>::template run<false, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+        PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                           R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab, pre);
       else
-        PipeEpi<EPI_OUT>::template run<true, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+        PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                          R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab, pre);
     } else if (full) {
-      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                         R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab);
     } else {
-      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                        R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab);
     }
     if (!more) break;
@@ -1609,6 +1807,57 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
     default: break;
   }
 #undef SR_F8_CASE
+  SR_LAUNCH_CHECK();
+}
+
+void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
+                      const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
+                      int M, int N, int K, hipStream_t stream) {
+  SR_CHECK(diag == 0 || diag == 2 || diag == 5 || diag == 6, "ffn1_diag: diag must be 0, 2, 5 or 6");
+  SR_CHECK(N % 256 == 0 && M > 0, "ffn1_diag: N % 256 == 0, M > 0");
+  LnFold lf;
+  lf.mr = mr;
+  lf.colsum = colsum;
+  lf.wexp = wexp;
+  if (diag == 0) {
+    if (f8)
+      launch_gemm_f8w(EPI_LNF_GELU_F8, reinterpret_cast<const uint8_t*>(X), lda,
+                      reinterpret_cast<const uint8_t*>(W), bias, nullptr, 0, Y, ldy, M, N, K, stream, &lf);
+    else
+      launch_gemm(EPI_LNF_GELU_F16, reinterpret_cast<const half_t*>(X), lda,
+                  reinterpret_cast<const half_t*>(W), bias, nullptr, 0, Y, ldy, M, N, K, stream, &lf);
+    return;
+  }
+  SR_CHECK(!f8 || (wexp && K % 128 == 0), "ffn1_diag: fp8 needs wexp, K % 128 == 0");
+  const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
+  const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+  lf.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;  // the product walk
+  ProfScope prof(f8 ? "ffn1_diag_f8" : "ffn1_diag", stream, 2.0 * M * (double)N * K, 0.0);
+  const half_t* x = reinterpret_cast<const half_t*>(X);
+  const half_t* w = reinterpret_cast<const half_t*>(W);
+  const int64_t la = f8 ? lda / 2 : lda;
+  const int kk = f8 ? K / 2 : K;
+#define SR_FD(D)                                                                                  \
+  if (f8)                                                                                         \
+    hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNF_GELU_F8, true, D, true>), grid, block, 0, stream, \
+                       x, la, w, bias, nullptr, 0, Y, ldy, M, N, kk, lf);                        \
+  else                                                                                            \
+    hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNF_GELU_F16, true, D>), grid, block, 0, stream, x,  \
+                       la, w, bias, nullptr, 0, Y, ldy, M, N, kk, lf);
+  if (diag == 2) {
+    SR_FD(2)
+  } else {
+#if SR_GEMM_GELU_V2
+    if (diag == 5) {
+      SR_FD(5)
+    } else {
+      SR_FD(6)
+    }
+#else
+    SR_CHECK(false, "ffn1_diag: diag 5 / 6 need the SR_GEMM_GELU_V2 epilogue");
+#endif
+  }
+#undef SR_FD
   SR_LAUNCH_CHECK();
 }
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 import logging
 import os
 import re
+from collections import OrderedDict
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -67,7 +68,8 @@ def longest_first_arrays(a: int, b: np.ndarray, budget: int):
 
 
 class Tokenizer:
-    def __init__(self, spec, path: str | None = None, synthetic: bool | None = None):
+    def __init__(self, spec, path: str | None = None, synthetic: bool | None = None,
+                 cache_mb: float | None = None):
         from .encoder import ModelAssetsError, synthetic_allowed
         self.spec = spec
         self.max_length = spec.max_length
@@ -91,53 +93,48 @@ class Tokenizer:
                 f"explicit opt-in SUPER_RAG_AMD_SYNTHETIC=1")
         self.synthetic = self._hf is None
         # caches: a search request re-scores passages the collection already holds, so the
-        # content ids of recently seen texts are kept (bounded; halved when full) and the hashing
+        # content ids of recently seen texts are kept -- ONE int32 array per text in an LRU
+        # (a hit moves the text to the young end) bounded by bytes (4 per token + the text's
+        # length), SUPER_RAG_AMD_TOKEN_CACHE_MB (default 64 MiB per tokenizer) -- and the hashing
         # tokenizer memoises its word ids
-        self._cache: dict = {}
-        self._cache_np: dict = {}
-        self._cache_cap = 1 << 18
+        self._cache: "OrderedDict[str, np.ndarray]" = OrderedDict()
+        self._cache_bytes = 0
+        self._cache_cap_bytes = int(float(os.environ.get("SUPER_RAG_AMD_TOKEN_CACHE_MB", "64")) * (1 << 20)) \
+            if cache_mb is None else int(cache_mb * (1 << 20))
         self._words: dict = {}
 
     # -- content tokens (no specials) -------------------------------------------------------------
+    def _lookup(self, text: str):
+        a = self._cache.get(text)
+        if a is not None:
+            self._cache.move_to_end(text)
+        return a
+
     def content_ids(self, text: str) -> List[int]:
-        hit = self._cache.get(text)
-        if hit is not None:
-            return hit
-        if self._hf is not None:
-            ids = list(self._hf.encode(text, add_special_tokens=False).ids)
-        else:
-            ids = [self._word_id(w) for w in _WORD.findall(text)]
-        self._remember(text, ids)
-        return ids
+        return self._content_arrays_many([text])[0].tolist()
 
     def content_ids_many(self, texts: Sequence[str]) -> List[List[int]]:
         """content_ids of many texts; the misses of an HF tokenizer go through one encode_batch
         (the Rust tokenizer, parallel) instead of one call each."""
-        out: List = [self._cache.get(t) for t in texts]
-        miss = [i for i, o in enumerate(out) if o is None]
-        if miss and self._hf is not None and len(miss) > 1:
-            enc = self._hf.encode_batch([texts[i] for i in miss], add_special_tokens=False)
-            for i, e in zip(miss, enc):
-                out[i] = list(e.ids)
-                self._remember(texts[i], out[i])
-        else:
-            for i in miss:
-                out[i] = self.content_ids(texts[i])
-        return out
+        return [a.tolist() for a in self._content_arrays_many(texts)]
 
     def _content_arrays_many(self, texts: Sequence[str]) -> List[np.ndarray]:
-        """content_ids_many as int32 arrays (kept beside the list cache, same eviction)."""
-        out: List = [self._cache_np.get(t) for t in texts]
+        """Content ids of many texts as int32 arrays (the cached form; do not modify them)."""
+        out: List = [self._lookup(t) for t in texts]
         miss = [i for i, o in enumerate(out) if o is None]
-        if miss:
-            ids = self.content_ids_many([texts[i] for i in miss])
-            if len(self._cache_np) >= self._cache_cap:
-                for k in list(self._cache_np)[: self._cache_cap // 2]:
-                    self._cache_np.pop(k, None)
-            for i, c in zip(miss, ids):
-                a = np.asarray(c, dtype=np.int32)
-                out[i] = a
-                self._cache_np[texts[i]] = a
+        if not miss:
+            return out
+        if self._hf is not None and len(miss) > 1:
+            enc = self._hf.encode_batch([texts[i] for i in miss], add_special_tokens=False)
+            ids = [e.ids for e in enc]
+        elif self._hf is not None:
+            ids = [self._hf.encode(texts[miss[0]], add_special_tokens=False).ids]
+        else:
+            ids = [[self._word_id(w) for w in _WORD.findall(texts[i])] for i in miss]
+        for i, c in zip(miss, ids):
+            a = np.asarray(c, dtype=np.int32)
+            out[i] = a
+            self._remember(texts[i], a)
         return out
 
     def _word_id(self, w: str) -> int:
@@ -148,20 +145,27 @@ class Tokenizer:
                 self._words[w] = i
         return i
 
-    def _remember(self, text: str, ids: List[int]) -> None:
-        if len(self._cache) >= self._cache_cap:
-            for k in list(self._cache)[: self._cache_cap // 2]:   # drop the older half
-                self._cache.pop(k, None)
+    def _remember(self, text: str, ids: np.ndarray) -> None:
+        cost = 4 * int(ids.size) + len(text) + 64
+        if cost > self._cache_cap_bytes:
+            return
+        old = self._cache.pop(text, None)
+        if old is not None:
+            self._cache_bytes -= 4 * int(old.size) + len(text) + 64
+        while self._cache and self._cache_bytes + cost > self._cache_cap_bytes:
+            k, v = self._cache.popitem(last=False)            # least recently used first
+            self._cache_bytes -= 4 * int(v.size) + len(k) + 64
         self._cache[text] = ids
+        self._cache_bytes += cost
 
     def content_batch(self, texts: Sequence[str], max_len: int) -> Tuple[np.ndarray, np.ndarray]:
         """[N, max_len] int32 content tokens (truncated, zero padded) and [N] lengths."""
         out = np.zeros((len(texts), max_len), dtype=np.int32)
         lens = np.zeros(len(texts), dtype=np.int32)
-        for i, t in enumerate(texts):
-            ids = self.content_ids(t)[:max_len]
-            out[i, : len(ids)] = ids
-            lens[i] = len(ids)
+        for i, a in enumerate(self._content_arrays_many(texts)):
+            ids = a[:max_len]
+            out[i, : ids.size] = ids
+            lens[i] = ids.size
         return out, lens
 
     # -- single sequences: [CLS] text [SEP] / <s> text </s> ---------------------------------------

@@ -1,0 +1,81 @@
+"""CPU tests of bench.py's PMC provenance: the roofline's traffic / pmc fields
+name the summary file, its commit and source fingerprint, and go stale -- traffic null, the old
+numbers kept beside it -- when the summary's kernel set or native sources differ from this run's."""
+import json
+import os
+import shutil
+
+import pytest
+
+import bench
+
+
+def _tree(tmp_path, kernels, sha):
+    root = tmp_path / "repo"
+    for d in ("profiles", "super-rag_amd/csrc", "include"):
+        (root / d).mkdir(parents=True)
+    (root / "super-rag_amd/csrc/k.hip").write_text("kernel v1\n")
+    (root / "include/a.h").write_text("int f(void);\n")
+    summary = {"source": "gpurun_out/prof_x", "commit": "abc123", "method": "test",
+               "source_sha256": sha,
+               "kernels": {k: {"launches": 4, "fetch_B": 100, "write_B": 20, "traffic_B": 120,
+                               "clock_ghz": 1.8, "mfma_util": 0.5} for k in kernels}}
+    (root / "profiles/r99_pmc_traffic.json").write_text(json.dumps(summary))
+    return str(root)
+
+
+def test_fresh_summary_fills_traffic(tmp_path):
+    root = _tree(tmp_path, ["gemm_a", "scan"], None)
+    sha = bench.source_fingerprint(root)
+    with open(os.path.join(root, "profiles/r99_pmc_traffic.json")) as f:
+        d = json.load(f)
+    d["source_sha256"] = sha
+    with open(os.path.join(root, "profiles/r99_pmc_traffic.json"), "w") as f:
+        json.dump(d, f)
+    roof = {"bound": "mfma", "peak": 2500.0}
+    bench.apply_pmc(roof, "gemm_a", ["gemm_a", "scan"], root)
+    assert roof["traffic"] == 120
+    assert roof["pmc_provenance"]["stale"] is False
+    assert roof["pmc_provenance"]["file"] == os.path.join("profiles", "r99_pmc_traffic.json")
+    assert roof["pmc_provenance"]["commit"] == "abc123"
+    assert roof["pmc_clock_ghz"] == 1.8 and "stale_pmc" not in roof
+
+
+def test_kernel_set_difference_marks_stale(tmp_path):
+    root = _tree(tmp_path, ["gemm_a", "scan"], None)
+    roof = {"bound": "mfma", "peak": 2500.0}
+    bench.apply_pmc(roof, "gemm_a", ["gemm_a", "scan", "gemm_new"], root)
+    prov = roof["pmc_provenance"]
+    assert prov["stale"] and not prov["kernel_set_match"]
+    assert "gemm_new" in prov["stale_reasons"][0]
+    assert roof["traffic"] is None and roof["stale_pmc"]["traffic"] == 120
+    assert "pmc_clock_ghz" not in roof
+
+
+def test_source_change_marks_stale(tmp_path):
+    root = _tree(tmp_path, ["gemm_a"], None)
+    sha = bench.source_fingerprint(root)
+    with open(os.path.join(root, "profiles/r99_pmc_traffic.json")) as f:
+        d = json.load(f)
+    d["source_sha256"] = sha
+    with open(os.path.join(root, "profiles/r99_pmc_traffic.json"), "w") as f:
+        json.dump(d, f)
+    with open(os.path.join(root, "super-rag_amd/csrc/k.hip"), "a") as f:
+        f.write("changed\n")
+    prov = bench.pmc_provenance(["gemm_a"], root)
+    assert prov["source_match"] is False and prov["stale"]
+
+
+def test_no_summary(tmp_path):
+    root = tmp_path / "empty"
+    (root / "profiles").mkdir(parents=True)
+    roof = {"bound": "hbm", "peak": 8000.0}
+    bench.apply_pmc(roof, "scan", ["scan"], str(root))
+    assert roof["traffic"] is None and roof["pmc_provenance"] is None
+
+
+def test_comm_record_single_process():
+    import torch.distributed as dist
+    rec = bench.comm_record(dist, 1, "nccl")
+    assert rec["world_size"] == 1 and rec["backend"] is None and rec["requested_backend"] is None
+    assert "rccl_version" in rec

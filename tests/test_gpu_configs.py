@@ -38,6 +38,9 @@ EMB_TOL = 1e-3            # north_star: embeddings within 1e-3
 # 1e-2 (1 + max|l|) without failing on that spread; ranking fidelity proper is pinned by
 # test_gpu_rerank_fidelity.py (discriminative weights, std / err >= 120).
 RERANK_TOL = 1.5e-3
+# and the MEAN |logit - ref| over the 400 logits (measured 1.9e-4): a
+# systematic drift fails here even while every single logit stays under RERANK_TOL
+RERANK_MEAN_TOL = 3e-4
 
 
 def _free():
@@ -212,9 +215,11 @@ def test_config3_rerank_top100_to_10_over_1m(corpus_1m, fp32_highest):
     lg = rer.cross_score_dev(*[torch.from_numpy(np.ascontiguousarray(a)).cuda().int()
                                for a in (pids, pmask)])[:, 0].view(nq, 100).cpu().numpy()
     dlog = np.abs(lg - lg_ref).max()
-    print(f"config3 rerank: max |logit - ref| {dlog:.2e}, logit std {lg_ref.std():.2e}, "
-          f"max |logit| {np.abs(lg_ref).max():.2e}")
+    dmean = np.abs(lg - lg_ref).mean()
+    print(f"config3 rerank: max |logit - ref| {dlog:.2e}, mean {dmean:.2e}, logit std "
+          f"{lg_ref.std():.2e}, max |logit| {np.abs(lg_ref).max():.2e}")
     assert dlog <= RERANK_TOL
+    assert dmean <= RERANK_MEAN_TOL
     final, flog = res.rows.cpu().numpy(), res.logits.cpu().numpy()
     for b in range(nq):
         order = sorted(range(100), key=lambda j: (-lg_ref[b, j], j))[:10]

@@ -35,3 +35,24 @@ def test_encode_pairs_array_form_equals_list_form():
             for x, y in zip(got, ref):
                 assert x.dtype == y.dtype and x.shape == y.shape
                 np.testing.assert_array_equal(x, y)
+
+
+def test_content_cache_is_a_byte_bounded_lru():
+    """one int32 array per text, bounded by bytes, hits refresh recency, results equal
+    the uncached tokenisation."""
+    tok = Tokenizer(MODELS["bge-reranker-base"], synthetic=True, cache_mb=0.01)  # ~10 KiB
+    fresh = Tokenizer(MODELS["bge-reranker-base"], synthetic=True, cache_mb=0)
+    texts = [" ".join(f"w{i}_{j}" for j in range(100)) for i in range(40)]  # ~500 B each
+    for t in texts:
+        assert tok.content_ids(t) == fresh.content_ids(t)
+    assert tok._cache_bytes <= tok._cache_cap_bytes
+    assert len(tok._cache) < len(texts)                 # evicted
+    assert all(isinstance(v, np.ndarray) and v.dtype == np.int32 for v in tok._cache.values())
+    assert not fresh._cache                             # cap 0: nothing kept
+    hot = texts[-len(tok._cache)]                       # the oldest cached text ...
+    tok.content_ids(hot)                                # ... refreshed by a hit
+    for t in texts[:3]:                                 # three new entries evict the LRU ones
+        tok.content_ids(t)
+    assert hot in tok._cache
+    many = tok.content_ids_many(texts[5:9] + texts[5:6])
+    assert many == [fresh.content_ids(t) for t in texts[5:9] + texts[5:6]]

@@ -72,7 +72,20 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     f_tot, f_n = read(f"{src}/fetch/pmc_1/run_counter_collection.csv", "FETCH_SIZE")
     w_tot, w_n = read(f"{src}/write/pmc_1/run_counter_collection.csv", "WRITE_SIZE")
-    out = {"source": src,
+    prov = {}
+    if os.path.exists(f"{src}/provenance.json"):  # written on the box by tools/profile_round.sh
+        with open(f"{src}/provenance.json") as f:
+            prov = json.load(f)
+    try:
+        import subprocess
+        commit = subprocess.run(["git", "rev-parse", "HEAD"], capture_output=True, text=True,
+                                check=True).stdout.strip()
+        dirty = subprocess.run(["git", "status", "--porcelain", "--", "super-rag_amd/csrc", "include"],
+                               capture_output=True, text=True, check=True).stdout.strip()
+        commit += "+uncommitted native sources" if dirty else ""
+    except Exception:  # noqa: BLE001
+        commit = None
+    out = {"source": src, "commit": commit, "source_sha256": prov.get("source_sha256"),
            "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over "
                      "`bench.py --steps 1 --warmup 1`; FETCH_SIZE x2 (gfx950 correction), "
                      "KiB -> bytes; mean per launch",

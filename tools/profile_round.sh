@@ -13,6 +13,9 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+# the native-source fingerprint the counters belong to (bench.py marks a summary stale without it)
+python3 -c "import json, bench; print(json.dumps({'source_sha256': bench.source_fingerprint()}))" \
+  > $OUT/provenance.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
   python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras > $OUT/bench_trace.log 2>&1
 timeout -k 10 600 rocprofv3 -i tools/pmc_fetch.txt -d $OUT/fetch -o run --output-format csv -- \
