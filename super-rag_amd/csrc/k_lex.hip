@@ -978,7 +978,14 @@ LexIndex* LexIndex::load(const char* path, int device) {
   int64_t rows = -1, P = -1;
   bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "SRMILEX1", 8) == 0;
   ok = ok && std::fread(&k1, 4, 1, f) == 1 && std::fread(&b, 4, 1, f) == 1;
-  ok = ok && std::fread(&rows, 8, 1, f) == 1 && std::fread(&P, 8, 1, f) == 1 && rows >= 0 && P >= 0;
+  ok = ok && std::fread(&rows, 8, 1, f) == 1 && std::fread(&P, 8, 1, f) == 1 && rows >= 0 && P >= 0 &&
+       rows < (int64_t(1) << 31) && P < (int64_t(1) << 40) && std::isfinite(k1) && std::isfinite(b);
+  // the exact size the header implies, before anything is allocated
+  if (ok) {
+    const long here = std::ftell(f);
+    ok = std::fseek(f, 0, SEEK_END) == 0 && std::ftell(f) == (long)(32 + rows * 5 + P * 12) &&
+         std::fseek(f, here, SEEK_SET) == 0;
+  }
   std::vector<int32_t> dl, ft;
   std::vector<uint8_t> live;
   std::vector<uint64_t> fv;
@@ -994,6 +1001,17 @@ LexIndex* LexIndex::load(const char* path, int device) {
   }
   std::fclose(f);
   if (!ok) throw Error(SR_ERR_IO, std::string("lex.load: not a valid lexical snapshot: ") + path);
+  // contents the kernels index by: document lengths >= 0, terms >= 0, postings in row order with
+  // rows < n_rows and tf >= 1 (a corrupt posting would address past the device arrays)
+  for (int64_t r = 0; r < rows && ok; ++r) ok = dl[(size_t)r] >= 0;
+  int64_t prev = 0;
+  for (int64_t i = 0; i < P && ok; ++i) {
+    const int64_t row = (int64_t)(fv[(size_t)i] >> 32);
+    const uint32_t tf = (uint32_t)(fv[(size_t)i] & 0xffffffffu);
+    ok = ft[(size_t)i] >= 0 && row < rows && row >= prev && tf >= 1 && tf < (1u << 31);
+    prev = row;
+  }
+  if (!ok) throw Error(SR_ERR_IO, std::string("lex.load: corrupt postings in ") + path);
   LexIndex* x = new LexIndex(device, k1, b);
   try {
     x->load_rows(dl, live, ft, fv);

@@ -492,7 +492,16 @@ Store* Store::load(const char* path, int device) {
   int64_t n = 0;
   f.read(reinterpret_cast<char*>(&d), 4);
   f.read(reinterpret_cast<char*>(&n), 8);
-  if (!f || d <= 0 || n < 0) throw Error(SR_ERR_IO, "store.load: corrupt header");
+  if (!f || d <= 0 || d > (1 << 16) || n < 0 || n > (int64_t(1) << 40))
+    throw Error(SR_ERR_IO, "store.load: corrupt header");
+  // the exact size the header implies, checked before anything is allocated: a corrupt count
+  // must not size a device allocation (or read past the rows into the live flags)
+  const std::streamoff here = f.tellg();
+  f.seekg(0, std::ios::end);
+  const std::streamoff size = f.tellg();
+  f.seekg(here);
+  if (!f || size != (std::streamoff)(20 + n * (int64_t)d * 2 + n))
+    throw Error(SR_ERR_IO, "store.load: file size does not match the header (truncated or corrupt)");
   Store* s = new Store(d, device, std::max<int64_t>(n, 1024));
   try {
     DeviceGuard g(device);
