@@ -183,6 +183,123 @@ def main():
     comm = comm_record(dist, world, a.dist_backend)
 
     from super_rag_amd import _native as N
+
+    W = setup_workload(a, world, rank, local, dev)
+    es, rs, w_embed, w_rerank = W.es, W.rs, W.w_embed, W.w_rerank
+    embedder, reranker, store, centers = W.embedder, W.reranker, W.store, W.centers
+    p_tok, batches, pipe = W.p_tok, W.batches, W.pipe
+    N_total, r0, r1, shard_p, setup_s, step_rows = W.N_total, W.r0, W.r1, W.shard_p, W.setup_s, W.step_rows
+    dt, prof = timed_steps(W, a, world, dev, dist)
+    queries = world * a.batch * a.steps
+    value = queries / dt
+
+    # ---- recall@10 of the search stage vs exact fp32 (outside the timed region) -----------------
+    recall = search_recall(W, a, dev) if world == 1 and not a.no_extras else None
+
+    peaks = measured_peaks(dev) if rank == 0 and not a.no_extras else None
+
+    # ---- search-only at B = 32 (config 2's query block) on this rank's shard: fp16 and fp8 -----
+    search32 = None
+    if rank == 0 and not a.no_extras and a.workload == "config4":
+        search32 = search_b32(store, centers, N_total, r0, r1, a.dim, dev)
+
+    # ---- fp8 precision modes: final top-10 vs the fp16 reranker on the same candidates -----------
+    fp8_fidelity = None
+    if a.fp8 and world == 1:
+        r8 = pipe.run(*batches[0])
+        reranker.set_fp8(0)
+        r16 = pipe.run(*batches[0])
+        reranker.set_fp8(a.fp8)
+        f8, f16 = r8.rows.cpu(), r16.rows.cpu()
+        overlap = sum(len(set(f8[i].tolist()) & set(f16[i].tolist())) for i in range(f8.shape[0]))
+        l16 = r16.logits.float().cpu()
+        fp8_fidelity = {"top10_overlap_vs_f16": round(overlap / f8.numel(), 4),
+                        "top1_equal_vs_f16": round(float((f8[:, 0] == f16[:, 0]).float().mean()), 4),
+                        "final_logit_std_f16": round(float(l16.std()), 5),
+                        "queries": int(f8.shape[0])}
+
+    # ---- ranking fidelity on a discriminative reranker (outside the timed region) ---------------
+    fidelity = None
+    if rank == 0 and not a.no_extras:
+        fidelity = rerank_fidelity(rs, local)
+
+    # ---- the drop-in per-request path (not the headline): concurrent callers through the pack's
+    # runners, coalesced embed / search / rerank, one query per request (tools/bench_dropin.py) ----
+    drop_in = None
+    if rank == 0 and world == 1 and not a.no_extras and a.dropin_seconds > 0:
+        from tools.bench_dropin import run as dropin_run
+        drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds)
+        drop_in["pipeline_qps_same_box"] = round(value, 2)
+
+    # ---- roofline of the dominant kernel -------------------------------------------------------
+    roof = dominant_roofline(prof)
+    step_ms = dt / a.steps * 1e3
+    kern = kernel_table(prof, a.steps)
+    search_roof = scan_roofline(prof)
+
+    # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) ----------------------------
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batches[0], p_tok, N_total,
+                           embedder, dev)
+
+    # ---- BASELINE config 5 on its fp8 path: its own timed steps after the
+    # headline, with the config-4 objects freed first --------------------------------------------
+    config5 = None
+    if a.workload == "config4" and not a.no_extras and a.config5_steps > 0:
+        del embedder, reranker, store, p_tok, batches, pipe
+        free_workload(W)
+        config5 = config5_field(a, world, rank, local, dev, dist,
+                                (fidelity or {}).get("fp8_mode3"))
+
+    workload = ("config4: bge-base-en embed (S=32) + exact cosine top-100 over "
+                f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
+                f"rerank of 100 pairs (S={a.pair_len}) -> top-{a.k}")
+    metric = "queries/sec (embed+ANN top-10+rerank) over 10M x 768-d; recall@10"
+    if a.workload == "config5":
+        workload = (f"config5: bge-m3 embed (S={a.q_len}) + fp8 cosine top-{a.k_cand} over "
+                    f"{N_total} x {a.dim} rows (row-sharded, fp16 re-scored) + BM25 top-{a.k_cand} "
+                    f"over the passage tokens, rrf-fused on the device + {a.rerank_model} rerank of "
+                    f"{a.k_cand} pairs (S={a.pair_len}) -> top-{a.k}")
+        metric = "queries/sec (config 5: bge-m3 embed + hybrid fp8-dense/BM25 retrieval + rerank)"
+    line = {
+        "metric": metric,
+        "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm", "f16+fp8mlp")[a.fp8],
+        "data": "synthetic",
+        "config": {"workload": workload,
+                   "queries_per_rank": a.batch, "global_batch": world * a.batch,
+                   "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
+                   "parallelism": f"corpus row-shard x{world}, query DP x{world}",
+                   "passages": "sharded (C3 fetch)" if shard_p else "replicated",
+                   "comm": comm},
+        "recall_at_10": recall,
+        **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
+        "rerank_fidelity": fidelity,
+        "drop_in": drop_in,
+        "roofline": roof,
+        "search_roofline": search_roof,
+        "search_b32": search32,
+        "measured_peaks": peaks,
+        "cpu_baseline": cpu,
+        "config5": config5,
+        "kernels": kern,
+        "setup_s": round(setup_s, 1),
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def setup_workload(a, world, rank, local, dev):
+    """Everything one step needs, resident on this rank's GPU: the embedder and reranker (seeded
+    random weights of the named shapes), this rank's corpus rows (and the fp8 scan copy and the
+    BM25 index of the passage tokens for config 5), the passage token table, a.batches resident
+    query batches and the SearchPipeline over them.  Returns a namespace; free_workload() releases
+    the device memory."""
+    from types import SimpleNamespace
     from super_rag_amd.encoder import MODELS, Encoder, random_weights
     from super_rag_amd.pipeline import SearchPipeline
     from super_rag_amd.store import NativeStore
@@ -199,7 +316,7 @@ def main():
     if a.fp8:
         reranker.set_fp8(a.fp8)
 
-    # ---- corpus shard (rows [r0, r1) of the global 10M) -----------------------------------------
+    # ---- corpus shard (rows [r0, r1) of the global corpus) -------------------------------------
     N_total = a.corpus_rows
     per = (N_total + world - 1) // world
     r0, r1 = rank * per, min(N_total, (rank + 1) * per)
@@ -246,89 +363,39 @@ def main():
     pipe = SearchPipeline(embedder, reranker, store, p_tok, p_len, k_candidates=a.k_cand,
                           k_final=a.k, pair_len=a.pair_len, shard_offset=r0, lexical=lexical,
                           k_each=a.k_cand, shard_passages=shard_p)
-    setup_s = time.time() - t_setup
-
-    # ---- warmup + timed region -----------------------------------------------------------------
-    for i in range(a.warmup):
-        pipe.run(*batches[i % a.batches])
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    N.profile_enable(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        res = pipe.run(*batches[i % a.batches])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    N.profile_enable(False)
-    prof = N.profile_read()
-    if world > 1:
-        t = torch.tensor([dt], device=dev if a.dist_backend != "gloo" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    queries = world * a.batch * a.steps
-    value = queries / dt
+    return SimpleNamespace(es=es, rs=rs, w_embed=w_embed, w_rerank=w_rerank, embedder=embedder,
+                           reranker=reranker, store=store, centers=centers, p_tok=p_tok,
+                           p_len=p_len, batches=batches, lexical=lexical, pipe=pipe,
+                           N_total=N_total, r0=r0, r1=r1, shard_p=shard_p, step_rows=step_rows,
+                           setup_s=time.time() - t_setup)
 
-    # ---- recall@10 of the search stage vs exact fp32 (outside the timed region) -----------------
-    recall = None
-    if world == 1 and not a.no_extras:
-        ids, mask, _, _ = batches[0]
-        nq = min(32, a.batch)
-        q16 = embedder.embed_dev(ids[:nq], mask[:nq], fp16=False)
-        _, rows = store.search_dev(q16, a.k)
-        best_s = torch.full((nq, 0), -2.0, device=dev)
-        best_r = torch.zeros((nq, 0), dtype=torch.int64, device=dev)
-        for c0 in range(0, N_total, step_rows):
-            x = gen_corpus_chunk(c0, min(N_total, c0 + step_rows), a.dim, centers, dev)
-            s = q16 @ torch.nn.functional.normalize(x, dim=1).T
-            best_s = torch.cat([best_s, s], 1)
-            best_r = torch.cat([best_r, torch.arange(c0, c0 + x.shape[0], device=dev).expand(nq, -1)], 1)
-            top = best_s.topk(a.k, dim=1)
-            best_s, best_r = top.values, best_r.gather(1, top.indices)
-        hit = sum(len(set(rows[i].tolist()) & set(best_r[i].tolist())) for i in range(nq))
-        recall = hit / (nq * a.k)
 
-    peaks = measured_peaks(dev) if rank == 0 and not a.no_extras else None
+def search_recall(W, a, dev, nq=32):
+    """recall@10 of the search stage (the store's top-k: fp16 K1, or for config 5 the fp8 scan
+    re-scored in fp16) for nq queries of batch 0 vs the exact fp32 top-k over the unquantised
+    rows (regenerated on the device chunk by chunk)."""
+    ids, mask, _, _ = W.batches[0]
+    nq = min(nq, a.batch)
+    q16 = W.embedder.embed_dev(ids[:nq], mask[:nq], fp16=False)
+    _, rows = W.store.search_dev(q16, a.k)
+    best_s = torch.full((nq, 0), -2.0, device=dev)
+    best_r = torch.zeros((nq, 0), dtype=torch.int64, device=dev)
+    for c0 in range(0, W.N_total, W.step_rows):
+        x = gen_corpus_chunk(c0, min(W.N_total, c0 + W.step_rows), a.dim, W.centers, dev)
+        s = q16 @ torch.nn.functional.normalize(x, dim=1).T
+        best_s = torch.cat([best_s, s], 1)
+        best_r = torch.cat([best_r, torch.arange(c0, c0 + x.shape[0], device=dev).expand(nq, -1)], 1)
+        top = best_s.topk(a.k, dim=1)
+        best_s, best_r = top.values, best_r.gather(1, top.indices)
+    hit = sum(len(set(rows[i].tolist()) & set(best_r[i].tolist())) for i in range(nq))
+    return hit / (nq * a.k)
 
-    # ---- search-only at B = 32 (config 2's query block) on this rank's shard: fp16 and fp8 -----
-    search32 = None
-    if rank == 0 and not a.no_extras and a.workload == "config4":
-        search32 = search_b32(store, centers, N_total, r0, r1, a.dim, dev)
 
-    # ---- fp8 precision modes: final top-10 vs the fp16 reranker on the same candidates -----------
-    fp8_fidelity = None
-    if a.fp8 and world == 1:
-        r8 = pipe.run(*batches[0])
-        reranker.set_fp8(0)
-        r16 = pipe.run(*batches[0])
-        reranker.set_fp8(a.fp8)
-        f8, f16 = r8.rows.cpu(), r16.rows.cpu()
-        overlap = sum(len(set(f8[i].tolist()) & set(f16[i].tolist())) for i in range(f8.shape[0]))
-        l16 = r16.logits.float().cpu()
-        fp8_fidelity = {"top10_overlap_vs_f16": round(overlap / f8.numel(), 4),
-                        "top1_equal_vs_f16": round(float((f8[:, 0] == f16[:, 0]).float().mean()), 4),
-                        "final_logit_std_f16": round(float(l16.std()), 5),
-                        "queries": int(f8.shape[0])}
-
-    # ---- ranking fidelity on a discriminative reranker (outside the timed region) ---------------
-    fidelity = None
-    if rank == 0 and not a.no_extras:
-        fidelity = rerank_fidelity(rs, local)
-
-    # ---- the drop-in per-request path (not the headline): concurrent callers through the pack's
-    # runners, coalesced embed / search / rerank, one query per request (tools/bench_dropin.py) ----
-    drop_in = None
-    if rank == 0 and world == 1 and not a.no_extras and a.dropin_seconds > 0:
-        from tools.bench_dropin import run as dropin_run
-        drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds)
-        drop_in["pipeline_qps_same_box"] = round(value, 2)
-
-    # ---- roofline of the dominant kernel -------------------------------------------------------
+def dominant_roofline(prof):
+    """Roofline record of the kernel with the largest total time: ALGORITHMIC flops (or bytes)
+    of its launches / their summed HIP-event durations against the spec peak (5 PF/s for the fp8
+    GEMMs, 2.5 PF/s f16, 8 TB/s HBM), with the PMC traffic of the committed summary."""
     dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
     if dom["flops"] > 0 and not dom_name.startswith("cosine_scan"):
@@ -344,76 +411,132 @@ def main():
                  "per_launch": (f"{dom['flops'] / dom['launches']:.4g} FLOP" if roof["bound"] == "mfma"
                                 else f"{dom['bytes'] / dom['launches']:.4g} B"),
                  "algorithmic_B_per_launch": round(dom["bytes"] / dom["launches"])})
-    apply_pmc(roof, dom_name, prof.keys())
-    step_ms = dt / a.steps * 1e3
-    kern = {k: {"ms_per_step": round(v["total_ms"] / a.steps, 3), "launches": v["launches"],
-                ("tflops" if v["flops"] > 0 else "gbs"):
-                    round((v["flops"] / 1e12 if v["flops"] > 0 else v["bytes"] / 1e9) / (v["total_ms"] * 1e-3), 1)}
-            for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["total_ms"])}
+    return apply_pmc(roof, dom_name, prof.keys())
+
+
+def kernel_table(prof, steps):
+    """Per logical kernel: ms per step, launches, and its rate (TF/s against its flops, or GB/s of
+    algorithmic bytes for the memory kernels); fp8 GEMMs also as a fraction of the 5 PF/s peak."""
+    out = {}
+    for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["total_ms"]):
+        rate = (v["flops"] / 1e12 if v["flops"] > 0 else v["bytes"] / 1e9) / (v["total_ms"] * 1e-3)
+        e = {"ms_per_step": round(v["total_ms"] / steps, 3), "launches": v["launches"],
+             ("tflops" if v["flops"] > 0 else "gbs"): round(rate, 1)}
+        if v["flops"] > 0 and (k.startswith("gemm_f8") or k.startswith("cosine_scan8")):
+            e["frac_of_fp8_peak"] = round(rate / PEAK_F8_TFLOPS, 4)
+        out[k] = e
+    return out
+
+
+def scan_roofline(prof):
+    """K1 (cosine_scan*) against HBM: the scans' algorithmic bytes / their time, and the ceiling
+    max(bytes / 8 TB/s, flop / MFMA peak) (at B = 256 the scan sits at the ridge)."""
     scan = {k: v for k, v in prof.items() if k.startswith("cosine_scan")}
-    if scan:
-        sb = sum(v["bytes"] for v in scan.values())
-        sm = sum(v["total_ms"] for v in scan.values())
-        search_roof = {"bound": "hbm", "achieved": round(sb / (sm * 1e-3) / 1e9, 1),
-                       "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                       "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
-        apply_pmc(search_roof, "cosine_scan", prof.keys())
-        search_roof.pop("pmc_provenance", None)  # (the same record as roofline's)
-        # at B = 256 the scan's intensity (2 B flop per row byte) sits at the ridge: its ceiling is
-        # the slower of the HBM time and the MFMA time at spec peak
-        mfma_s = sum(v["flops"] / ((PEAK_F8_TFLOPS if k.startswith("cosine_scan8") else PEAK_F16_TFLOPS) * 1e12)
-                     for k, v in scan.items())
-        ceil_ms = max(sb / (PEAK_HBM_GBS * 1e9), mfma_s) * 1e3
-        search_roof["ceiling"] = {"ms": round(ceil_ms, 3), "achieved_ms": round(sm, 3),
-                                  "frac": round(ceil_ms / sm, 4),
-                                  "note": "max(bytes / 8 TB/s, flop / MFMA peak (2.5 PF/s f16, 5 PF/s fp8)) over the timed steps"}
-    else:
-        search_roof = None
+    if not scan:
+        return None
+    sb = sum(v["bytes"] for v in scan.values())
+    sm = sum(v["total_ms"] for v in scan.values())
+    search_roof = {"bound": "hbm", "achieved": round(sb / (sm * 1e-3) / 1e9, 1),
+                   "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    apply_pmc(search_roof, "cosine_scan", prof.keys())
+    search_roof.pop("pmc_provenance", None)  # (the same record as roofline's)
+    mfma_s = sum(v["flops"] / ((PEAK_F8_TFLOPS if k.startswith("cosine_scan8") else PEAK_F16_TFLOPS) * 1e12)
+                 for k, v in scan.items())
+    ceil_ms = max(sb / (PEAK_HBM_GBS * 1e9), mfma_s) * 1e3
+    search_roof["ceiling"] = {"ms": round(ceil_ms, 3), "achieved_ms": round(sm, 3),
+                              "frac": round(ceil_ms / sm, 4),
+                              "note": "max(bytes / 8 TB/s, flop / MFMA peak (2.5 PF/s f16, 5 PF/s fp8)) over the timed steps"}
+    return search_roof
 
-    # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) ----------------------------
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a, es, rs, w_embed, w_rerank, centers, batches[0], p_tok, N_total,
-                           embedder, dev)
 
-    workload = ("config4: bge-base-en embed (S=32) + exact cosine top-100 over "
-                f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
-                f"rerank of 100 pairs (S={a.pair_len}) -> top-{a.k}")
-    metric = "queries/sec (embed+ANN top-10+rerank) over 10M x 768-d; recall@10"
-    if a.workload == "config5":
-        workload = (f"config5: bge-m3 embed (S={a.q_len}) + fp8 cosine top-{a.k_cand} over "
-                    f"{N_total} x {a.dim} rows (row-sharded, fp16 re-scored) + BM25 top-{a.k_cand} "
-                    f"over the passage tokens, rrf-fused on the device + {a.rerank_model} rerank of "
-                    f"{a.k_cand} pairs (S={a.pair_len}) -> top-{a.k}")
-        metric = "queries/sec (config 5: bge-m3 embed + hybrid fp8-dense/BM25 retrieval + rerank)"
-    line = {
-        "metric": metric,
-        "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm", "f16+fp8mlp")[a.fp8],
-        "data": "synthetic",
-        "config": {"workload": workload,
-                   "queries_per_rank": a.batch, "global_batch": world * a.batch,
-                   "corpus_rows": N_total, "rows_per_rank": r1 - r0, "weights": "seeded random",
-                   "parallelism": f"corpus row-shard x{world}, query DP x{world}",
-                   "passages": "sharded (C3 fetch)" if shard_p else "replicated",
-                   "comm": comm},
+def config5_field(a, world, rank, local, dev, dist, mode3_fidelity):
+    """BASELINE config 5 on its fp8 path, beside the config-4 headline: bge-m3
+    embed (24 layers, 1024-d, S = q_len), this rank's 6.25M x 1024 rows of the 50M corpus scanned
+    in fp8 (block-scaled MFMA, exact fp16 re-scoring), BM25 top-100 over the passage tokens and
+    rrf fusion on the device, bge-reranker-base in fp8 mode 3 (FFN1 + FFN2 on the fp8 MFMA), top-10.
+    Its own warmup / timed steps (max over ranks), kernels, roofline (fp8 GEMMs against 5 PF/s),
+    recall@10 of the dense stage, and mode 3's ranking fidelity on the discriminative set."""
+    import copy
+    a5 = as_config5(copy.copy(a))
+    if a.corpus_rows != 10_000_000:   # a smaller corpus asked for: scale the config-5 shard alike
+        a5.corpus_rows = a.corpus_rows
+    a5.fp8, a5.fp8_ffn = 3, False
+    a5.steps, a5.warmup = a.config5_steps, a.config5_warmup
+    W = setup_workload(a5, world, rank, local, dev)
+    try:
+        dt, prof = timed_steps(W, a5, world, dev, dist)
+        recall = search_recall(W, a5, dev) if world == 1 else None
+    finally:
+        setup_s = W.setup_s
+        free_workload(W)
+    value = world * a5.batch * a5.steps / dt
+    return {
+        "metric": "queries/sec (config 5: bge-m3 embed + hybrid fp8-dense/BM25 retrieval + rerank)",
+        "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a5.steps,
+        "warmup": a5.warmup, "ms_per_step": round(dt / a5.steps * 1e3, 3),
+        "dtype": "f16+fp8mlp",
+        "workload": (f"config5: bge-m3 embed (S={a5.q_len}) + fp8 cosine top-{a5.k_cand} over "
+                     f"{a5.corpus_rows} x {a5.dim} rows (row-sharded, fp16 re-scored) + BM25 "
+                     f"top-{a5.k_cand} over the passage tokens, rrf-fused on the device + "
+                     f"{a5.rerank_model} rerank in fp8 mode 3 (FFN1 + FFN2 block-scaled fp8 MFMA, "
+                     f"QKV + attention fp16) of {a5.k_cand} pairs (S={a5.pair_len}) -> top-{a5.k}"),
+        "corpus_rows": a5.corpus_rows, "rows_per_rank": shard_rows(a5.corpus_rows, world, rank),
         "recall_at_10": recall,
-        **({"rerank_fp8_fidelity": fp8_fidelity} if fp8_fidelity else {}),
-        "rerank_fidelity": fidelity,
-        "drop_in": drop_in,
-        "roofline": roof,
-        "search_roofline": search_roof,
-        "search_b32": search32,
-        "measured_peaks": peaks,
-        "cpu_baseline": cpu,
-        "kernels": kern,
+        "rerank_fp8_mode3_fidelity": mode3_fidelity,
+        "roofline": dominant_roofline(prof),
+        "search_roofline": scan_roofline(prof),
+        "kernels": kernel_table(prof, a5.steps),
         "setup_s": round(setup_s, 1),
     }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+
+
+def shard_rows(n_total, world, rank):
+    per = (n_total + world - 1) // world
+    return min(n_total, (rank + 1) * per) - rank * per
+
+
+def free_workload(W):
+    """Release a workload's device memory (encoder workspaces, corpus, BM25 index, tokens)."""
+    for obj in (W.embedder, W.reranker, W.store, W.lexical):
+        if obj is not None:
+            obj.close()
+    for k in list(vars(W)):
+        setattr(W, k, None)
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def timed_steps(W, a, world, dev, dist):
+    """a.warmup untimed steps, then EXACTLY a.steps steps bracketed by a barrier and a device
+    synchronisation on both sides; the library's HIP-event profile of the timed region; the time
+    is the max over ranks.  Returns (seconds, per-kernel profile)."""
+    from super_rag_amd import _native as N
+    for i in range(a.warmup):
+        W.pipe.run(*W.batches[i % a.batches])
+    torch.cuda.synchronize()
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    N.profile_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        W.pipe.run(*W.batches[i % a.batches])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    N.profile_enable(False)
+    prof = N.profile_read()
+    if world > 1:
+        t = torch.tensor([dt], device=dev if a.dist_backend != "gloo" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, prof
 
 
 def comm_record(dist, world, backend):
@@ -477,16 +600,19 @@ def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
 
 def rerank_fidelity(rs, device):
     """Ranking fidelity of the cross-encoder kernels at the bench shape (12 layers, 768-d, S_pair =
-    128) on a DISCRIMINATIVE reranker: the relevance-structured weights of super_rag_amd/synthetic.py
-    (the bench's seeded-random reranker spreads one query's logits by std ~1e-2 only) on 8 queries
-    x 100 candidates sharing 0..15 query terms, against the fp32 oracle's logits committed in
-    tests/golden/rerank_fidelity.npz (data; tests/golden/gen_rerank_fidelity.py).  Per precision
+    128; bge-reranker-v2-m3's 24 layers, 1024-d with --rerank-model bge-reranker-v2-m3) on a
+    DISCRIMINATIVE reranker: the relevance-structured weights of super_rag_amd/synthetic.py (the
+    bench's seeded-random reranker spreads one query's logits by std ~1e-2 only) on 8 queries x
+    100 candidates sharing 0..15 query terms, against the fp32 oracle's logits committed in
+    tests/golden/rerank_fidelity{,_v2m3}.npz (data; tests/golden/gen_rerank_fidelity.py).  Per precision
     mode: max |logit error|, the smallest per-query (logit std / max error), top-10 identical modulo
     ties within 1 % of the logit std, mean top-10 overlap, top-1 equal."""
     from super_rag_amd.encoder import Encoder
     from super_rag_amd.synthetic import fidelity_setup
-    path = os.path.join(ROOT, "tests", "golden", "rerank_fidelity.npz")
-    if not os.path.exists(path):
+    fixture = {"bge-reranker-base": "rerank_fidelity.npz",
+               "bge-reranker-v2-m3": "rerank_fidelity_v2m3.npz"}.get(rs.name)
+    path = os.path.join(ROOT, "tests", "golden", fixture) if fixture else None
+    if path is None or not os.path.exists(path):
         return None
     fx = np.load(path)
     w, ids, mask, _, m = fidelity_setup(rs)
@@ -499,7 +625,7 @@ def rerank_fidelity(rs, device):
     dmask = torch.from_numpy(mask).to(f"cuda:{device}")
     out = {"set": (f"{ref.shape[0]} queries x {m['cand']} pairs, S_pair={m['pair_len']}, "
                    f"{rs.name} shape, relevance-structured weights (super_rag_amd/synthetic.py) vs the "
-                   f"fp32 oracle (tests/golden/rerank_fidelity.npz)"),
+                   f"fp32 oracle (tests/golden/{fixture})"),
            "logit_std_mean": round(float(std.mean()), 4)}
     try:
         for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3")):

@@ -45,6 +45,9 @@
 #define SR_GEMM_GELU_V2 1  // FFN1 epilogues: 2 GELU(x) = x * T(x), T = erfc(-x / sqrt 2) from a
                            // 2049-entry LDS table over [-4 sqrt 2, 4 sqrt 2] (0: gelu2_lut)
 #endif
+#ifndef SR_GEMM_GELU_LINE
+#define SR_GEMM_GELU_LINE 1  // fp16 FFN1 epilogue: whole 128-B line stores through a 2 KiB scratch
+#endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
@@ -191,16 +194,17 @@ __device__ __forceinline__ void gelu_tab_init(float2* __restrict__ tab, int tid,
 // 2 GELU(x) = x * T(x), T(x) = 1 + erf(x / sqrt 2) = erfc(-x / sqrt 2), linearly interpolated
 // from an LDS table of GELU_NT + 1 nodes x_i = -XMAX + i h over [-XMAX, XMAX] (XMAX = 4 sqrt 2,
 // h = 2 XMAX / GELU_NT; entries (T(x_i), T(x_i+1) - T(x_i))); x outside the range takes the end
-// nodes (T(-XMAX) = 1.5e-8, T(XMAX) = 2 - 1.5e-8).  |T error| <= h^2 / 8 max|T''| = 1.9e-6.  Per
+// nodes (T(-XMAX) = 1.5e-8, T(XMAX) = 2 - 1.5e-8).  |T error| <= h^2 / 8 max|T''| = 7.4e-6 (1.5 %
+// of an fp16 ulp of the output x T; 1,025 entries = 8 KiB beside the FFN1 line scratch).  Per
 // element: v_fma + v_med3 (index space, clamped), v_cvt_u32 + v_fract, one address op, one
 // ds_read_b64, v_fma + v_mul: 7 VALU against gelu2_lut's 9-10 (and no abs / sign handling).
-constexpr int GELU_NT = 2048;
+constexpr int GELU_LOG2_NT = 10;
+constexpr int GELU_NT = 1 << GELU_LOG2_NT;
 constexpr float GELU_XMAX = 5.6568542494923802f;  // 4 sqrt 2
 // (index space through [0, 1] (the clamp modifier) and an exact ldexp)
 __device__ __forceinline__ float gelu2_t(float x, const float2* __restrict__ tab) {
-  static_assert(GELU_NT == 2048, "ldexp by 11");
   const float zc = __builtin_amdgcn_fmed3f(fmaf(x, 1.0f / (2.0f * GELU_XMAX), 0.5f), 0.0f, 1.0f);
-  const float az = __builtin_amdgcn_ldexpf(zc, 11);
+  const float az = __builtin_amdgcn_ldexpf(zc, GELU_LOG2_NT);
   const float2 t = tab[(uint32_t)az];
   return x * fmaf(__builtin_amdgcn_fractf(az), t.y, t.x);
 }
@@ -666,18 +670,25 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   }
 }
 
-// The LayerNorm-folded FFN1 epilogues (EPI_LNF_GELU_F16 / _F8) column-group outer: the bias and
-// column sums of ONE 8-column group p live at a time (16 VGPRs, the next group's loaded while this
-// one is processed) instead of all four (64 VGPRs), which left no room for the 2 GELU(x) = x T(x)
-// table form without spilling the K-loop's LDS bases.  Same outputs, same stores (16 per wave),
-// in (p, j) instead of (j, p) order.
-// DMODE (timing diagnostics, wrong results): 5 = the math without the stores, 6 = the stores of the
-// raw accumulators without the math.
+// The LayerNorm-folded FFN1 epilogues (EPI_LNF_GELU_F16 / _F8): 2 GELU(x) = x T(x) from the LDS
+// table (gelu2_t), x = rstd (acc - mu c) + b.  Per 8 outputs of one row (column group p, row
+// group j): 16 fma of the LayerNorm fold, 7 VALU + one ds_read_b64 each of the GELU.
+//   fp16 (scr != nullptr, SR_GEMM_GELU_LINE): half-tile outer -- the bias / column sums of column
+//     groups 2h, 2h + 1 live at a time (32 VGPRs) -- and per row group the 16 rows x 64 columns
+//     pass through the wave's 2 KiB LDS scratch and leave as WHOLE 128-byte lines (8 rows x 128 B
+//     per dwordx4 store instead of 16 rows x 64 B): the per-CU store path moves whole lines ~3.7x
+//     faster (tools/diag/store_rate.hip) and the FFN1 tile writes 128 KiB.
+//   fp8 / fallback: column-group outer (the bias / column sums of ONE group live, the next one's
+//     loaded while this one is processed), one 8-byte / 16-byte store per (p, j).
+// Same outputs and the same 16 stores per wave either way.
+// DMODE (timing diagnostics, wrong results): 5 = the math (and the scratch exchange) without the
+// global stores, 6 = the stores of the raw accumulators without the math.
 template <int EPI, bool CHECK, bool PERM, class Pre = NoPre, int DMODE = 0>
 __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, int mw0, int lane,
                                                 int M, const float* __restrict__ bias,
                                                 void* __restrict__ Y, int64_t ldy, const LnFold& lf,
-                                                const float2* __restrict__ gtab, const Pre& pre = Pre{}) {
+                                                const float2* __restrict__ gtab, half_t* __restrict__ scr,
+                                                const Pre& pre = Pre{}) {
   constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;
   static_assert(EPI == EPI_LNF_GELU_F16 || OUT8, "store_tile_gelu: LN-folded FFN1 epilogues");
   const int g = lane >> 4, odd = g & 1;
@@ -689,91 +700,141 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
     m = (CHECK && m >= M) ? M - 1 : m;
     mrj[j] = *reinterpret_cast<const float2*>(lf.mr + (int64_t)m * lf.stat_ld * 2);
   }
-  float4v bc[2][4];  // [buffer][b0, b1, c0, c1] of column group p
   auto load_consts = [&](float4v (&d)[4], int p) __attribute__((always_inline)) {
     d[0] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p);
     d[1] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p + 4);
     d[2] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p);
     d[3] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p + 4);
   };
-  load_consts(bc[0], 0);
-  if constexpr (!std::is_same<Pre, NoPre>::value) {
-    __builtin_amdgcn_sched_barrier(0);
-    pre();
-    __builtin_amdgcn_sched_barrier(0);
-  }
+  // the 8 outputs of (column group p, row group j): columns nlane + 32 p + 0..7 of row j
+  auto gelu8 = [&](float (&v)[8], int p, int j, const float4v (&cst)[4]) __attribute__((always_inline)) {
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    if (p < 3) load_consts(bc[(p + 1) & 1], p + 1);
-    const float4v(&cst)[4] = bc[p & 1];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = mw0 + j * 16 + (lane & 15);
-      if (CHECK && m >= M) continue;
-      const float mu = mrj[j].x, rstd = mrj[j].y;
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (PERM) {
-          v[r] = acc[2 * p][j][r];
-          v[4 + r] = acc[2 * p + 1][j][r];
-        } else {
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
-                                                           __float_as_uint(acc[2 * p + 1][j][r]), false, false);
-          v[r] = __uint_as_float(sw[0]);
-          v[4 + r] = __uint_as_float(sw[1]);
-        }
-      }
-      // (each value through an empty asm: kept scalar -- SLP packing it into v_pk_fma_f32 cost
-      // two v_mov per packed pair here, and packed f32 VALU issues no faster than two scalar ops)
-      if constexpr (DMODE != 6) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = fmaf(rstd, fmaf(-mu, cst[2][r], v[r]), cst[0][r]);
-        v[4 + r] = fmaf(rstd, fmaf(-mu, cst[3][r], v[4 + r]), cst[1][r]);
-        asm("" : "+v"(v[r]));
-        asm("" : "+v"(v[4 + r]));
-      }
-      // the 8 table reads issued together, consumed after a scheduling fence (left to the
-      // scheduler, each read was awaited right behind its own issue)
-      float fr[8];
-      float2 tv[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float az = __builtin_amdgcn_ldexpf(
-            __builtin_amdgcn_fmed3f(fmaf(v[r], 1.0f / (2.0f * GELU_XMAX), 0.5f), 0.0f, 1.0f), 11);
-        fr[r] = __builtin_amdgcn_fractf(az);
-        tv[r] = gtab[(uint32_t)az];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        v[r] *= fmaf(fr[r], tv[r].y, tv[r].x);
-        // e4m3: 2 GELU >= -0.34, so only the upper saturation bound can apply (e4m3x4's clamp)
-        if constexpr (OUT8) v[r] = fminf(v[r], 448.f);
-        asm("" : "+v"(v[r]));
-      }
-      }  // DMODE != 6
-      if constexpr (DMODE == 5) {
-        float z = 0.f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) z += v[r];
-        if (z == 12345.678f) reinterpret_cast<float*>(Y)[lane] = z;
-      } else if constexpr (OUT8) {
-        uint2 q8;
-        q8.x = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
-            v[2], v[3], __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false), true);
-        q8.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
-            v[6], v[7], __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false), true);
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (PERM) {
+        v[r] = acc[2 * p][j][r];
+        v[4 + r] = acc[2 * p + 1][j][r];
       } else {
-        half8 h;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) h[r] = (half_t)v[r];
-        *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = h;
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * p][j][r]),
+                                                         __float_as_uint(acc[2 * p + 1][j][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);  // keep the next groups' constant loads where they are
+    if constexpr (DMODE == 6) return;
+    const float mu = mrj[j].x, rstd = mrj[j].y;
+    // (each value through an empty asm: kept scalar -- SLP packing it into v_pk_fma_f32 cost two
+    // v_mov per packed pair here, and packed f32 VALU issues no faster than two scalar ops)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = fmaf(rstd, fmaf(-mu, cst[2][r], v[r]), cst[0][r]);
+      v[4 + r] = fmaf(rstd, fmaf(-mu, cst[3][r], v[4 + r]), cst[1][r]);
+      asm("" : "+v"(v[r]));
+      asm("" : "+v"(v[4 + r]));
+    }
+    // the 8 table reads issued together, consumed after a scheduling fence (left to the
+    // scheduler, each read was awaited right behind its own issue)
+    float fr[8];
+    float2 tv[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float az = __builtin_amdgcn_ldexpf(
+          __builtin_amdgcn_fmed3f(fmaf(v[r], 1.0f / (2.0f * GELU_XMAX), 0.5f), 0.0f, 1.0f), GELU_LOG2_NT);
+      fr[r] = __builtin_amdgcn_fractf(az);
+      tv[r] = gtab[(uint32_t)az];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      v[r] *= fmaf(fr[r], tv[r].y, tv[r].x);
+      // e4m3: 2 GELU >= -0.34, so only the upper saturation bound can apply (e4m3x4's clamp)
+      if constexpr (OUT8) v[r] = fminf(v[r], 448.f);
+      asm("" : "+v"(v[r]));
+    }
+  };
+  if constexpr (!OUT8 && SR_GEMM_GELU_LINE) {
+    // ---- fp16, whole-line stores through the 2 KiB scratch (16 rows x 128 B, chunk k of row r
+    // at k ^ (r & 7): conflict-free b128 writes and reads) --------------------------------------
+    float4v bc[2][4];  // bias / colsum of column groups 2h, 2h + 1
+    load_consts(bc[0], 0);
+    load_consts(bc[1], 1);
+    if constexpr (!std::is_same<Pre, NoPre>::value) {
+      __builtin_amdgcn_sched_barrier(0);
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1) {
+        load_consts(bc[0], 2);
+        load_consts(bc[1], 3);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          float v[8];
+          gelu8(v, 2 * h + pp, j, bc[pp]);
+          half8 hv;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) hv[r] = (half_t)v[r];
+          const int ln = lane_id_here(), gl = ln >> 4, row = ln & 15;
+          const int k = 4 * pp + 2 * (gl & 1) + (gl >> 1);       // 16-B chunk of the 128-B row
+          *reinterpret_cast<half8*>(scr + row * 64 + ((k ^ (row & 7)) << 3)) = hv;
+        }
+        // read back as 8 rows x 8 chunks per instruction: row 8q + (lane >> 3), chunk lane & 7
+        half_t* const yw = reinterpret_cast<half_t*>(Y) + (int64_t)(mw0 + j * 16) * ldy + nw0 + 64 * h;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ln = lane_id_here(), c = ln & 7, rr = 8 * q + (ln >> 3);
+          const half8 o = *reinterpret_cast<const half8*>(scr + rr * 64 + ((c ^ (rr & 7)) << 3));
+          if constexpr (DMODE == 5) {
+            if ((float)o[0] == 12345.f) reinterpret_cast<half_t*>(Y)[ln] = o[1];
+          } else if (!CHECK || mw0 + j * 16 + rr < M) {
+            *reinterpret_cast<half8*>(yw + (int64_t)rr * ldy + c * 8) = o;
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
+    }
+  } else {
+    // ---- column-group outer, one 8- / 16-byte store per (p, j) -----------------------------------
+    float4v bc[2][4];  // [buffer][b0, b1, c0, c1] of column group p
+    load_consts(bc[0], 0);
+    if constexpr (!std::is_same<Pre, NoPre>::value) {
+      __builtin_amdgcn_sched_barrier(0);
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p < 3) load_consts(bc[(p + 1) & 1], p + 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mw0 + j * 16 + (lane & 15);
+        if (CHECK && m >= M) continue;
+        float v[8];
+        gelu8(v, p, j, bc[p & 1]);
+        if constexpr (DMODE == 5) {
+          float z = 0.f;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) z += v[r];
+          if (z == 12345.678f) reinterpret_cast<float*>(Y)[lane] = z;
+        } else if constexpr (OUT8) {
+          uint2 q8;
+          q8.x = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
+              v[2], v[3], __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false), true);
+          q8.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
+              v[6], v[7], __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false), true);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+        } else {
+          half8 hv;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) hv[r] = (half_t)v[r];
+          *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the next groups' constant loads where they are
+    }
   }
 }
 
@@ -793,7 +854,7 @@ struct PipeEpi {
                                              const float2* __restrict__ gtab = nullptr,
                                              const Pre& pre = Pre{}) {
     if constexpr (WIDE && GLUT && SR_GEMM_GELU_V2 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
-      store_tile_gelu<EPI, CHECK, PERM, Pre>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, pre);
+      store_tile_gelu<EPI, CHECK, PERM, Pre>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre);
     else if constexpr (WIDE)
       store_tile_wide<EPI, CHECK, LINE, GLUT, PERM, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
     else
@@ -984,9 +1045,11 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
   // and the 32-bit-output epilogues index the rows as staged)
   constexpr bool PERMW = SR_GEMM_PERMW && PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (SCAN ? 512 : 0) +
-                                                     (GLUT ? 4 * GTAB : 0)];
-  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0));
+  // GLINE: the fp16 FFN1 epilogue's 2 KiB per-wave line scratch (store_tile_gelu)
+  constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE && EPI == EPI_LNF_GELU_F16;
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
+                                                     (SCAN ? 512 : 0) + (GLUT ? 4 * GTAB : 0)];
+  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0));
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
   // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
   constexpr bool LATE = SR_GEMM_LATE_STAGE && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
@@ -1027,6 +1090,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wm = wave & 3;
+  // the epilogue's per-wave scratch: LINE 4 KiB / GLINE 2 KiB (nothing else uses it)
+  half_t* const escr = lds + 2 * STAGE + wave * (GLINE ? 1024 : 2048);
+  half_t* const gscr = GLINE ? escr : nullptr;
+  (void)gscr;
 #ifdef SR_GEMM_PRIO_HALF  // experiment: static priority for the second-dispatched half
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -1311,9 +1378,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     if constexpr (DIAG == 5 || DIAG == 6) {  // FFN1 epilogue without its stores / its math
       static_assert(GLUT && SR_GEMM_GELU_V2, "DIAG 5 / 6: the FFN1 epilogue");
       if (full)
-        store_tile_gelu<EPI, false, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab);
+        store_tile_gelu<EPI, false, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
       else
-        store_tile_gelu<EPI, true, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab);
+        store_tile_gelu<EPI, true, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
     } else if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
       const int g = lane >> 4, odd = g & 1;
       const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
@@ -1375,16 +1442,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       };
       if (full)
         PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                          R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab, pre);
+                                                          R, ldr, Y, ldy, lf, escr, gtab, pre);
       else
         PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                         R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab, pre);
+                                                         R, ldr, Y, ldy, lf, escr, gtab, pre);
     } else if (full) {
       PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                        R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab);
+                                                        R, ldr, Y, ldy, lf, escr, gtab);
     } else {
       PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                       R, ldr, Y, ldy, lf, lds + 2 * STAGE + wave * 2048, gtab);
+                                                       R, ldr, Y, ldy, lf, escr, gtab);
     }
     if (!more) break;
     // next tile: K-step 0 (group 0's 16 glds) landed; younger: the epilogue's NSTORE stores

@@ -1,0 +1,63 @@
+"""GPU: ranking fidelity at the shape of the reranker the reference actually seeds,
+BAAI/bge-reranker-v2-m3 (migration/sql/model_configs_init.sql:4148; XLM-R large: 24 layers,
+1024-d, 16 heads of 64, FFN 4096), at FULL depth.  The relevance-structured
+construction of super_rag_amd/synthetic.py at that shape (layers 2..23 HF-random, residual branches
+scaled by 1/sqrt(2L)) on the fidelity set (8 queries x 100 candidates, S_pair = 128) against the
+fp32 oracle's logits committed in tests/golden/rerank_fidelity_v2m3.npz
+(tests/golden/gen_rerank_fidelity.py --model bge-reranker-v2-m3):
+  fp16          per query logit std >= RATIO_MIN x max |logit error|, top-10 identical to the
+                oracle's modulo ties within 1 % of the logit std;
+  fp8 mode 3    the same gate at RATIO_MIN_FP8 (FFN1 + FFN2 on the block-scaled fp8 MFMA).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIX = os.path.join(os.path.dirname(__file__), "golden", "rerank_fidelity_v2m3.npz")
+RATIO_MIN = 100.0
+RATIO_MIN_FP8 = 50.0
+TIE_BAND = 0.01
+
+
+@pytest.fixture(scope="module")
+def fidelity_v2m3():
+    import torch
+    from super_rag_amd.encoder import MODELS, Encoder
+    from super_rag_amd.synthetic import fidelity_setup, weight_checksum
+    fx = np.load(FIX)
+    spec = MODELS["bge-reranker-v2-m3"]
+    w, ids, mask, overlap, _ = fidelity_setup(spec)
+    assert np.array_equal(ids, fx["ids"]) and np.array_equal(overlap, fx["overlap"])
+    assert abs(weight_checksum(w) - float(fx["checksum"])) <= 1e-9 * abs(float(fx["checksum"]))
+    enc = Encoder(spec, weights=w, max_tokens=ids.size)
+    del w
+    yield enc, torch.from_numpy(ids).cuda(), torch.from_numpy(mask).cuda(), fx["logits"].reshape(-1, 100)
+    enc.close()
+
+
+def _gate(lg, ref, ratio, label):
+    std = ref.std(1)
+    err = np.abs(lg - ref).max(1)
+    print(f"{label}: logit std per query {std.round(3).tolist()}; max |logit - oracle| "
+          f"{err.round(5).tolist()}; std / err min {float((std / err).min()):.1f}")
+    assert (std >= ratio * err).all(), (std / err)
+    for b in range(ref.shape[0]):
+        want = np.argsort(-ref[b], kind="stable")[:10]
+        got = np.argsort(-lg[b], kind="stable")[:10]
+        kth = ref[b][want[-1]]
+        assert all(abs(ref[b][j] - kth) <= TIE_BAND * std[b] for j in set(want) ^ set(got)), b
+
+
+@pytest.mark.parametrize("mode", [0, 3])
+def test_v2m3_reranker_ranks_like_the_oracle(fidelity_v2m3, mode):
+    enc, ids, mask, ref = fidelity_v2m3
+    enc.set_fp8(mode)
+    try:
+        lg = enc.cross_score_dev(ids, mask)[:, 0].float().cpu().numpy().reshape(-1, 100)
+    finally:
+        enc.set_fp8(0)
+    _gate(lg, ref, RATIO_MIN if mode == 0 else RATIO_MIN_FP8,
+          "bge-reranker-v2-m3 " + ("fp16" if mode == 0 else f"fp8 mode {mode}"))
