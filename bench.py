@@ -71,6 +71,10 @@ def parse():
                          "(0 = skip)")
     ap.add_argument("--dropin-rows", type=int, default=100000,
                     help="drop_in field: chunks in the connector collection it searches")
+    ap.add_argument("--dropin-procs", type=int, default=4,
+                    help="drop_in field: also run this many serving processes on the GPU together "
+                         "(C = 64 callers each; started before this process touches the GPU, "
+                         "released after the timed region; 0 / 1 = skip)")
     ap.add_argument("--workload", default="config4", choices=["config4", "config5"],
                     help="config4 (default, the BASELINE metric) or config5: bge-m3 embed, 6.25M x "
                          "1024 rows per GPU scanned in fp8, BM25 over the passage tokens fused by "
@@ -158,6 +162,83 @@ def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
         sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    # the multi-process drop-in run's serving processes start NOW, before this process initialises
+    # the GPU (they wait for a go file and touch nothing until then)
+    mp = None
+    if ("WORLD_SIZE" not in os.environ or os.environ.get("WORLD_SIZE") == "1") and not a.no_extras \
+            and a.dropin_seconds > 0 and a.dropin_procs > 1 and a.workload == "config4":
+        mp = DropinProcs(a.dropin_procs, a.dropin_rows, a.dropin_seconds)
+    try:
+        run_bench(a, mp)
+    finally:
+        if mp is not None:
+            mp.stop()
+
+
+class DropinProcs:
+    """N serving processes of the drop-in per-request path on this GPU (tools/bench_dropin.py, one
+    collection, models and coalescers each, C = 64 closed-loop callers each), started as child
+    processes before the bench initialises the GPU; release() lets them set up and measure the
+    same window together, collect() sums their throughput and pools their request latencies."""
+
+    def __init__(self, n, rows, seconds):
+        import tempfile
+        self.dir = tempfile.mkdtemp(prefix="sr_dropin_")
+        self.go = os.path.join(self.dir, "go.json")
+        self.procs = []
+        for i in range(n):
+            cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "bench_dropin.py"),
+                   "--rows", str(rows), "--concurrency", "64", "--seconds", str(seconds),
+                   "--go-file", self.go, "--lat-out", os.path.join(self.dir, f"lat{i}")]
+            out = open(os.path.join(self.dir, f"p{i}.json"), "w")
+            err = open(os.path.join(self.dir, f"p{i}.err"), "w")
+            self.procs.append((subprocess.Popen(cmd, stdout=out, stderr=err), out, err))
+
+    def release(self, delay_s=60.0):
+        with open(self.go + ".tmp", "w") as f:
+            json.dump({"start_at": time.time() + delay_s}, f)
+        os.replace(self.go + ".tmp", self.go)
+
+    def collect(self, timeout_s=300.0):
+        runs, lats = [], []
+        t_end = time.time() + timeout_s
+        for i, (p, out, err) in enumerate(self.procs):
+            try:
+                rc = p.wait(timeout=max(1.0, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                rc = "timeout"
+            out.close()
+            err.close()
+            if rc != 0:
+                with open(err.name) as f:
+                    tail = f.read()[-600:]
+                return {"error": f"serving process {i} exited {rc}: {tail}"}
+            with open(out.name) as f:
+                runs.append(json.loads(f.read().strip().splitlines()[-1])["runs"][0])
+            lats.append(np.load(os.path.join(self.dir, f"lat{i}_c64.npy")))
+        lat = np.concatenate(lats)
+        return {"procs": len(runs), "concurrency_per_proc": 64,
+                "qps": round(sum(r["qps"] for r in runs), 1),
+                "per_proc_qps": [r["qps"] for r in runs],
+                "p50_ms": round(float(np.percentile(lat, 50)), 1),
+                "p99_ms": round(float(np.percentile(lat, 99)), 1),
+                "requests": int(sum(r["requests"] for r in runs)),
+                "seconds": max(r["seconds"] for r in runs),
+                "rerank_mean_batch": [r["coalesced"].get("rerank", {}).get("mean_batch") for r in runs]}
+
+    def stop(self):
+        for p, out, err in self.procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            out.close()
+            err.close()
+        import shutil
+        shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def run_bench(a, mp=None):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -230,6 +311,12 @@ def main():
         from tools.bench_dropin import run as dropin_run
         drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds)
         drop_in["pipeline_qps_same_box"] = round(value, 2)
+        if mp is not None:
+            # N serving processes on this GPU, C = 64 callers each, measured together (this
+            # process idle meanwhile): the per-process host cost (~5 ms of Python per request)
+            # spread over N interpreters
+            mp.release()
+            drop_in["multi_process"] = mp.collect()
 
     # ---- roofline of the dominant kernel -------------------------------------------------------
     roof = dominant_roofline(prof)

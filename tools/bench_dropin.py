@@ -114,7 +114,8 @@ def _profiled_worker_init():
     pr.enable()
 
 
-def measure(concurrency: int, seconds: float, col_id: str, queries, profile: bool = False) -> dict:
+def measure(concurrency: int, seconds: float, col_id: str, queries, profile: bool = False,
+            lat_out: str | None = None) -> dict:
     loop = asyncio.new_event_loop()
     # one worker thread per concurrent request for the blocking device calls (asyncio.to_thread):
     # the default executor's min(32, cpus + 4) threads would cap the coalesced batches at 32
@@ -147,13 +148,29 @@ def measure(concurrency: int, seconds: float, col_id: str, queries, profile: boo
                 e["device_busy_frac"] = round((sec - s0) / dt, 3)
                 e["device_ms_per_batch"] = round((sec - s0) / (holds - h0) * 1e3, 2)
     lat_ms = np.asarray(lat) * 1e3
+    if lat_out:
+        np.save(lat_out, lat_ms.astype(np.float32))
     return {"concurrency": concurrency, "requests": n, "seconds": round(dt, 2),
             "qps": round(n / dt, 1), "p50_ms": round(float(np.percentile(lat_ms, 50)), 1),
             "p99_ms": round(float(np.percentile(lat_ms, 99)), 1), "coalesced": stages}
 
 
+def wait_for_go(path: str, timeout_s: float = 1800.0) -> float:
+    """Block (no GPU touched) until `path` exists, then return the start time it holds: bench.py
+    starts its serving processes before it initialises the GPU itself and releases them once its
+    timed region is over (no exec from a process that has initialised the GPU)."""
+    t_end = time.time() + timeout_s
+    while not os.path.exists(path):
+        if time.time() > t_end:
+            raise SystemExit(f"bench_dropin: no go file {path} after {timeout_s:.0f} s")
+        time.sleep(0.2)
+    time.sleep(0.1)
+    with open(path) as f:
+        return float(json.load(f)["start_at"])
+
+
 def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16,
-        start_at: float = 0.0) -> dict:
+        start_at: float = 0.0, lat_out: str | None = None) -> dict:
     col_id = "dropin"
     t = time.time()
     build_collection(col_id, rows)
@@ -169,7 +186,8 @@ def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup
                     "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
                     "(synthetic weights, hashing tokenizer); vector_topk 100, S_pair <= 128"),
            "rows": rows, "setup_s": round(setup, 1),
-           "runs": [measure(c, seconds, col_id, queries) for c in concurrency],
+           "runs": [measure(c, seconds, col_id, queries,
+                            lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None)) for c in concurrency],
            "reference_orchestration_ms_per_query": 5.14}
     return out
 
@@ -182,6 +200,11 @@ def main():
     ap.add_argument("--start-at", type=float, default=0.0,
                     help="wall-clock time (time.time()) to start the measured runs at, after "
                          "setup and warmup: several processes serving from one GPU measure together")
+    ap.add_argument("--go-file", default=None,
+                    help="wait for this file (written by bench.py) before touching the GPU; it "
+                         "holds the common start time of the measured runs")
+    ap.add_argument("--lat-out", default=None,
+                    help="save each run's request latencies (ms) to <lat-out>_c<C>.npy")
     ap.add_argument("--profile", action="store_true",
                     help="cProfile the event loop and every worker thread of one run at "
                          "--profile-concurrency (host time per request by function), printed after "
@@ -208,7 +231,9 @@ def main():
             st.add(pr)
         st.sort_stats("tottime").print_stats(45)
         return
-    print(json.dumps(run(a.rows, a.concurrency, a.seconds, start_at=a.start_at)), flush=True)
+    start_at = wait_for_go(a.go_file) if a.go_file else a.start_at
+    print(json.dumps(run(a.rows, a.concurrency, a.seconds, start_at=start_at, lat_out=a.lat_out)),
+          flush=True)
 
 
 if __name__ == "__main__":
