@@ -188,6 +188,17 @@ def device_gate(device: int, stage: str = "device"):
     return g.hold(stage)
 
 
+@contextlib.contextmanager
+def devices_gate(devices, stage: str = "device"):
+    """device_gate over several devices (a collection sharded over them): every device's gate,
+    taken in ascending device order (one global order, so two multi-device holders cannot
+    deadlock), each charged the hold time of `stage`."""
+    with contextlib.ExitStack() as st:
+        for d in sorted(set(int(x) for x in devices)):
+            st.enter_context(device_gate(d, stage))
+        yield
+
+
 def gate_busy() -> dict:
     """{device: {stage: (seconds held, holds)}} accumulated by device_gate."""
     return {d: {k: (v[0], v[1]) for k, v in g.busy.items()} for d, g in list(_gates.items())}

@@ -33,7 +33,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
 
-from ._native import device_gate
+from ._native import devices_gate
 from .models import DocumentWithScore, QueryResult
 
 logger = logging.getLogger(__name__)
@@ -458,11 +458,11 @@ class MI355XVectorStoreConnector:
                 Q = np.stack([np.asarray(items[i][0], dtype=np.float32).reshape(-1) for i in idx])
                 kmax = max(items[i][1] for i in idx)
                 if key == "":
-                    with device_gate(getattr(c.store, "device", 0), "search"):
+                    with devices_gate(_store_devices(c.store), "search"):
                         dist, rows = c.store.search(Q, kmax)
                 else:
                     mkey, allow = MI355XVectorStoreConnector._allow_mask(c, items[idx[0]][2])
-                    with device_gate(getattr(c.store, "device", 0), "search"):
+                    with devices_gate(_store_devices(c.store), "search"):
                         dist, rows = c.store.search(Q, kmax, allow=allow, mask_key=mkey)
                 for j, i in enumerate(idx):
                     k = items[i][1]
@@ -482,8 +482,9 @@ class MI355XVectorStoreConnector:
             allow, mkey = None, 0
             if flt is not None:
                 mkey, allow = self._allow_mask(c, flt)
-            scores, rows = c.lex.hybrid(c.store, q.reshape(1, -1), [terms], k, k_each,
-                                        self.rrf_rank_const, allow=allow, mask_key=mkey)
+            with devices_gate(_store_devices(c.store), "search"):
+                scores, rows = c.lex.hybrid(c.store, q.reshape(1, -1), [terms], k, k_each,
+                                            self.rrf_rank_const, allow=allow, mask_key=mkey)
             return [_make_doc(text=c.texts[r], score=float(s), metadata=_json_copy(c.metadatas[r]))
                     for s, r in zip(scores[0].tolist(), rows[0].tolist()) if r >= 0]
 
@@ -507,7 +508,9 @@ class MI355XVectorStoreConnector:
             allow, mkey = None, 0
             if flt is not None:
                 mkey, allow = self._allow_mask(c, flt)
-            scores, rows = c.lex.search([terms], min(int(top_k), 1024), allow=allow, mask_key=mkey)
+            with devices_gate(_store_devices(c.store), "search"):
+                scores, rows = c.lex.search([terms], min(int(top_k), 1024), allow=allow,
+                                            mask_key=mkey)
             return [_make_doc(text=c.texts[r], score=float(s), metadata=_json_copy(c.metadatas[r]))
                     for s, r in zip(scores[0].tolist(), rows[0].tolist()) if r >= 0]
 
@@ -518,6 +521,13 @@ class MI355XVectorStoreConnector:
             raise KeyError(self.collection_name)
         with c.lock:
             return c.store.get(np.asarray([c.row_of[u] for u in ids], dtype=np.int64))
+
+
+def _store_devices(store) -> List[int]:
+    """The devices a collection's store computes on: every shard's for a ShardedStore (its
+    searches run on all of them), else the store's one device."""
+    devs = getattr(store, "devices", None)
+    return list(devs) if devs else [int(getattr(store, "device", 0))]
 
 
 class VectorStoreConnectorAdaptor:

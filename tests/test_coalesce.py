@@ -160,3 +160,37 @@ def test_rerank_batch_width_is_bucketed_and_padding_is_masked():
             ids, mask, _ = tok.encode_pairs(q, ts)
             np.testing.assert_array_equal(g, ((ids * mask).sum(1, dtype=np.int64) % 10007).astype(np.float32))
         assert gate_busy()[0]["rerank"][1] == before + 1
+
+
+def test_devices_gate_takes_every_shard_device_in_order():
+    """a sharded collection's search holds the gate of EVERY device it computes on
+    (ascending order), so it serialises with embed / rerank batches on those devices and its busy
+    time is charged to each of them; a single-device store keeps its one gate."""
+    import threading
+    from super_rag_amd._native import devices_gate, gate_busy, device_gate
+    from super_rag_amd.vectorstore import _store_devices
+
+    class Sharded:
+        devices = [3, 1, 2]
+
+    class One:
+        device = 5
+
+    assert _store_devices(Sharded()) == [3, 1, 2] and _store_devices(One()) == [5]
+    before = gate_busy()
+    with devices_gate([3, 1, 2, 1], "search"):
+        # another thread cannot take device 2's gate while the sharded search holds it
+        got = []
+
+        def other():
+            with device_gate(2, "embed"):
+                got.append(1)
+        t = threading.Thread(target=other)
+        t.start()
+        t.join(0.2)
+        assert t.is_alive() and not got
+    t.join(2.0)
+    assert not t.is_alive() and got == [1]
+    after = gate_busy()
+    for d in (1, 2, 3):
+        assert after[d]["search"][1] == before.get(d, {}).get("search", (0, 0))[1] + 1
