@@ -92,12 +92,26 @@ def parse():
                          "SearchPipeline shard_passages / C3)")
     ap.add_argument("--dist-backend", default=os.environ.get("SR_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
+    ap.add_argument("--config5-steps", type=int, default=5,
+                    help="config5 field of the default (config4) line: timed steps of BASELINE "
+                         "config 5 on its fp8 path (bge-m3 embed, 6.25M x 1024 rows per GPU "
+                         "scanned in fp8, BM25 + rrf on the device, reranker in fp8 mode 3), run "
+                         "after the headline with the config-4 objects freed (0 = skip)")
+    ap.add_argument("--config5-warmup", type=int, default=2)
     a = ap.parse_args()
     if a.workload == "config5":
-        a.embed_model, a.dim = "bge-m3", 1024
-        if a.corpus_rows == 10_000_000:  # default: the 50M / 8-GPU shard size per GPU (weak)
-            a.corpus_rows = 6_250_000 * int(os.environ.get("WORLD_SIZE", "1"))
+        as_config5(a)
         a.no_cpu_baseline = True
+    return a
+
+
+def as_config5(a):
+    """BASELINE config 5 on one rank's share: bge-m3 (1024-d) embed, the 50M / 8-GPU shard size
+    (6.25M rows) per rank scanned in fp8, BM25 over the passage tokens fused by rrf."""
+    a.workload = "config5"
+    a.embed_model, a.dim = "bge-m3", 1024
+    if a.corpus_rows == 10_000_000:  # default: the 50M / 8-GPU shard size per GPU (weak)
+        a.corpus_rows = 6_250_000 * int(os.environ.get("WORLD_SIZE", "1"))
     return a
 
 
@@ -544,12 +558,7 @@ def config5_field(a, world, rank, local, dev, dist, mode3_fidelity):
     rrf fusion on the device, bge-reranker-base in fp8 mode 3 (FFN1 + FFN2 on the fp8 MFMA), top-10.
     Its own warmup / timed steps (max over ranks), kernels, roofline (fp8 GEMMs against 5 PF/s),
     recall@10 of the dense stage, and mode 3's ranking fidelity on the discriminative set."""
-    import copy
-    a5 = as_config5(copy.copy(a))
-    if a.corpus_rows != 10_000_000:   # a smaller corpus asked for: scale the config-5 shard alike
-        a5.corpus_rows = a.corpus_rows
-    a5.fp8, a5.fp8_ffn = 3, False
-    a5.steps, a5.warmup = a.config5_steps, a.config5_warmup
+    a5 = config5_args(a)
     W = setup_workload(a5, world, rank, local, dev)
     try:
         dt, prof = timed_steps(W, a5, world, dev, dist)
@@ -576,6 +585,18 @@ def config5_field(a, world, rank, local, dev, dist, mode3_fidelity):
         "kernels": kernel_table(prof, a5.steps),
         "setup_s": round(setup_s, 1),
     }
+
+
+def config5_args(a):
+    """The config-5 field's arguments from the headline's: config 5's models and shard size, the
+    reranker in fp8 mode 3, the field's own step counts."""
+    import copy
+    a5 = as_config5(copy.copy(a))
+    if a.corpus_rows != 10_000_000:   # a smaller corpus asked for: scale the config-5 shard alike
+        a5.corpus_rows = a.corpus_rows
+    a5.fp8, a5.fp8_ffn = 3, False
+    a5.steps, a5.warmup = a.config5_steps, a.config5_warmup
+    return a5
 
 
 def shard_rows(n_total, world, rank):
