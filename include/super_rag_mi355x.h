@@ -346,7 +346,8 @@ int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W
  * or fp8 (f8 = 1: X, W OCP e4m3 bytes, wexp the E8M0 exponent byte of each W row, Y e4m3 bytes);
  * mr = (mu, rstd) per X row, colsum / bias N fp32.  diag: 0 the product kernel, 2 the main loop
  * without an epilogue, 5 the epilogue math without its stores, 6 the stores of the raw
- * accumulators without the math (2 / 5 / 6: timing only, wrong results). */
+ * accumulators without the math, 7 the product epilogue with every tile's stores folded onto the
+ * first tile (L2-resident) (2 / 5 / 6 / 7: timing only, wrong results). */
 int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                  const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
                  int N, int K, int device, void* stream);

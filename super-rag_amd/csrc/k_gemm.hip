@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
                         (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
   // GLUT: the FFN1 epilogues' 8 KiB erf table (gelu2_lut) past the stages / line scratch
-  constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6) &&
+  constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
   constexpr int GTAB = SR_GEMM_GELU_V2 ? GELU_NT + 1 : GELU_TAB;  // float2 entries
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
@@ -1375,7 +1375,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 
     // (EPI_SCAN issues a data-dependent number of atomics / stores: never counted as pending)
     const bool full = !SCAN && m0 + BM <= M;
-    if constexpr (DIAG == 5 || DIAG == 6) {  // FFN1 epilogue without its stores / its math
+    if constexpr (DIAG == 7) {  // the FFN1 epilogue with every tile's stores folded onto tile (0, 0)
+      store_tile_gelu<EPI, false, PERMW, NoPre, 0>(acc, wn * 128, wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
+    } else if constexpr (DIAG == 5 || DIAG == 6) {  // FFN1 epilogue without its stores / its math
       static_assert(GLUT && SR_GEMM_GELU_V2, "DIAG 5 / 6: the FFN1 epilogue");
       if (full)
         store_tile_gelu<EPI, false, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
@@ -1880,7 +1882,7 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
                       int M, int N, int K, hipStream_t stream) {
-  SR_CHECK(diag == 0 || diag == 2 || diag == 5 || diag == 6, "ffn1_diag: diag must be 0, 2, 5 or 6");
+  SR_CHECK(diag == 0 || diag == 2 || (diag >= 5 && diag <= 7), "ffn1_diag: diag must be 0, 2, 5, 6 or 7");
   SR_CHECK(N % 256 == 0 && M > 0, "ffn1_diag: N % 256 == 0, M > 0");
   LnFold lf;
   lf.mr = mr;
@@ -1917,8 +1919,10 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
 #if SR_GEMM_GELU_V2
     if (diag == 5) {
       SR_FD(5)
-    } else {
+    } else if (diag == 6) {
       SR_FD(6)
+    } else {
+      SR_FD(7)
     }
 #else
     SR_CHECK(false, "ffn1_diag: diag 5 / 6 need the SR_GEMM_GELU_V2 epilogue");
