@@ -82,10 +82,11 @@ def parse():
     ap.add_argument("--fp8-ffn", action="store_true",
                     help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
                          "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
-    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3),
+    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3, 4),
                     help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
                          "e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16 "
-                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp)")
+                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp); 4 = 3 + QKV fp8 on normalised "
+                         "e4m3 rows (f16+fp8mlp+qkvn, experimental)")
     ap.add_argument("--replicate-passages", action="store_true",
                     help="N > 1: keep the whole passage token table on every rank (default: each "
                          "rank holds its shard's rows, the candidates' rows are fetched per batch, "
@@ -367,7 +368,7 @@ def run_bench(a, mp=None):
         "metric": metric,
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm", "f16+fp8mlp")[a.fp8],
+        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm", "f16+fp8mlp", "f16+fp8mlp+qkvn")[a.fp8],
         "data": "synthetic",
         "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
@@ -736,7 +737,8 @@ def rerank_fidelity(rs, device):
                    f"fp32 oracle (tests/golden/{fixture})"),
            "logit_std_mean": round(float(std.mean()), 4)}
     try:
-        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3")):
+        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3"),
+                           (4, "fp8_mode4")):
             enc.set_fp8(mode)
             lg = enc.cross_score_dev(dids, dmask)[:, 0].float().cpu().numpy().reshape(ref.shape)
             err = np.abs(lg - ref).max(1)

@@ -184,7 +184,7 @@ static bool kvfree_cls_enabled() {
 }
 
 void Encoder::set_fp8(int mode) {
-  SR_CHECK(mode >= 0 && mode <= 3, "encoder: fp8 mode must be 0, 1, 2 or 3");
+  SR_CHECK(mode >= 0 && mode <= 4, "encoder: fp8 mode must be 0 .. 4");
   if (mode) {
     SR_CHECK(fold_enabled(), "encoder: fp8 modes need the LN-folded fp16-residual path");
     SR_CHECK(cfg_.intermediate % 128 == 0 && cfg_.intermediate >= 256 &&
@@ -248,7 +248,7 @@ void Encoder::prepare_fold(hipStream_t s) {
       launch_kv_blockdiag(L.wqkv_f.as<half_t>(), (int)D, cfg_.heads, L.wk_bd.as<half_t>(),
                           L.wv_bd.as<half_t>(), s);
     }
-    if (fp8_ == 2) {
+    if (fp8_ == 2 || fp8_ == 4) {
       L.wqkv8.reserve((size_t)3 * D * D);
       L.wqkve.reserve((size_t)3 * D);
       L.cqkv8.reserve((size_t)3 * D * sizeof(float));
@@ -257,6 +257,12 @@ void Encoder::prepare_fold(hipStream_t s) {
       launch_colsum_fp8(L.wqkv8.as<uint8_t>(), L.wqkve.as<uint8_t>(), (int)(3 * D), (int)D,
                         L.cqkv8.as<float>(), s);
     }
+  }
+  if (fp8_ == 4) {  // (mu, rstd) = (0, 1) for every row: mode 4's QKV reads normalised rows
+    unit_mr_.reserve(2 * sizeof(float));
+    const float one[2] = {0.f, 1.f};
+    SR_HIP(hipMemcpyAsync(unit_mr_.p, one, sizeof(one), hipMemcpyHostToDevice, s));
+    SR_HIP(hipStreamSynchronize(s));
   }
   fold_ready_ = true;
 }
@@ -358,7 +364,9 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       // K5c: QKV projection + attention in one kernel (the QKV activation stays in LDS)
       // fp8 modes: 2 and 3 run FFN1 (and FFN2) on e4m3 copies of the residual sums, mode 2 also the
       // QKV projection of layers >= 1 (then unfused); mode 3 keeps QKV + attention in fp16 (K5c)
-      const bool ffn1_8 = fp8_ >= 2, qkv_8 = fp8_ == 2;
+      // mode 4 = mode 3 + the QKV projection of layers >= 1 in fp8 on an e4m3 copy of the
+      // NORMALISED rows (u - mu) rstd (its own pass after the row statistics; unfused)
+      const bool ffn1_8 = fp8_ >= 2, qkv_8 = fp8_ == 2 || fp8_ == 4, qkv_norm8 = fp8_ == 4;
       const bool fuse_qa = fused_qkv_attention_enabled() && !qkv_8 && qkv_attention_supported(S, d, H);
       // (qkv_8: mode 2 keeps the e4m3 QKV path in every layer)
       const bool kvfree = cls_only && !qkv_8 && kvfree_cls_enabled() && layers_.size() > 1 &&
@@ -380,9 +388,11 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         } else if (l == 0) {
           launch_gemm(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
                       3 * d, M, 3 * d, d, s);
-        } else if (qkv_8) {  // A = e4m3 copy of u (written by the previous FFN2)
+        } else if (qkv_8) {  // A = e4m3 copy of u (mode 2: by the previous FFN2) or of the
+                             // normalised rows (mode 4: quantize_norm_fp8, (mu, rstd) = (0, 1))
           LnFold lq;
-          lq.mr = mB;
+          lq.mr = qkv_norm8 ? unit_mr_.as<float>() : mB;
+          lq.stat_ld = qkv_norm8 ? 0 : 1;
           lq.colsum = L.cqkv8.as<float>();
           lq.wexp = L.wqkve.as<uint8_t>();
           launch_gemm_f8w(EPI_LNF_F16, u8, d, L.wqkv8.as<uint8_t>(), L.dqkv.as<float>(), nullptr, 0,
@@ -460,7 +470,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         l2.gamma = L.ln1g.as<float>();
         l2.stat_out = sB;
         l2.wexp = L.w2e.as<uint8_t>();
-        l2.y8 = (qkv_8 && !last) ? u8 : nullptr;  // e4m3 copy of u2 for the next fp8 QKV
+        l2.y8 = (qkv_8 && !qkv_norm8 && !last) ? u8 : nullptr;  // e4m3 copy of u2 for the next fp8 QKV
         if (fp8_)  // ffn holds e4m3 bytes (F per row)
           launch_gemm_f8w(l2.y8 ? EPI_LNR16_STATS_Y8 : EPI_LNR16_STATS, reinterpret_cast<const uint8_t*>(ffn), F,
                           L.w2_8.as<uint8_t>(), L.b2_f.as<float>(), Uo, d, Uo, d, Mr, d, F, s, &l2);
@@ -468,6 +478,7 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
           launch_gemm(EPI_LNR16_STATS, ffn, F, L.w2h.as<half_t>(), L.b2_f.as<float>(), Uo, d, Uo,
                       d, Mr, d, F, s, &l2);
         launch_ln_stats_finalize(sB, nparts, cfg_.ln_eps, Mr, mB, s);
+        if (qkv_norm8 && l + 1 < layers_.size()) launch_quantize_norm_fp8(Uo, d, mB, Mr, d, u8, s);
       }
       // final LayerNorm (LN2 of the last block) of the rows that are consumed -> h16
       const Layer& Lz = layers_.back();

@@ -330,6 +330,34 @@ __global__ __launch_bounds__(256) void ln_apply_kernel(const half_t* __restrict_
   }
 }
 
+// e4m3 copy of the LayerNorm-NORMALISED residual rows x = (u - mu) rstd (fp8 mode 4's QKV operand:
+// the un-normalised u quantised directly loses its centred part to the common offset).  One wave
+// per row, 4 columns per lane and step; saturates at +-448 like e4m3x4.
+__global__ __launch_bounds__(256) void quantize_norm_fp8_kernel(const half_t* __restrict__ u, int64_t ldu,
+                                                                const float* __restrict__ mr, int M, int d,
+                                                                uint8_t* __restrict__ x8) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const float mu = mr[2 * m], rstd = mr[2 * m + 1];
+  for (int c = lane; c < (d >> 2); c += 64) {
+    const half4 hv = reinterpret_cast<const half4*>(u + m * ldu)[c];
+    reinterpret_cast<uint32_t*>(x8 + m * d)[c] =
+        e4m3x4(((float)hv[0] - mu) * rstd, ((float)hv[1] - mu) * rstd, ((float)hv[2] - mu) * rstd,
+               ((float)hv[3] - mu) * rstd);
+  }
+}
+
+void launch_quantize_norm_fp8(const half_t* u, int64_t ldu, const float* mr, int M, int d, uint8_t* x8,
+                              hipStream_t s) {
+  SR_CHECK(d % 4 == 0, "quantize_norm_fp8: hidden must be a multiple of 4");
+  if (M <= 0) return;
+  ProfScope prof("quantize_norm_fp8", s, 0.0, (double)M * d * 3.0);
+  hipLaunchKernelGGL(quantize_norm_fp8_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, u, ldu,
+                     mr, M, d, x8);
+  SR_LAUNCH_CHECK();
+}
+
 __global__ void scale_f16_kernel(const half_t* in, float scale, half_t* out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) out[i] = (half_t)((float)in[i] * scale);

@@ -142,6 +142,9 @@ void launch_ln_stats_finalize(const float* stat, int nparts, float eps, int M, f
 void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float* gamma,
                      const float* beta, int M, int d, half_t* h16, hipStream_t s);
 void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s);
+// fp8 mode 4: e4m3 copy of the normalised rows (u - mu) rstd (k_encoder_misc.hip)
+void launch_quantize_norm_fp8(const half_t* u, int64_t ldu, const float* mr, int M, int d, uint8_t* x8,
+                              hipStream_t s);
 // K/V-free CLS-only last layer (k_encoder_misc.hip): block-diagonal K / V weights from the folded
 // QKV weight, and per sequence scores + softmax + z' = sum_j p_j rstd_j (u_j - mu_j)
 bool cls_attn_fold_supported(int S, int D, int H);

@@ -228,7 +228,8 @@ class Encoder {
   // [fp16(W) | fp16(W - fp16(W))] and the GEMMs run K = 2 K_x over the repeated activation, which
   // removes the fp16 weight rounding (~9e-4 of the 1.1e-3 embedding error of 24-layer bge-m3)
   bool split_ = false;
-  DevBuf u8_;  // e4m3 copy of the residual sums (fp8 mode 2)
+  DevBuf u8_;  // e4m3 copy of the residual sums (fp8 modes 2 / 3) or normalised rows (mode 4)
+  DevBuf unit_mr_;  // (mu, rstd) = (0, 1): fp8 mode 4 QKV statistics (stat_ld 0)
   int64_t ws_tokens_ = 0;
 };
 

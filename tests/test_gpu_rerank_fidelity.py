@@ -158,7 +158,7 @@ def test_pipeline_rerank_path_ranks_like_the_oracle(fidelity):
         assert np.abs(logits[b] - ref[b][got_j]).max() * RATIO_MIN <= std[b], b
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 def test_fp8_modes_top10_agreement(fidelity, mode):
     """The opt-in fp8 precision modes (1: FFN2 on e4m3; 2: also FFN1 and QKV; 3: FFN1 + FFN2, QKV
     fp16) against the fp32
