@@ -348,16 +348,6 @@ __global__ __launch_bounds__(256) void quantize_norm_fp8_kernel(const half_t* __
   }
 }
 
-void launch_quantize_norm_fp8(const half_t* u, int64_t ldu, const float* mr, int M, int d, uint8_t* x8,
-                              hipStream_t s) {
-  SR_CHECK(d % 4 == 0, "quantize_norm_fp8: hidden must be a multiple of 4");
-  if (M <= 0) return;
-  ProfScope prof("quantize_norm_fp8", s, 0.0, (double)M * d * 3.0);
-  hipLaunchKernelGGL(quantize_norm_fp8_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, u, ldu,
-                     mr, M, d, x8);
-  SR_LAUNCH_CHECK();
-}
-
 __global__ void scale_f16_kernel(const half_t* in, float scale, half_t* out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) out[i] = (half_t)((float)in[i] * scale);
@@ -478,6 +468,16 @@ void launch_ln_apply(const half_t* u, int64_t ldu, const float* mr, const float*
   ProfScope prof("ln_apply", s, 0.0, (double)M * d * 4.0);
   hipLaunchKernelGGL(ln_apply_kernel<MAXV>, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, u, ldu,
                      mr, gamma, beta, M, d, h16);
+  SR_LAUNCH_CHECK();
+}
+
+void launch_quantize_norm_fp8(const half_t* u, int64_t ldu, const float* mr, int M, int d, uint8_t* x8,
+                              hipStream_t s) {
+  SR_CHECK(d % 4 == 0, "quantize_norm_fp8: hidden must be a multiple of 4");
+  if (M <= 0) return;
+  ProfScope prof("quantize_norm_fp8", s, 0.0, (double)M * d * 3.0);
+  hipLaunchKernelGGL(quantize_norm_fp8_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, s, u, ldu,
+                     mr, M, d, x8);
   SR_LAUNCH_CHECK();
 }
 

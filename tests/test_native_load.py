@@ -51,3 +51,17 @@ def test_error_codes_and_messages_without_device():
     assert lib.sr_store_count(None, None, None) == _native.SR_ERR_INVALID
     stats = _native.profile_read()
     assert isinstance(stats, dict)
+
+
+def test_library_has_no_unresolved_internal_symbols():
+    """Every sr:: symbol the library references is defined in it: a launcher left inside an
+    anonymous namespace links into the .so as an undefined symbol (lazy binding then fails only
+    when the path is first called, on the GPU box)."""
+    import shutil
+    import subprocess
+    from super_rag_amd import _native
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--undefined-only", _native.library_path()], capture_output=True,
+                         text=True, check=True).stdout
+    bad = [l.split()[-1] for l in out.splitlines() if "_ZN2sr" in l]
+    assert not bad, bad
