@@ -796,6 +796,51 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
       }
       __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
     }
+  } else if constexpr (OUT8 && SR_GEMM_GELU_LINE) {
+    // ---- fp8 (e4m3 bytes): per (half, row group) the 16 rows x 64 B pass through 1 KiB of the
+    // scratch (16-B chunk c of row r at c ^ (r & 3)) and leave as ONE dwordx4 store: 8 stores
+    // per wave instead of 16 x dwordx2 (the store cost here is per instruction, not per byte)
+    uint8_t* const sb = reinterpret_cast<uint8_t*>(scr);
+    float4v bc[2][4];
+    load_consts(bc[0], 0);
+    load_consts(bc[1], 1);
+    if constexpr (!std::is_same<Pre, NoPre>::value) {
+      __builtin_amdgcn_sched_barrier(0);
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1) {
+        load_consts(bc[0], 2);
+        load_consts(bc[1], 3);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          float v[8];
+          gelu8(v, 2 * h + pp, j, bc[pp]);
+          uint2 q8;
+          q8.x = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
+              v[2], v[3], __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false), true);
+          q8.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
+              v[6], v[7], __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false), true);
+          const int ln = lane_id_here(), gl = ln >> 4, row = ln & 15;
+          const int k8 = 4 * pp + 2 * (gl & 1) + (gl >> 1);      // 8-B chunk of the 64-B row
+          *reinterpret_cast<uint2*>(sb + row * 64 + ((((k8 >> 1) ^ (row & 3)) << 4) | ((k8 & 1) << 3))) = q8;
+        }
+        const int ln = lane_id_here(), c = ln & 3, rr = ln >> 2;
+        const uint4 o = *reinterpret_cast<const uint4*>(sb + rr * 64 + ((c ^ (rr & 3)) << 4));
+        if constexpr (DMODE == 5) {
+          if (o.x == 0x12345678u) reinterpret_cast<uint32_t*>(Y)[ln] = o.y;
+        } else if (!CHECK || mw0 + j * 16 + rr < M) {
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)(mw0 + j * 16 + rr) * ldy +
+                                    nw0 + 64 * h + 16 * c) = o;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
+    }
   } else {
     // ---- column-group outer, one 8- / 16-byte store per (p, j) -----------------------------------
     float4v bc[2][4];  // [buffer][b0, b1, c0, c1] of column group p
@@ -844,7 +889,9 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
 template <int EPI>
 struct PipeEpi {
   static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
-  static constexpr int NSTORE = WIDE ? 16 : 32;
+  // (the fp8-output FFN1 epilogue through its scratch: 8 x 16-B stores, 16 rows x 64 B each)
+  static constexpr int NSTORE = (EPI == EPI_LNF_GELU_F8 && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE && SR_GEMM_GELU_LUT)
+                                    ? 8 : WIDE ? 16 : 32;
   template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
                                              int N, const float* __restrict__ bias,
@@ -1046,7 +1093,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // and the 32-bit-output epilogues index the rows as staged)
   constexpr bool PERMW = SR_GEMM_PERMW && PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
   // GLINE: the fp16 FFN1 epilogue's 2 KiB per-wave line scratch (store_tile_gelu)
-  constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE && EPI == EPI_LNF_GELU_F16;
+  constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE &&
+                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
                                                      (SCAN ? 512 : 0) + (GLUT ? 4 * GTAB : 0)];
   float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0));
@@ -1227,10 +1275,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     SR_INTERLEAVE(4);
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
     if (lenient) {
-      if constexpr (PipeEpi<EPI>::NSTORE == 16)
-        SR_WAITCNT(16, 0);
-      else
-        SR_WAITCNT(32, 0);
+      SR_WAITCNT(PipeEpi<EPI>::NSTORE, 0);
     } else
       SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
@@ -1284,6 +1329,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         for (int j = 0; j < 4; ++j) acc[2 * q + i][j] = mfma8(use[i], fb[j], acc[2 * q + i][j], sa[2 * q + i], F8W ? 127 : 119);
       SR_INTERLEAVE8(4);
     }
+    // (the fp8 K-step waits for everything, the previous tile's epilogue stores included: a
+    // lenient first K-step -- a runtime choice, or a peeled constant one -- spilled 48-112 B in
+    // every fp8 kernel at 256 VGPRs)
     (void)lenient;
     SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
@@ -1460,17 +1508,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     // (group 1: its K-step 1 glds too, awaited in K-step 0).  Unchecked tiles: wait for all.
     if (!full)
       SR_WAITCNT(0, 15);
-    else if constexpr (PipeEpi<EPI>::NSTORE == 16) {
-      if (grp == 0)
-        SR_WAITCNT(16, 15);
-      else
-        SR_WAITCNT(32, 15);
-    } else {
-      if (grp == 0)
-        SR_WAITCNT(32, 15);
-      else
-        SR_WAITCNT(48, 15);
-    }
+    else if (grp == 0)  // (group 1: its K-step 1 glds too, awaited in K-step 0)
+      SR_WAITCNT(PipeEpi<EPI>::NSTORE, 15);
+    else
+      SR_WAITCNT(PipeEpi<EPI>::NSTORE + 16, 15);
     __builtin_amdgcn_s_barrier();
     stores_pending = full;
     t = t_next;
