@@ -196,13 +196,13 @@ class DropinProcs:
     processes before the bench initialises the GPU; release() lets them set up and measure the
     same window together, collect() sums their throughput and pools their request latencies."""
 
-    def __init__(self, n, rows, seconds):
+    def __init__(self, n, rows, seconds, script=None):
         import tempfile
         self.dir = tempfile.mkdtemp(prefix="sr_dropin_")
         self.go = os.path.join(self.dir, "go.json")
         self.procs = []
         for i in range(n):
-            cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "bench_dropin.py"),
+            cmd = [sys.executable, "-u", script or os.path.join(ROOT, "tools", "bench_dropin.py"),
                    "--rows", str(rows), "--concurrency", "64", "--seconds", str(seconds),
                    "--go-file", self.go, "--lat-out", os.path.join(self.dir, f"lat{i}")]
             out = open(os.path.join(self.dir, f"p{i}.json"), "w")

@@ -100,3 +100,33 @@ def test_parse_defaults_and_config5_field_args(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "config5"])
     c = bench.parse()
     assert c.embed_model == "bge-m3" and c.no_cpu_baseline
+
+
+def test_dropin_procs_release_and_collect(tmp_path):
+    """bench.DropinProcs with a stand-in serving script (no GPU): the children wait for the go
+    file, start at its common time, and collect() sums their throughput and pools the latencies
+    of all of them for p50 / p99."""
+    script = tmp_path / "fake_dropin.py"
+    script.write_text(
+        "import argparse, json, os, sys, time\n"
+        "import numpy as np\n"
+        "sys.path.insert(0, %r)\n"
+        "from tools.bench_dropin import wait_for_go\n"
+        "ap = argparse.ArgumentParser()\n"
+        "for a in ('--rows', '--concurrency', '--seconds', '--go-file', '--lat-out'): ap.add_argument(a)\n"
+        "a = ap.parse_args()\n"
+        "t0 = wait_for_go(a.go_file, timeout_s=60)\n"
+        "assert abs(t0 - time.time()) < 30\n"
+        "i = int(a.lat_out[-1])\n"
+        "np.save(a.lat_out + '_c64.npy', np.full(100, 10.0 * (i + 1), np.float32))\n"
+        "print(json.dumps({'runs': [{'qps': 100.0 + i, 'requests': 100, 'seconds': 1.0, 'p50_ms': 1, 'p99_ms': 2,\n"
+        "                            'coalesced': {'rerank': {'mean_batch': 4.0}}}]}))\n" % bench.ROOT)
+    mp = bench.DropinProcs(3, 100, 1.0, script=str(script))
+    try:
+        mp.release(delay_s=0.5)
+        r = mp.collect(timeout_s=120)
+    finally:
+        mp.stop()
+    assert r["procs"] == 3 and r["qps"] == 303.0 and r["requests"] == 300
+    assert r["p50_ms"] == 20.0 and r["p99_ms"] == 30.0
+    assert not os.path.exists(mp.dir)
