@@ -194,6 +194,12 @@ int sr_lex_totals(sr_lex* x, int64_t* n_live, int64_t* sum_dl);
 int sr_lex_search_global(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
                          const uint8_t* allow, int64_t mask_key, const sr_lex_global* global,
                          float* out_score, int64_t* out_rows);
+/* The same with the exact 2^-16 fixed-point scores too (out_fixed, B x k uint32; score =
+ * out_fixed / 65536, 0 past the matches): fp32 rounds scores above 256, so a row-sharded
+ * collection merges its shards' lists on these to keep one index's (score, row) order. */
+int sr_lex_search_global_fixed(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                               const uint8_t* allow, int64_t mask_key, const sr_lex_global* global,
+                               float* out_score, int64_t* out_rows, uint32_t* out_fixed);
 int sr_lex_df(sr_lex* x, const int32_t* terms, int n, int64_t* out_df);
 /* Device outputs (B x k on the index's device, score fp32 / row int64 + row_offset; -inf / -1 past
  * the matches), asynchronous on `stream` after the host-side term preparation; global may be NULL

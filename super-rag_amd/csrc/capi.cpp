@@ -448,6 +448,23 @@ int sr_lex_search_global(sr_lex* x, const int64_t* qoff, const int32_t* qterms, 
   SR_API_END
 }
 
+int sr_lex_search_global_fixed(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int B, int k,
+                               const uint8_t* allow, int64_t mask_key, const sr_lex_global* global,
+                               float* out_score, int64_t* out_rows, uint32_t* out_fixed) {
+  SR_API_BEGIN
+  SR_NONNULL(x);
+  if (B > 0) {
+    SR_NONNULL(qoff);
+    SR_NONNULL(out_score);
+    SR_NONNULL(out_rows);
+    SR_NONNULL(out_fixed);
+    if (qoff[B] > 0) SR_NONNULL(qterms);
+  }
+  std::lock_guard<std::mutex> lk(x->impl->mu);
+  x->impl->search_host(qoff, qterms, B, k, allow, mask_key, out_score, out_rows, global, out_fixed);
+  SR_API_END
+}
+
 int sr_lex_totals(sr_lex* x, int64_t* n_live, int64_t* sum_dl) {
   SR_API_BEGIN
   SR_NONNULL(x);

@@ -335,7 +335,7 @@ struct LexSelSmem {
 __global__ __launch_bounds__(SEL_THREADS, 1) void lex_select_kernel(
     const uint64_t* __restrict__ keys, const int* __restrict__ kcnt,
     const int64_t* __restrict__ koff, int k, float* __restrict__ out_score,
-    int64_t* __restrict__ out_rows, int64_t row_offset) {
+    int64_t* __restrict__ out_rows, int64_t row_offset, uint32_t* __restrict__ out_fixed) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   LexSelSmem& S = *reinterpret_cast<LexSelSmem*>(smem_raw);
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -397,6 +397,9 @@ __global__ __launch_bounds__(SEL_THREADS, 1) void lex_select_kernel(
     const uint64_t kk = ok ? S.sh.sel[i] : 0ull;
     out_score[(int64_t)q * k + i] = ok ? (float)(uint32_t)(kk >> 32) / LEX_SCALE : -INFINITY;
     out_rows[(int64_t)q * k + i] = ok ? (int64_t)(0xffffffffu - (uint32_t)kk) + row_offset : -1;
+    // the exact 2^-16 fixed-point score (fp32 rounds it once it passes 2^24, a score of 256):
+    // what a sharded index merges on to keep one index's order
+    if (out_fixed) out_fixed[(int64_t)q * k + i] = ok ? (uint32_t)(kk >> 32) : 0u;
   }
 }
 
@@ -681,7 +684,7 @@ void LexIndex::df(const int32_t* terms, int n, int64_t* out) {
 void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k,
                           const uint8_t* allow, int64_t mask_key, float* out_score,
                           int64_t* out_rows, hipStream_t s, const sr_lex_global* glob,
-                          int64_t row_offset) {
+                          int64_t row_offset, uint32_t* out_fixed) {
   SR_CHECK(B >= 0, "lex.search: negative batch");
   SR_CHECK(k >= 1 && k <= SR_MAX_TOPK, "lex.search: top_k must be in [1, 1024]");
   if (B == 0) return;
@@ -810,7 +813,8 @@ void LexIndex::search_dev(const int64_t* qoff, const int32_t* qterms, int B, int
       ProfScope prof("lex_select", s, 0.0, (double)koff[(size_t)qb] * 8.0);
       hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), sizeof(LexSelSmem), s,
                          d_keys, d_cnt, d_ko, k, out_score + (int64_t)b0 * k,
-                         out_rows + (int64_t)b0 * k, row_offset);
+                         out_rows + (int64_t)b0 * k, row_offset,
+                         out_fixed ? out_fixed + (int64_t)b0 * k : nullptr);
       SR_LAUNCH_CHECK();
     }
     // the host vectors above back async copies: finish the block before they go away
@@ -902,7 +906,7 @@ void LexIndex::search_tok_dev(const int32_t* tok, const int32_t* qlen, int B, in
       ProfScope prof("lex_select", s, 0.0, 0.0);
       hipLaunchKernelGGL(lex_select_kernel, dim3(qb), dim3(SEL_THREADS), sizeof(LexSelSmem), s,
                          d_keys, d_cnt, d_ko, k, out_score + (int64_t)b0 * k,
-                         out_rows + (int64_t)b0 * k, row_offset);
+                         out_rows + (int64_t)b0 * k, row_offset, (uint32_t*)nullptr);
       SR_LAUNCH_CHECK();
     }
   }
@@ -911,17 +915,20 @@ void LexIndex::search_tok_dev(const int32_t* tok, const int32_t* qlen, int B, in
 
 void LexIndex::search_host(const int64_t* qoff, const int32_t* qterms, int B, int k,
                            const uint8_t* allow, int64_t mask_key, float* out_score,
-                           int64_t* out_rows, const sr_lex_global* glob) {
+                           int64_t* out_rows, const sr_lex_global* glob, uint32_t* out_fixed) {
   if (B == 0) return;
   SR_CHECK(out_score && out_rows, "lex.search: null output");
   DeviceGuard g(device_);
   const size_t ob = (size_t)B * k;
-  out_.reserve((size_t)round_up((int64_t)ob * 4, 16) + ob * 8);
+  const size_t o_rows = (size_t)round_up((int64_t)ob * 4, 16), o_fix = o_rows + ob * 8;
+  out_.reserve(o_fix + (out_fixed ? ob * 4 : 0));
   float* ds = out_.as<float>();
-  int64_t* dr = reinterpret_cast<int64_t*>(out_.as<char>() + round_up((int64_t)ob * 4, 16));
-  search_dev(qoff, qterms, B, k, allow, mask_key, ds, dr, stream_, glob);
+  int64_t* dr = reinterpret_cast<int64_t*>(out_.as<char>() + o_rows);
+  uint32_t* dfx = out_fixed ? reinterpret_cast<uint32_t*>(out_.as<char>() + o_fix) : nullptr;
+  search_dev(qoff, qterms, B, k, allow, mask_key, ds, dr, stream_, glob, 0, dfx);
   SR_HIP(hipMemcpyAsync(out_score, ds, ob * 4, hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipMemcpyAsync(out_rows, dr, ob * 8, hipMemcpyDeviceToHost, stream_));
+  if (out_fixed) SR_HIP(hipMemcpyAsync(out_fixed, dfx, ob * 4, hipMemcpyDeviceToHost, stream_));
   SR_HIP(hipStreamSynchronize(stream_));
 }
 

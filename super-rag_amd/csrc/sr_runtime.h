@@ -249,7 +249,8 @@ class LexIndex {
   // on stream s) or the host
   void search_dev(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
                   int64_t mask_key, float* out_score, int64_t* out_rows, hipStream_t s,
-                  const sr_lex_global* glob = nullptr, int64_t row_offset = 0);
+                  const sr_lex_global* glob = nullptr, int64_t row_offset = 0,
+                  uint32_t* out_fixed = nullptr);
   // device-resident queries: tok [B, Lq] int32 (row stride Lq), qlen [B] int32, both in HBM.
   // query_stats_dev writes [n_live, sum_dl, df of every (query, position)] (2 + B Lq int64, the
   // vector a row-sharded corpus sums over its shards); search_tok_dev scores with those summed
@@ -263,7 +264,7 @@ class LexIndex {
   void df(const int32_t* terms, int n, int64_t* out);
   void search_host(const int64_t* qoff, const int32_t* qterms, int B, int k, const uint8_t* allow,
                    int64_t mask_key, float* out_score, int64_t* out_rows,
-                   const sr_lex_global* glob = nullptr);
+                   const sr_lex_global* glob = nullptr, uint32_t* out_fixed = nullptr);
   void stats(int64_t* rows, int64_t* live, int64_t* postings, int64_t* vocab, double* avgdl);
   void save(const char* path);
   static LexIndex* load(const char* path, int device);

@@ -144,6 +144,8 @@ SIGNATURES = {
     "sr_diag_attention": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_void_p]),
     "sr_diag_copy": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "sr_lex_search_global_fixed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                           c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sr_diag_ffn1": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
 }

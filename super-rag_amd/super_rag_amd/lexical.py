@@ -177,24 +177,34 @@ class NativeLexIndex:
                 "vocab": v[3].value, "avgdl": a.value}
 
     def search(self, queries: Sequence[Sequence[int]], k: int, allow=None, mask_key: int = 0,
-               global_stats=None):
+               global_stats=None, fixed: bool = False):
         """BM25 top-k per query (token-id lists) -> (score [B,k] fp32 desc, rows [B,k] int64).
-        global_stats: (n_live, sum_dl, terms, df) of a whole row-sharded corpus (ShardedLex)."""
+        global_stats: (n_live, sum_dl, terms, df) of a whole row-sharded corpus (ShardedLex).
+        fixed: also return the exact 2^-16 fixed-point scores [B,k] uint32 (sr_lex_search_global_
+        fixed; the fp32 scores round above 256), the key a sharded merge orders by."""
         Bq = len(queries)
         scores = np.empty((Bq, k), dtype=np.float32)
         rows = np.empty((Bq, k), dtype=np.int64)
+        fx = np.zeros((Bq, k), dtype=np.uint32) if fixed else None
         if Bq == 0:
-            return scores, rows
+            return (scores, rows, fx) if fixed else (scores, rows)
         qoff, qterms = query_arrays(queries)
         a = None if allow is None else _mask(allow, self.stats()["rows"])
-        if global_stats is None:
-            N.call("sr_lex_search", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
-                   None if a is None else N.ptr(a), int(mask_key), N.ptr(scores), N.ptr(rows))
-        else:
+        g = None
+        if global_stats is not None:
             n_live, sum_dl, gt, gdf = global_stats
             gt = np.ascontiguousarray(gt, dtype=np.int32)
             gdf = np.ascontiguousarray(gdf, dtype=np.int64)
             g = LexGlobalC(int(n_live), int(sum_dl), gt.ctypes.data, gdf.ctypes.data, int(gt.size))
+        if fixed:
+            N.call("sr_lex_search_global_fixed", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+                   None if a is None else N.ptr(a), int(mask_key),
+                   None if g is None else ctypes.byref(g), N.ptr(scores), N.ptr(rows), N.ptr(fx))
+            return scores, rows, fx
+        if g is None:
+            N.call("sr_lex_search", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
+                   None if a is None else N.ptr(a), int(mask_key), N.ptr(scores), N.ptr(rows))
+        else:
             N.call("sr_lex_search_global", self._h, N.ptr(qoff), N.ptr(qterms), Bq, int(k),
                    None if a is None else N.ptr(a), int(mask_key), ctypes.byref(g), N.ptr(scores),
                    N.ptr(rows))
@@ -282,9 +292,9 @@ class ShardedLex:
     a fulltext / hybrid collection can span GPUs.  Every shard scores with the corpus-wide N,
     summed length and df of the query terms (sr_lex_search_global; the totals and df are summed on
     the host, as the connector's queries are host arrays), each shard's top-k is mapped to global
-    rows and the lists merge on (score desc, global row asc) -- one index's order, so results equal
-    a single-device collection's (exactly while a query's BM25 score stays below 256, where its
-    2^-16 fixed-point value is still exact in the fp32 score the shards report).  Global rows are
+    rows and the lists merge on (exact 2^-16 fixed-point score desc, global row asc) -- one
+    index's order, so results equal a single-device collection's for every score (the shards'
+    fp32 scores round above 256; sr_lex_search_global_fixed returns the exact ones).  Global rows are
     the store's: ``add`` must follow the store's add of the same rows (the connector's order)."""
 
     MAGIC = "SRMILEXSHARDS1"
@@ -378,19 +388,21 @@ class ShardedLex:
             a = None if allow is None else np.asarray(allow, dtype=np.uint8)[self.tables[s]]
             # a shard's device mask cache is keyed per shard (0 = never cached)
             mk = (int(mask_key) << 6) | s if (a is not None and mask_key) else 0
-            sc, r = sh.search(queries, k, allow=a, mask_key=mk, global_stats=st)
+            # merged on the exact fixed-point scores (fp32 rounds them above 256, where a merge
+            # on fp32 would order two distinct scores by row): one index's order for every score
+            sc, r, fx = sh.search(queries, k, allow=a, mask_key=mk, global_stats=st, fixed=True)
             t = self.tables[s]
             g = np.where(r >= 0, t[np.clip(r, 0, None)] if len(t) else -1, -1)
-            scores.append(np.where(g >= 0, np.asarray(sc, np.float32), -np.inf))
+            scores.append(np.where(g >= 0, np.asarray(fx, np.int64), -1))
             rows.append(g)
         S, R = np.concatenate(scores, 1), np.concatenate(rows, 1)
         out_s = np.full((Bq, k), -np.inf, np.float32)
         out_r = np.full((Bq, k), -1, np.int64)
         for b in range(Bq):
             big = np.where(R[b] >= 0, R[b], np.iinfo(np.int64).max)
-            o = np.lexsort((big, -S[b].astype(np.float64)))[:k]
+            o = np.lexsort((big, -S[b]))[:k]
             ok = R[b][o] >= 0
-            out_s[b, : ok.sum()] = S[b][o][ok]
+            out_s[b, : ok.sum()] = S[b][o][ok].astype(np.float32) / np.float32(65536.0)
             out_r[b, : ok.sum()] = R[b][o][ok]
         return out_s, out_r
 

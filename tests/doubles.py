@@ -135,14 +135,22 @@ class NumpyLex:
         return np.asarray([int(c.df[t]) if 0 <= t < c.vocab else 0 for t in np.asarray(terms).tolist()],
                           np.int64)
 
-    def search(self, queries, k, allow=None, mask_key=0, global_stats=None):
-        from oracle.bm25 import bm25_topk
+    def search(self, queries, k, allow=None, mask_key=0, global_stats=None, fixed=False):
+        from oracle.bm25 import bm25_fixed_scores, bm25_topk
         st = None
         if global_stats is not None:
             n_live, sum_dl, gt, gdf = global_stats
             d = dict(zip(np.asarray(gt).tolist(), np.asarray(gdf).tolist()))
             st = (n_live, sum_dl, d.__getitem__)
-        return bm25_topk(self._corpus(), queries, k, allow=allow, stats=st)
+        scores, rows = bm25_topk(self._corpus(), queries, k, allow=allow, stats=st)
+        if not fixed:
+            return scores, rows
+        fx = np.zeros(rows.shape, np.uint32)
+        for i, q in enumerate(queries):
+            acc = bm25_fixed_scores(self._corpus(), q, 1.2, 0.75, allow, st)
+            ok = rows[i] >= 0
+            fx[i, ok] = acc[rows[i][ok]]
+        return scores, rows, fx
 
     def hybrid(self, store, queries, query_terms, k, k_each=None, rank_const=1,
                min_score=float("-inf"), allow=None, mask_key=0):

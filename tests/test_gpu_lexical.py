@@ -273,3 +273,31 @@ def test_device_stats_of_two_shards_equal_one_index():
         m = int((ro[i] >= 0).sum())
         np.testing.assert_array_equal(got_r, ro[i][:m])
         np.testing.assert_array_equal(got_s, so[i][:m])
+
+
+def test_fixed_point_scores_exact_above_256():
+    """sr_lex_search_global_fixed: the 2^-16 fixed-point scores equal the oracle's integers, on
+    queries whose BM25 scores pass 256 (many rare query terms repeated in one document), where
+    the fp32 scores round; and the fp32 scores are those integers / 65536 rounded once."""
+    from oracle.bm25 import bm25_fixed_scores, bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(11)
+    n, vocab = 4000, 2000
+    docs = _docs(rng, n, vocab)
+    rare = list(range(vocab, vocab + 40))          # terms in exactly one document each
+    for i, t in enumerate(rare):
+        docs[7 + (i % 3)] = docs[7 + (i % 3)] + [t] * 3
+    lex = NativeLexIndex()
+    lex.add(docs)
+    qs = [rare[:12], rare[:40] * 3, rare[3:30] + [5, 6], [1, 2, 3]]
+    s, r, fx = lex.search(qs, 10, fixed=True)
+    corpus = _oracle(docs, np.ones(n, bool))
+    so, ro = bm25_topk(corpus, qs, 10)
+    np.testing.assert_array_equal(r, ro)
+    np.testing.assert_array_equal(s, so)
+    for b, q in enumerate(qs):
+        acc = bm25_fixed_scores(corpus, q, 1.2, 0.75, None, None)
+        ok = r[b] >= 0
+        np.testing.assert_array_equal(fx[b][ok], acc[r[b][ok]].astype(np.uint32))
+        np.testing.assert_array_equal(s[b][ok], fx[b][ok].astype(np.float32) / np.float32(65536))
+    assert s[1].max() > 256.0                       # the test reaches the rounding range

@@ -172,3 +172,40 @@ def test_sharded_fulltext_and_hybrid_collections_equal_one_device(mode, tmp_path
         V.set_store_backend(V._native_store, V._native_load)
         V.set_lex_backend(V._native_lex, V._native_lex_load)
         lexical.set_rrf_backend(None)
+
+
+def test_sharded_bm25_merges_on_exact_fixed_point_scores():
+    """ADVICE r3: above a BM25 score of 256 distinct 2^-16 fixed-point scores share one fp32 value;
+    the sharded merge orders by the exact fixed-point score (then global row), as one index does,
+    not by row among equal fp32 scores."""
+    import numpy as np
+    from super_rag_amd import lexical
+
+    big = (300 << 16)                       # score 300: fp32 spacing there is 2^-15 > 2^-16
+    assert np.float32(big) == np.float32(big + 1)
+
+    class Shard:
+        def __init__(self, fx, rows):
+            self.fx, self.rows = np.asarray([fx], np.uint32), np.asarray([rows], np.int64)
+
+        def totals(self):
+            return 10, 100
+
+        def df(self, terms):
+            return np.ones(len(terms), np.int64)
+
+        def search(self, queries, k, allow=None, mask_key=0, global_stats=None, fixed=False):
+            assert fixed
+            sc = self.fx.astype(np.float32) / np.float32(65536)
+            return sc[:, :k], self.rows[:, :k], self.fx[:, :k]
+
+    class Store:
+        devices = [0, 1]
+
+    # shard 0 holds global row 0 with the LOWER exact score, shard 1 global row 5 with the higher
+    s0, s1 = Shard([big, 7 << 16], [0, 1]), Shard([big + 1, 0], [0, -1])
+    lex = lexical.ShardedLex(Store(), _shards=[s0, s1],
+                             _tables=[np.asarray([0, 2], np.int64), np.asarray([5], np.int64)])
+    sc, rows = lex.search([[3, 4]], 3)
+    assert rows[0].tolist() == [5, 0, 2]
+    assert sc[0].tolist() == [np.float32(big + 1) / 65536, np.float32(big) / 65536, 7.0]
