@@ -18,6 +18,7 @@ Reference call sites replaced: embedding_service.py:168-175, seekdb_connector.py
 rerank_service.py:95-104.
 """
 import gc
+import os
 
 import numpy as np
 import pytest
@@ -41,6 +42,8 @@ RERANK_TOL = 1.5e-3
 # and the MEAN |logit - ref| over the 400 logits (measured 1.9e-4): a
 # systematic drift fails here even while every single logit stays under RERANK_TOL
 RERANK_MEAN_TOL = 3e-4
+# the default K/V-free last layer against the SR_KVFREE_CLS=0 path on the same pairs
+KVFREE_TOL = 3e-4
 
 
 def _free():
@@ -220,6 +223,18 @@ def test_config3_rerank_top100_to_10_over_1m(corpus_1m, fp32_highest):
           f"{lg_ref.std():.2e}, max |logit| {np.abs(lg_ref).max():.2e}")
     assert dlog <= RERANK_TOL
     assert dmean <= RERANK_MEAN_TOL
+    # the K/V-free CLS-only last layer against the K, V GEMM + CLS attention path on the same
+    # pairs: a rounding-order change only, measured <= 2.1e-4
+    os.environ["SR_KVFREE_CLS"] = "0"
+    try:
+        lg_kv = rer.cross_score_dev(*[torch.from_numpy(np.ascontiguousarray(a)).cuda().int()
+                                      for a in (pids, pmask)])[:, 0].view(nq, 100).cpu().numpy()
+    finally:
+        del os.environ["SR_KVFREE_CLS"]
+    dkv = np.abs(lg - lg_kv).max()
+    print(f"config3 rerank: K/V-free vs K/V last layer max |dlogit| {dkv:.2e}, K/V path vs ref "
+          f"{np.abs(lg_kv - lg_ref).max():.2e}")
+    assert dkv <= KVFREE_TOL
     final, flog = res.rows.cpu().numpy(), res.logits.cpu().numpy()
     for b in range(nq):
         order = sorted(range(100), key=lambda j: (-lg_ref[b, j], j))[:10]
