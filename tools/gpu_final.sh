@@ -1,7 +1,8 @@
 #!/bin/bash
 # Final-tree evidence, tag $1 (e.g. r03g), part $2:
 #   1  the driver's own commands: GPU tests, smoke, default bench 20 / 5
-#   2  rocprofv3 kernel trace + PMC passes of the bench (tools/profile_round.sh), config 5, fp8 mode 3
+#   2  rocprofv3 kernel trace + PMC passes of the bench (tools/profile_round.sh), config 5, fp8 modes
+#      3 / 4, the bench with bge-reranker-v2-m3 (24 layers) as the reranker
 TAG=${1:?tag}; PART=${2:?part}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG
 if [ "$PART" = 1 ]; then
@@ -19,5 +20,7 @@ else
   find gpurun_out/prof_$TAG -name "*.csv" -size +1M -delete
   timeout -k 10 400 python -u bench.py --workload config5 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/$TAG/bench_config5.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --fp8 3 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/$TAG/bench_fp8m3.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py --fp8 4 --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/$TAG/bench_fp8m4.log 2>&1 || exit 1
+  timeout -k 10 400 python -u bench.py --rerank-model bge-reranker-v2-m3 --steps 5 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/$TAG/bench_v2m3.log 2>&1 || exit 1
 fi
 exit 0
