@@ -832,35 +832,49 @@ def pmc_file(root=ROOT):
         return os.path.relpath(files[-1], root), json.load(f)
 
 
+# ProfScope names (the bench's kernel table) that differ from the logical names tools/pmc_traffic.py
+# derives from the mangled kernel names (the same kernels)
+PMC_ALIASES = {"cls_attn_fold1": "cls_attn_fold", "cosine_scan_dense": "cosine_scan"}
+
+
+def _pmc_name(k):
+    return PMC_ALIASES.get(k, k)
+
+
 def pmc_provenance(run_kernels, root=ROOT):
     """Which PMC summary the roofline's `traffic` / `pmc_*` fields come from and whether it
     describes THIS run: the summary's commit and native-source fingerprint (recorded on the box by
-    tools/profile_round.sh) against the running tree's, and its kernel set against the kernels
-    timed here.  stale = the sources differ, or the kernel sets differ (another workload / precision
-    mode, or kernels added or removed since): the counters then describe other code, so the
-    roofline reports traffic null and keeps the stale numbers beside it."""
+    tools/profile_round.sh) against the running tree's, and the kernels timed here against the
+    summary's (names normalised through PMC_ALIASES; the summary also holds setup kernels the
+    timed region does not launch, which is no difference).  stale = the sources differ, or a kernel
+    timed here is missing from the summary (another workload / precision mode, or kernels added
+    since): the counters then describe other code, so the roofline reports traffic null and keeps
+    the stale numbers beside it."""
     path, d = pmc_file(root)
     if d is None:
         return None
-    mine = set(run_kernels)
-    theirs = set(d.get("kernels", {}))
+    mine = {_pmc_name(k) for k in run_kernels}
+    theirs = {_pmc_name(k) for k in d.get("kernels", {})}
     fp = d.get("source_sha256")
     src_match = None if fp is None else fp == source_fingerprint(root)
+    missing = sorted(mine - theirs)
     reasons = []
     if src_match is False:
         reasons.append("native sources differ from the profiled tree")
-    if mine != theirs:
-        reasons.append(f"kernel sets differ (only here: {sorted(mine - theirs)}, only in the "
-                       f"summary: {sorted(theirs - mine)})")
+    if missing:
+        reasons.append(f"kernels timed here but absent from the summary: {missing}")
     return {"file": path, "commit": d.get("commit"), "source_sha256": fp,
-            "source_match": src_match, "kernel_set_match": mine == theirs,
+            "source_match": src_match, "kernel_set_match": not missing,
             "stale": bool(reasons), "stale_reasons": reasons}
 
 
 def pmc_record(kernel, root=ROOT):
     """The kernel's record in the newest committed PMC summary (tools/pmc_traffic.py), or None."""
     _, d = pmc_file(root)
-    return None if d is None else d["kernels"].get(kernel)
+    if d is None:
+        return None
+    ks = {_pmc_name(k): v for k, v in d["kernels"].items()}
+    return ks.get(_pmc_name(kernel))
 
 
 def pmc_traffic(kernel, root=ROOT):
@@ -871,7 +885,7 @@ def pmc_traffic(kernel, root=ROOT):
     path, d = pmc_file(root)
     if d is None:
         return None, None
-    k = d["kernels"].get(kernel)
+    k = pmc_record(kernel, root)
     if not k:
         return None, None
     return k["traffic_B"], (f"{path}: fetch {k['fetch_B']} B + write "

@@ -52,6 +52,18 @@ def test_kernel_set_difference_marks_stale(tmp_path):
     assert "pmc_clock_ghz" not in roof
 
 
+def test_setup_kernels_and_profscope_aliases_are_no_difference(tmp_path):
+    """The summary counts every library kernel of the profiled run (setup kernels such as
+    fold_ln_weight included) under the mangled-name logical names; the bench times its ProfScope
+    names (cls_attn_fold for cls_attn_fold1_kernel, cosine_scan_dense for the EPI_SCAN kernel)."""
+    root = _tree(tmp_path, ["gemm_a", "cosine_scan", "cls_attn_fold1", "fold_ln_weight"], None)
+    prov = bench.pmc_provenance(["gemm_a", "cosine_scan_dense", "cls_attn_fold"], root)
+    assert prov["kernel_set_match"] and not prov["stale"], prov
+    roof = {"bound": "hbm", "peak": 8000.0}
+    bench.apply_pmc(roof, "cosine_scan_dense", ["gemm_a", "cosine_scan_dense"], root)
+    assert roof["traffic"] == 120
+
+
 def test_source_change_marks_stale(tmp_path):
     root = _tree(tmp_path, ["gemm_a"], None)
     sha = bench.source_fingerprint(root)
