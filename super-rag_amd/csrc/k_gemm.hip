@@ -48,6 +48,10 @@
 #ifndef SR_GEMM_GELU_LINE
 #define SR_GEMM_GELU_LINE 1  // fp16 FFN1 epilogue: whole 128-B line stores through a 2 KiB scratch
 #endif
+#ifndef SR_GEMM_STATS_MODE
+#define SR_GEMM_STATS_MODE 2  // *_STATS epilogues' row partials: 0 two-pass M2, 1 one-pass fp32,
+                              // 2 one-pass v_dot2c_f32_f16 (A/B builds)
+#endif
 #ifndef SR_GEMM_GELU_LINE8
 #define SR_GEMM_GELU_LINE8 0  // fp8 FFN1 epilogue: 16-B row stores through 1 KiB of scratch (A/B:
                               // 8 stores per wave instead of 16, but the scratch exchange costs
@@ -578,10 +582,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         for (int r = 0; r < 8; ++r) v[r] += (float)r16[p][r];
       }
       if constexpr (LNR) {
+        // (r - mu) rstd as one FMA with -mu rstd (one VALU per output fewer than sub + mul)
+        const float nmr = -mu * rstd;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          v[r] = fmaf(((float)r16[p][r] - mu) * rstd, c0[p][r], v[r]);
-          v[4 + r] = fmaf(((float)r16[p][4 + r] - mu) * rstd, c1[p][r], v[4 + r]);
+          v[r] = fmaf(fmaf((float)r16[p][r], rstd, nmr), c0[p][r], v[r]);
+          v[4 + r] = fmaf(fmaf((float)r16[p][4 + r], rstd, nmr), c1[p][r], v[4 + r]);
         }
       }
       if constexpr (GELU) {
@@ -647,24 +653,55 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     }
     if constexpr (STATS) {
       // partner lanes (xor 16 / 32) share the row m, so they are active together
-      float sum = 0.f;
+      float sum = 0.f, m2 = 0.f;
+      if constexpr (SR_GEMM_STATS_MODE == 0) {  // two passes: M2 around the span's mean
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < 4; ++p)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) sum += (float)hv[p][r];
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      const float mw = sum * (1.f / 128.f);
-      float m2 = 0.f;
+          for (int r = 0; r < 8; ++r) sum += (float)hv[p][r];
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mw = sum * (1.f / 128.f);
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < 4; ++p)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float dx = (float)hv[p][r] - mw;
-          m2 = fmaf(dx, dx, m2);
+          for (int r = 0; r < 8; ++r) {
+            const float dx = (float)hv[p][r] - mw;
+            m2 = fmaf(dx, dx, m2);
+          }
+        m2 += __shfl_xor(m2, 16, 64);
+        m2 += __shfl_xor(m2, 32, 64);
+      } else {
+        // one pass: sum and sum of squares of the fp16 values (1: fp32 add + fma per value, 2:
+        // v_dot2c_f32_f16 per value pair -- the products of fp16 values are exact in fp32), then
+        // M2 = sq - sum^2 / 128 per 128-column span (fp32; the span's values are 128 different
+        // hidden dimensions, so sq / 128 is never within a few ulps of mean^2)
+        float sq = 0.f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          if constexpr (SR_GEMM_STATS_MODE == 2) {
+            typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+              const h2v x2 = {hv[p][r], hv[p][r + 1]};
+              sum = __builtin_amdgcn_fdot2(x2, h2v{(_Float16)1.f, (_Float16)1.f}, sum, false);
+              sq = __builtin_amdgcn_fdot2(x2, x2, sq, false);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const float x = (float)hv[p][r];
+              sum += x;
+              sq = fmaf(x, x, sq);
+            }
+          }
         }
-      m2 += __shfl_xor(m2, 16, 64);
-      m2 += __shfl_xor(m2, 32, 64);
+        sum += __shfl_xor(sum, 16, 64);
+        sq += __shfl_xor(sq, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        sq += __shfl_xor(sq, 32, 64);
+        m2 = fmaxf(fmaf(-sum * (1.f / 128.f), sum, sq), 0.f);
+      }
       if (g == 0 && (!CHECK || m_row < M)) {
         float2 st;
         st.x = sum;
