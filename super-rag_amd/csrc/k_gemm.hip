@@ -48,6 +48,9 @@
 #ifndef SR_GEMM_GELU_LINE
 #define SR_GEMM_GELU_LINE 1  // fp16 FFN1 epilogue: whole 128-B line stores through a 2 KiB scratch
 #endif
+#ifndef SR_GEMM_GELU_BUFST
+#define SR_GEMM_GELU_BUFST 1  // fp16 FFN1 line stores: lane-constant addresses + buffer stores
+#endif
 #ifndef SR_GEMM_STATS_MODE
 #define SR_GEMM_STATS_MODE 2  // *_STATS epilogues' row partials: 0 two-pass M2, 1 one-pass fp32,
                               // 2 one-pass v_dot2c_f32_f16 (A/B builds)
@@ -793,7 +796,67 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
       asm("" : "+v"(v[r]));
     }
   };
-  if constexpr (!OUT8 && SR_GEMM_GELU_LINE) {
+  if constexpr (!OUT8 && SR_GEMM_GELU_LINE && SR_GEMM_GELU_BUFST) {
+    // ---- fp16, whole-line stores through the 2 KiB scratch (16 rows x 128 B, chunk k of row r
+    // at k ^ (r & 7): conflict-free b128 writes and reads) --------------------------------------
+    // Every address is a lane constant computed once: the scratch write of pp = 0 (pp = 1 writes
+    // chunk k + 4, i.e. byte offset ^ 64: k < 4 and the swizzle XORs 3 bits), the scratch read
+    // (rows 8q + lane / 8, chunk lane & 7: q = 1 is + 1 KiB) and the row-group store offset
+    // (rows (lane / 8) (+ 8 q) x ldy, 16 B chunk lane & 7) against a buffer resource whose base is
+    // the row group's first output (SGPRs) and whose size ends at row M: rows past M are dropped by
+    // the range check (no compare / exec mask).  The per-store 64-bit address arithmetic and the
+    // recomputed swizzles were ~4 VALU per output, about a third of the epilogue's VALU.
+    float4v bc[2][4];  // bias / colsum of column groups 2h, 2h + 1
+    load_consts(bc[0], 0);
+    load_consts(bc[1], 1);
+    if constexpr (!std::is_same<Pre, NoPre>::value) {
+      __builtin_amdgcn_sched_barrier(0);
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    char* const sb = reinterpret_cast<char*>(scr);
+    const int ln0 = lane_id_here();
+    const uint32_t wofs = (uint32_t)((ln0 & 15) * 128 +
+                                     (((2 * ((ln0 >> 4) & 1) + (ln0 >> 5)) ^ (ln0 & 7)) << 4));
+    const uint32_t rofs = (uint32_t)((ln0 >> 3) * 128 + (((ln0 & 7) ^ (ln0 >> 3)) << 4));
+    const uint32_t gofs = (uint32_t)(((ln0 >> 3) * (int)ldy + (ln0 & 7) * 8) * 2);
+    const uint32_t g8 = (uint32_t)(8 * ldy * 2);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1) {
+        load_consts(bc[0], 2);
+        load_consts(bc[1], 3);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          float v[8];
+          gelu8(v, 2 * h + pp, j, bc[pp]);
+          half8 hv;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) hv[r] = (half_t)v[r];
+          *reinterpret_cast<half8*>(sb + (wofs ^ (uint32_t)(pp << 6))) = hv;
+        }
+        const int row0 = mw0 + j * 16;
+        const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldy * 2 : (int64_t)16 * ldy * 2;
+        const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(Y) + (int64_t)row0 * ldy + nw0 + 64 * h, nb);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const half8 o = *reinterpret_cast<const half8*>(sb + rofs + q * 1024);
+          if constexpr (DMODE == 5) {
+            if ((float)o[0] == 12345.f) reinterpret_cast<half_t*>(Y)[ln0] = o[1];
+          } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, 0);
+#endif
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
+    }
+  } else if constexpr (!OUT8 && SR_GEMM_GELU_LINE) {
     // ---- fp16, whole-line stores through the 2 KiB scratch (16 rows x 128 B, chunk k of row r
     // at k ^ (r & 7): conflict-free b128 writes and reads) --------------------------------------
     float4v bc[2][4];  // bias / colsum of column groups 2h, 2h + 1
@@ -1985,6 +2048,11 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
   const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
   lf.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;  // the product walk
+  {  // the product's walker de-phasing (SR_GEMM_STAGGER, launch_gemm)
+    const char* e = std::getenv("SR_GEMM_STAGGER");
+    const int st = e ? std::atoi(e) : 0;
+    lf.stagger = st > 0 ? std::max(1, st * K / 768) : 0;
+  }
   ProfScope prof(f8 ? "ffn1_diag_f8" : "ffn1_diag", stream, 2.0 * M * (double)N * K, 0.0);
   const half_t* x = reinterpret_cast<const half_t*>(X);
   const half_t* w = reinterpret_cast<const half_t*>(W);
