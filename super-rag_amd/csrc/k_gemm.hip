@@ -51,6 +51,12 @@
 #ifndef SR_GEMM_GELU_BUFST
 #define SR_GEMM_GELU_BUFST 1  // fp16 FFN1 line stores: lane-constant addresses + buffer stores
 #endif
+#ifndef SR_GEMM_WIDE_BUFST
+#define SR_GEMM_WIDE_BUFST 1  // wide LINE epilogues: lane-constant addresses + buffer loads / stores
+#endif
+#ifndef SR_GEMM_WIDE_BUFLD
+#define SR_GEMM_WIDE_BUFLD 1  // ... and the residual rows through buffer loads
+#endif
 #ifndef SR_GEMM_STATS_MODE
 #define SR_GEMM_STATS_MODE 2  // *_STATS epilogues' row partials: 0 two-pass M2, 1 one-pass fp32,
                               // 2 one-pass v_dot2c_f32_f16 (A/B builds)
@@ -437,15 +443,45 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     pre();
     __builtin_amdgcn_sched_barrier(0);
   }
+  // BUFST (LINE): lane-constant byte offsets -- the residual read of the lane's row
+  // in a 16-row group (+ 64 B per column group p: an immediate), the scratch write (column group p
+  // is offset ^ 64 p: chunk 4p + k0 XOR-swizzled by the row), the scratch read (rows 4q + lane /
+  // 16: offset ^ 64 q, + 1 KiB q) and the store offset within the row group (+ 8 ldy q bytes) --
+  // against buffer resources whose base is the row group's first element and whose range ends
+  // at row M (checked tiles: rows past M read zeros and are not stored)
+  // (recomputed per row group from a fresh lane id: hoisted over the whole epilogue, the four
+  // offsets spilled the residual epilogues at 256 VGPRs)
+  constexpr bool BUFST = LINE && SR_GEMM_WIDE_BUFST;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
+    uint32_t bo_res = 0, bo_wr = 0, bo_rd = 0, bo_st = 0;
+    if constexpr (BUFST) {
+      const int ln0 = lane_id_here(), l16 = ln0 & 15, l4 = ln0 >> 4;
+      bo_res = (uint32_t)((l16 * (int)ldr + 16 * (l4 & 1) + 4 * (l4 & 2)) * 2);
+      bo_wr = (uint32_t)(l16 * 256 + (((2 * (l4 & 1) + (l4 >> 1)) ^ l16) << 4));
+      bo_rd = (uint32_t)(l4 * 256 + ((l16 ^ l4) << 4));
+      bo_st = (uint32_t)((l4 * (int)ldy + l16 * 8) * 2);
+    }
+    (void)bo_res; (void)bo_wr; (void)bo_rd; (void)bo_st;
     const int m_row = mw0 + j * 16 + (lane & 15);
     // LINE: every lane takes part in the scratch exchange; rows past M compute on row M - 1's
     // operands and are never stored
     if (!LINE && CHECK && m_row >= M) continue;
     const int m = (LINE && CHECK && m_row >= M) ? M - 1 : m_row;
     half8 r16[(RESN || LNR) ? 4 : 1];
-    if constexpr ((RESN || LNR) && LINE) {
+    if constexpr ((RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD) {
+      const int row0 = mw0 + j * 16;
+      const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
+      const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        r16[p] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rr, bo_res + 64 * p, 0, 0));
+#else
+        (void)rr;
+#endif
+      }
+    } else if constexpr ((RESN || LNR) && LINE) {
       // residual row segments at offsets re-derived from the lane id where used (no hoisted
       // per-lane 64-bit addresses: they spill at 256 VGPRs); m is clamped to row M - 1
 #pragma unroll
@@ -534,7 +570,9 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
           hv[p][2 * q] = (half_t)x[q].x;
           hv[p][2 * q + 1] = (half_t)x[q].y;
         }
-        if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
+        if constexpr (BUFST) {
+          *reinterpret_cast<half8*>(reinterpret_cast<char*>(scr) + (bo_wr ^ (uint32_t)(p << 6))) = hv[p];
+        } else if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
           const int ln = lane_id_here(), gl = ln >> 4;
           *reinterpret_cast<half8*>(scr + (ln & 15) * 128 +
                                     (((4 * p + 2 * (gl & 1) + ((gl >> 1) & 1)) ^ (ln & 15)) << 3)) = hv[p];
@@ -616,7 +654,9 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
-        if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
+        if constexpr (BUFST) {
+          *reinterpret_cast<half8*>(reinterpret_cast<char*>(scr) + (bo_wr ^ (uint32_t)(p << 6))) = hv[p];
+        } else if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
           const int ln = lane_id_here(), gl = ln >> 4;
           *reinterpret_cast<half8*>(scr + (ln & 15) * 128 +
                                     (((4 * p + 2 * (gl & 1) + ((gl >> 1) & 1)) ^ (ln & 15)) << 3)) = hv[p];
@@ -634,7 +674,32 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       }
     }
     }
-    if constexpr (LINE) {
+    if constexpr (BUFST) {
+      const int row0 = mw0 + j * 16;
+      const int64_t nr = CHECK ? (int64_t)max(0, min(16, M - row0)) : 16;
+      const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(Y) + (int64_t)row0 * ldy + nw0, nr * ldy * 2);
+      const auto r8 = panel_rsrc(reinterpret_cast<const half_t*>(Y8 ? lf.y8 + (int64_t)row0 * ldy + nw0 : nullptr),
+                                 Y8 ? nr * ldy : 0);
+      (void)r8;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const half8 o = *reinterpret_cast<const half8*>(reinterpret_cast<const char*>(scr) +
+                                                        (bo_rd ^ (uint32_t)(q << 6)) + q * 1024);
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, bo_st + q * (uint32_t)(8 * ldy), 0, 0);
+        if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+          typedef int v2i __attribute__((ext_vector_type(2)));
+          const v2i q8 = {(int)e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]),
+                          (int)e4m3x4((float)o[4], (float)o[5], (float)o[6], (float)o[7])};
+          __builtin_amdgcn_raw_buffer_store_b64(q8, r8, (bo_st >> 1) + q * (uint32_t)(4 * ldy), 0, 0);
+        }
+#else
+        (void)o;
+        (void)ry;
+#endif
+      }
+    } else if constexpr (LINE) {
       // the row group's 16 x 128 columns were written to the scratch (chunk c of row r at
       // c ^ r: conflict-free b128 writes and reads); read back as rows 4q + (lane >> 4), chunk
       // lane & 15, so each store instruction writes 4 whole 256-B row segments
@@ -850,6 +915,10 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef int v4i __attribute__((ext_vector_type(4)));
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, 0);
+#else
+            (void)ry;
+            (void)gofs;
+            (void)g8;
 #endif
           }
         }
