@@ -958,35 +958,41 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
       const int m = m0 + tid;
       kbias[tid] = (m < M && mask[m < M ? m : M - 1] != 0) ? 0.f : -INFINITY;
     }
+    // column-group outer: the bias / column sums of a group are loaded once (not once per row
+    // group), and its LDS image address is one per lane -- the swizzles depend on the row only
+    // through (row >> 1) & 7, which a row group's 16 j does not change -- with the row groups at
+    // immediate offsets
     const int g = lane >> 4;
+    float2 mrj[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ml = wm * 64 + 16 * j + (lane & 15);
       const int mg = m0 + ml < M ? m0 + ml : M - 1;
-      float mu = 0.f, rstd = 1.f;
-      if constexpr (LNF) {
-        const float2 v = *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2);
-        mu = v.x;
-        rstd = v.y;
-      }
+      mrj[j] = LNF ? *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2) : make_float2(0.f, 1.f);
+    }
+    const int ml0 = wm * 64 + (lane & 15);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
-        const int seg = n >> 6, dim = n & 63;
-        const int col = seg * d + h * DH + dim;
-        const float4v b = *reinterpret_cast<const float4v*>(bias + col);
+    for (int i = 0; i < 6; ++i) {
+      const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
+      const int seg = n >> 6, dim = n & 63;
+      const int col = seg * d + h * DH + dim;
+      const float4v b = *reinterpret_cast<const float4v*>(bias + col);
+      float4v c = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (LNF) c = *reinterpret_cast<const float4v*>(colsum + col);
+      half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
+      const int chunk = seg == 2 ? a2_vswz(ml0, dim >> 3) : a2_kswz(ml0, dim >> 3);
+      half_t* const wp = img + ml0 * DH + chunk * 8 + (dim & 7);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
         half4 y;
         if constexpr (LNF) {
-          const float4v c = *reinterpret_cast<const float4v*>(colsum + col);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) y[r] = (half_t)fmaf(rstd, fmaf(-mu, c[r], acc[i][j][r]), b[r]);
+          for (int r = 0; r < 4; ++r) y[r] = (half_t)fmaf(mrj[j].y, fmaf(-mrj[j].x, c[r], acc[i][j][r]), b[r]);
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) y[r] = (half_t)(acc[i][j][r] + b[r]);
         }
-        half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
-        const int chunk = seg == 2 ? a2_vswz(ml, dim >> 3) : a2_kswz(ml, dim >> 3);
-        *reinterpret_cast<half4*>(img + ml * DH + chunk * 8 + (dim & 7)) = y;
+        *reinterpret_cast<half4*>(wp + j * 16 * DH) = y;
       }
     }
     __syncthreads();

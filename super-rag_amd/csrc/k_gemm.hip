@@ -57,6 +57,9 @@
 #ifndef SR_GEMM_WIDE_BUFLD
 #define SR_GEMM_WIDE_BUFLD 1  // ... and the residual rows through buffer loads
 #endif
+#ifndef SR_GEMM_GELU_BUFST8
+#define SR_GEMM_GELU_BUFST8 1  // fp8 FFN1 stores: range-checked buffer stores at lane offsets
+#endif
 #ifndef SR_GEMM_STATS_MODE
 #define SR_GEMM_STATS_MODE 2  // *_STATS epilogues' row partials: 0 two-pass M2, 1 one-pass fp32,
                               // 2 one-pass v_dot2c_f32_f16 (A/B builds)
@@ -1024,13 +1027,22 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
       pre();
       __builtin_amdgcn_sched_barrier(0);
     }
+    // fp8 (BUFST8): the e4m3 rows leave through a range-checked buffer resource per row group
+    // (rows past M dropped by the bounds check, no exec mask) at one lane offset per column group
+    constexpr bool B8 = OUT8 && SR_GEMM_GELU_BUFST8 && DMODE == 0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       if (p < 3) load_consts(bc[(p + 1) & 1], p + 1);
+      uint32_t bo8 = 0;
+      if constexpr (B8) {
+        const int ln0 = lane_id_here(), g0 = ln0 >> 4;
+        bo8 = (uint32_t)((ln0 & 15) * (int)ldy + 16 * (g0 & 1) + 4 * (g0 & 2) + 32 * p);
+      }
+      (void)bo8;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = mw0 + j * 16 + (lane & 15);
-        if (CHECK && m >= M) continue;
+        if (!B8 && CHECK && m >= M) continue;
         float v[8];
         gelu8(v, p, j, bc[p & 1]);
         if constexpr (DMODE == 5) {
@@ -1044,7 +1056,20 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
               v[2], v[3], __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false), true);
           q8.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
               v[6], v[7], __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false), true);
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+          if constexpr (B8) {
+            const int row0 = mw0 + j * 16;
+            const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldy : (int64_t)16 * ldy;
+            const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(reinterpret_cast<const uint8_t*>(Y) +
+                                                                       (int64_t)row0 * ldy + nw0), nb);
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef int v2i __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(v2i{(int)q8.x, (int)q8.y}, ry, bo8, 0, 0);
+#else
+            (void)ry;
+#endif
+          } else {
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = q8;
+          }
         } else {
           half8 hv;
 #pragma unroll
