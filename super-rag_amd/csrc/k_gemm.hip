@@ -60,6 +60,12 @@
 #ifndef SR_GEMM_GELU_BUFST8
 #define SR_GEMM_GELU_BUFST8 1  // fp8 FFN1 stores: range-checked buffer stores at lane offsets
 #endif
+#ifndef SR_GEMM_ST_AUX
+#define SR_GEMM_ST_AUX 2  // cache-policy bits of the FFN1 line stores: nt (streaming; A/B: 0, sc0, sc0 sc1)
+#endif
+#ifndef SR_GEMM_WST_AUX
+#define SR_GEMM_WST_AUX 0  // cache-policy bits of the wide epilogues' line stores (A/B builds)
+#endif
 #ifndef SR_GEMM_STATS_MODE
 #define SR_GEMM_STATS_MODE 2  // *_STATS epilogues' row partials: 0 two-pass M2, 1 one-pass fp32,
                               // 2 one-pass v_dot2c_f32_f16 (A/B builds)
@@ -690,7 +696,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
                                                         (bo_rd ^ (uint32_t)(q << 6)) + q * 1024);
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef int v4i __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, bo_st + q * (uint32_t)(8 * ldy), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, bo_st + q * (uint32_t)(8 * ldy), 0, SR_GEMM_WST_AUX);
         if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
           typedef int v2i __attribute__((ext_vector_type(2)));
           const v2i q8 = {(int)e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]),
@@ -917,7 +923,7 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
           } else {
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef int v4i __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, SR_GEMM_ST_AUX);
 #else
             (void)ry;
             (void)gofs;
