@@ -954,10 +954,12 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     half_t* Qi = lds;
     half_t* Ki = lds + QA_BM * DH;
     half_t* Vi = lds + 2 * QA_BM * DH;
-    if (tid < QA_BM) {
-      const int m = m0 + tid;
-      kbias[tid] = (m < M && mask[m < M ? m : M - 1] != 0) ? 0.f : -INFINITY;
-    }
+    // the key mask of the panel: loaded here, written to LDS after the image writes (its global
+    // load latency then overlaps the constant loads instead of preceding them)
+    // (every thread loads -- threads past QA_BM repeat a row -- so no branch merges the value
+    // and the load stays in flight until its use)
+    const int m_mk = m0 + (tid & (QA_BM - 1));
+    const int mkv = mask[m_mk < M ? m_mk : M - 1];
     // column-group outer: the bias / column sums of a group are loaded once (not once per row
     // group), and its LDS image address is one per lane -- the swizzles depend on the row only
     // through (row >> 1) & 7, which a row group's 16 j does not change -- with the row groups at
@@ -995,6 +997,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         *reinterpret_cast<half4*>(wp + j * 16 * DH) = y;
       }
     }
+    if (tid < QA_BM) kbias[tid] = (m_mk < M && mkv != 0) ? 0.f : -INFINITY;
     __syncthreads();
     const int t_next = t + t_step;
     const bool more = t_next < t_end;
