@@ -243,6 +243,27 @@ __global__ void lex_qstats_kernel(const int32_t* __restrict__ tok, const int32_t
   out[2 + i] = (p < qlen[q] && t >= 0 && t < T) ? off[t + 1] - off[t] : 0;
 }
 
+// lex_qcap_kernel: caps[q] = min(sum of the postings of query q's distinct terms, rows) -- the
+// candidate keys lex_qprep_kernel will reserve for it -- for a whole batch (one thread per query),
+// so a batch whose worst case does not fit one query group is grouped by its actual caps.
+__global__ void lex_qcap_kernel(const int32_t* __restrict__ tok, const int32_t* __restrict__ qlen,
+                                int B, int Lq, const int64_t* __restrict__ off, int64_t T,
+                                int64_t rows, int64_t* __restrict__ caps) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  const int32_t* tq = tok + (int64_t)q * Lq;
+  const int L = min(max(qlen[q], 0), Lq);
+  int64_t cap = 0;
+  for (int i = 0; i < L; ++i) {
+    const int32_t t = tq[i];
+    if (t < 0 || t >= T) continue;
+    bool first = true;
+    for (int j = 0; j < i && first; ++j) first = tq[j] != t;
+    if (first) cap += off[t + 1] - off[t];
+  }
+  caps[q] = cap < rows ? cap : rows;
+}
+
 // lex_qprep_kernel: one workgroup, thread q = query q of the group (G <= 1024).  Slot q Lq + i is
 // the query's i-th token if that is its FIRST occurrence of a term with postings here (start, len,
 // idf, multiplicity = occurrences in the query), else empty (len 0): the host path's slots in the
@@ -860,19 +881,49 @@ void LexIndex::search_tok_dev(const int32_t* tok, const int32_t* qlen, int B, in
     attr_set = true;
   }
   // keys per query <= min(Lq * max df, rows), known on the host without looking at the queries:
-  // query groups of G <= 1024 sized so the group's keys stay within LEX_KEY_BUDGET
+  // query groups of G <= 1024 sized so the group's keys stay within LEX_KEY_BUDGET.  A batch that
+  // fits one such group runs without a host round trip.  Otherwise (a stopword-like term makes the
+  // worst case the whole index: ~42 queries per group at 6.25M rows, a 2 GiB key workspace and
+  // bounds / score launches over padded slots) the actual per-query caps are computed on the
+  // device (lex_qcap_kernel), read back once, and the batch is grouped by them, as search_dev does.
   const int64_t per_q = std::max<int64_t>(1, std::min<int64_t>((int64_t)Lq * max_df_, rows_));
-  const int G = (int)std::max<int64_t>(1, std::min<int64_t>({1024, (int64_t)B, LEX_KEY_BUDGET / per_q}));
-  const int64_t nslots = (int64_t)G * Lq;
+  const int G_worst = (int)std::max<int64_t>(1, std::min<int64_t>({1024, (int64_t)B, LEX_KEY_BUDGET / per_q}));
+  std::vector<std::pair<int, int>> groups;  // (first query, queries)
+  int64_t keys_alloc = (int64_t)G_worst * per_q;
+  int G_alloc = G_worst;
+  if (B <= G_worst) {
+    groups.push_back({0, B});
+  } else {
+    caps_.reserve((size_t)B * 8);
+    hipLaunchKernelGGL(lex_qcap_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0, s, tok, qlen, B, Lq,
+                       off_.as<int64_t>(), vocab_, rows_, caps_.as<int64_t>());
+    SR_LAUNCH_CHECK();
+    std::vector<int64_t> cap((size_t)B);
+    SR_HIP(hipMemcpyAsync(cap.data(), caps_.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    SR_HIP(hipStreamSynchronize(s));
+    keys_alloc = 1;
+    G_alloc = 1;
+    for (int b0 = 0; b0 < B;) {
+      int qb = 0;
+      int64_t nkeys = 0;
+      while (b0 + qb < B && qb < 1024 && (qb == 0 || nkeys + cap[(size_t)(b0 + qb)] <= LEX_KEY_BUDGET))
+        nkeys += cap[(size_t)(b0 + qb++)];
+      groups.push_back({b0, qb});
+      keys_alloc = std::max<int64_t>(keys_alloc, nkeys);
+      G_alloc = std::max(G_alloc, qb);
+      b0 += qb;
+    }
+  }
+  const int64_t nslots = (int64_t)G_alloc * Lq;
   size_t o = 0;
   auto carve = [&](size_t bytes) {
     const size_t at = o;
     o += (size_t)round_up((int64_t)std::max<size_t>(bytes, 1), 256);
     return at;
   };
-  const size_t o_sl = carve((size_t)nslots * sizeof(LexTerm)), o_so = carve((size_t)(G + 1) * 4),
-               o_ko = carve((size_t)(G + 1) * 8), o_cnt = carve((size_t)G * 4),
-               o_bnd = carve((size_t)nslots * (NB + 1) * 4), o_keys = carve((size_t)G * per_q * 8),
+  const size_t o_sl = carve((size_t)nslots * sizeof(LexTerm)), o_so = carve((size_t)(G_alloc + 1) * 4),
+               o_ko = carve((size_t)(G_alloc + 1) * 8), o_cnt = carve((size_t)G_alloc * 4),
+               o_bnd = carve((size_t)nslots * (NB + 1) * 4), o_keys = carve((size_t)keys_alloc * 8),
                o_avg = carve(4);
   ws_.reserve(o);
   char* w = ws_.as<char>();
@@ -883,8 +934,7 @@ void LexIndex::search_tok_dev(const int32_t* tok, const int32_t* qlen, int B, in
   int32_t* d_bnd = reinterpret_cast<int32_t*>(w + o_bnd);
   uint64_t* d_keys = reinterpret_cast<uint64_t*>(w + o_keys);
   float* d_avg = reinterpret_cast<float*>(w + o_avg);
-  for (int b0 = 0; b0 < B; b0 += G) {
-    const int qb = std::min(G, B - b0);
+  for (const auto& [b0, qb] : groups) {
     hipLaunchKernelGGL(lex_qprep_kernel, dim3(1), dim3(1024), 0, s, tok + (int64_t)b0 * Lq, qlen + b0,
                        qb, Lq, off_.as<int64_t>(), vocab_, rows_, live_n_, sum_dl_, gstats,
                        (int64_t)b0 * Lq, d_sl, d_so, d_ko, d_cnt, d_avg);

@@ -291,7 +291,7 @@ class LexIndex {
   int64_t rows_ = 0, live_n_ = 0, P_ = 0, vocab_ = 0, nnz_ = 0, sum_dl_ = 0, max_df_ = 0;
   bool dirty_ = true;
   // device: forward index, per-row data, inverted index, workspaces
-  DevBuf fterm_, fval_, dlen_, live_, off_, post_, ws_, out_, mask_;
+  DevBuf fterm_, fval_, dlen_, live_, off_, post_, ws_, out_, mask_, caps_;
   // host mirrors
   std::vector<int32_t> dl_host_, df_host_;
   std::vector<uint8_t> live_host_;

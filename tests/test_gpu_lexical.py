@@ -301,3 +301,28 @@ def test_fixed_point_scores_exact_above_256():
         np.testing.assert_array_equal(fx[b][ok], acc[r[b][ok]].astype(np.uint32))
         np.testing.assert_array_equal(s[b][ok], fx[b][ok].astype(np.float32) / np.float32(65536))
     assert s[1].max() > 256.0                       # the test reaches the rounding range
+
+
+def test_device_queries_with_a_stopword_group_by_actual_caps():
+    """A term in every row makes the worst-case candidate count per query the whole index
+    (Lq x max df >= rows); a batch that does not fit one worst-case query group (here 1,100 queries
+    > the 1,024-query group limit) is grouped by the queries' actual caps, computed on the device
+    (lex_qcap_kernel) and read back once: 1,024 + 76 queries.  Results equal the
+    oracle bit for bit."""
+    from oracle.bm25 import bm25_topk
+    from super_rag_amd.lexical import NativeLexIndex
+    rng = np.random.default_rng(77)
+    n, vocab, k = 20_000, 3000, 20
+    docs = _docs(rng, n, vocab, max_len=12)
+    stop = vocab                                  # in every row: df = n
+    docs = [d + [stop] for d in docs]
+    lex = NativeLexIndex()
+    lex.add(docs)
+    qs = _queries(rng, 1100, vocab)
+    for i in range(4, 1100, 3):                   # a third of the queries carry the stopword
+        qs[i] = qs[i] + [stop]
+    tok, qlen = _pad(qs, 10)
+    s, r = lex.search_tok_dev(tok, qlen, k)
+    so, ro = bm25_topk(_oracle(docs, np.ones(n, bool)), qs, k)
+    np.testing.assert_array_equal(r.cpu().numpy(), ro)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
