@@ -2146,7 +2146,14 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
   }
   SR_CHECK(!f8 || (wexp && K % 128 == 0), "ffn1_diag: fp8 needs wexp, K % 128 == 0");
   const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
-  const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+  // SR_FFN1_DIAG_WALKERS = walkers per XCD (1..32; default 32 = every CU): with fewer CUs storing
+  // at once, a store cost that is the chip's write bandwidth shrinks, a per-CU one does not
+  static const int walkers = [] {
+    const char* e = std::getenv("SR_FFN1_DIAG_WALKERS");
+    const int w = e ? std::atoi(e) : 32;
+    return w < 1 ? 1 : (w > 32 ? 32 : w);
+  }();
+  const dim3 grid((unsigned)(8 * std::min<int64_t>(walkers, ceil_div(tiles, 8)))), block(512);
   lf.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;  // the product walk
   {  // the product's walker de-phasing (SR_GEMM_STAGGER, launch_gemm)
     const char* e = std::getenv("SR_GEMM_STAGGER");
