@@ -12,6 +12,7 @@ from __future__ import annotations
 import logging
 import os
 import re
+import threading
 from collections import OrderedDict
 from typing import List, Sequence, Tuple
 
@@ -99,16 +100,25 @@ class Tokenizer:
         # tokenizer memoises its word ids
         self._cache: "OrderedDict[str, np.ndarray]" = OrderedDict()
         self._cache_bytes = 0
+        # one lock around every read-modify of the LRU: the tokenizer is shared between the
+        # worker threads of aembed_documents, the coalescer leaders and uncoalesced rerank calls
+        # (get + move_to_end / pop + popitem are separate steps; another thread's eviction in
+        # between raised KeyError and drifted the byte count).  The HF encode stays outside it.
+        self._cache_lock = threading.Lock()
         self._cache_cap_bytes = int(float(os.environ.get("SUPER_RAG_AMD_TOKEN_CACHE_MB", "64")) * (1 << 20)) \
             if cache_mb is None else int(cache_mb * (1 << 20))
         self._words: dict = {}
 
     # -- content tokens (no specials) -------------------------------------------------------------
-    def _lookup(self, text: str):
-        a = self._cache.get(text)
-        if a is not None:
-            self._cache.move_to_end(text)
-        return a
+    def _lookup_many(self, texts: Sequence[str]) -> List:
+        with self._cache_lock:
+            out = []
+            for t in texts:
+                a = self._cache.get(t)
+                if a is not None:
+                    self._cache.move_to_end(t)
+                out.append(a)
+            return out
 
     def content_ids(self, text: str) -> List[int]:
         return self._content_arrays_many([text])[0].tolist()
@@ -120,7 +130,7 @@ class Tokenizer:
 
     def _content_arrays_many(self, texts: Sequence[str]) -> List[np.ndarray]:
         """Content ids of many texts as int32 arrays (the cached form; do not modify them)."""
-        out: List = [self._lookup(t) for t in texts]
+        out: List = self._lookup_many(texts)
         miss = [i for i, o in enumerate(out) if o is None]
         if not miss:
             return out
@@ -131,10 +141,11 @@ class Tokenizer:
             ids = [self._hf.encode(texts[miss[0]], add_special_tokens=False).ids]
         else:
             ids = [[self._word_id(w) for w in _WORD.findall(texts[i])] for i in miss]
-        for i, c in zip(miss, ids):
-            a = np.asarray(c, dtype=np.int32)
-            out[i] = a
-            self._remember(texts[i], a)
+        with self._cache_lock:
+            for i, c in zip(miss, ids):
+                a = np.asarray(c, dtype=np.int32)
+                out[i] = a
+                self._remember(texts[i], a)
         return out
 
     def _word_id(self, w: str) -> int:
@@ -146,6 +157,7 @@ class Tokenizer:
         return i
 
     def _remember(self, text: str, ids: np.ndarray) -> None:
+        # (caller holds _cache_lock)
         cost = 4 * int(ids.size) + len(text) + 64
         if cost > self._cache_cap_bytes:
             return

@@ -56,3 +56,35 @@ def test_content_cache_is_a_byte_bounded_lru():
     assert hot in tok._cache
     many = tok.content_ids_many(texts[5:9] + texts[5:6])
     assert many == [fresh.content_ids(t) for t in texts[5:9] + texts[5:6]]
+
+
+def test_content_cache_is_thread_safe_under_constant_eviction():
+    # the LRU is shared by the embed worker threads, the coalescer leaders and
+    # uncoalesced rerank calls; with a ~4 KiB cache every insert evicts, so an unlocked
+    # get / move_to_end or pop / popitem sequence raced into KeyError and a drifting byte count
+    import threading
+    tok = Tokenizer(MODELS["bge-reranker-base"], synthetic=True, cache_mb=0.004)
+    ref = Tokenizer(MODELS["bge-reranker-base"], synthetic=True, cache_mb=0)
+    texts = [" ".join(f"t{(i * 7 + j) % 97}" for j in range(1 + i % 40)) for i in range(300)]
+    want = {t: ref.content_ids(t) for t in texts}
+    errors = []
+
+    def worker(seed):
+        rng = random.Random(seed)
+        try:
+            for _ in range(400):
+                batch = [rng.choice(texts) for _ in range(rng.randint(1, 6))]
+                for t, got in zip(batch, tok.content_ids_many(batch)):
+                    if got != want[t]:
+                        errors.append(("ids", t))
+        except Exception as e:  # noqa: BLE001 - collected and asserted below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(s,)) for s in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors[:3]
+    held = sum(4 * int(v.size) + len(k) + 64 for k, v in tok._cache.items())
+    assert tok._cache_bytes == held <= tok._cache_cap_bytes
