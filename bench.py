@@ -33,6 +33,8 @@ import torch  # noqa: E402
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_F16_TFLOPS = 2500.0    # dense fp16/bf16 MFMA spec (no sparsity)
 PEAK_F8_TFLOPS = 5000.0     # dense fp8 MFMA spec (no sparsity)
+# compute dtype of the line per reranker precision mode (bench --fp8)
+FP8_DTYPES = {0: "f16", 1: "f16+fp8ffn", 2: "f16+fp8gemm", 3: "f16+fp8mlp"}
 
 
 def parse():
@@ -82,11 +84,10 @@ def parse():
     ap.add_argument("--fp8-ffn", action="store_true",
                     help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
                          "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
-    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3, 4),
+    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3),
                     help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
                          "e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16 "
-                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp); 4 = 3 + QKV fp8 on normalised "
-                         "e4m3 rows (f16+fp8mlp+qkvn, experimental)")
+                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp)")
     ap.add_argument("--replicate-passages", action="store_true",
                     help="N > 1: keep the whole passage token table on every rank (default: each "
                          "rank holds its shard's rows, the candidates' rows are fetched per batch, "
@@ -368,7 +369,7 @@ def run_bench(a, mp=None):
         "metric": metric,
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": ("f16", "f16+fp8ffn", "f16+fp8gemm", "f16+fp8mlp", "f16+fp8mlp+qkvn")[a.fp8],
+        "scaling": "weak", "vs_baseline": None, "dtype": FP8_DTYPES[a.fp8],
         "data": "synthetic",
         "config": {"workload": workload,
                    "queries_per_rank": a.batch, "global_batch": world * a.batch,
@@ -737,8 +738,7 @@ def rerank_fidelity(rs, device):
                    f"fp32 oracle (tests/golden/{fixture})"),
            "logit_std_mean": round(float(std.mean()), 4)}
     try:
-        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3"),
-                           (4, "fp8_mode4")):
+        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3")):
             enc.set_fp8(mode)
             lg = enc.cross_score_dev(dids, dmask)[:, 0].float().cpu().numpy().reshape(ref.shape)
             err = np.abs(lg - ref).max(1)
@@ -773,7 +773,7 @@ def measured_peaks(dev):
     y = torch.empty_like(x)
     st = torch.cuda.current_stream().cuda_stream
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for name, fn in (("hbm_copy_GBs", lambda: N.call("sr_diag_copy", x.data_ptr(), y.data_ptr(),
+    for name, fn in (("hbm_copy_GBs", lambda: N.call_diag("sr_diag_copy", x.data_ptr(), y.data_ptr(),
                                                      x.numel() * 2, 0, st)),
                      ("hbm_torch_copy_GBs", lambda: y.copy_(x))):
         fn()
@@ -791,7 +791,7 @@ def measured_peaks(dev):
     Y = torch.empty(M, Nn, device=dev, dtype=torch.float16)
 
     def g():
-        N.call("sr_diag_gemm", 9, 0, X.data_ptr(), X.stride(0), W.data_ptr(), bias.data_ptr(), None, 0,
+        N.call_diag("sr_diag_gemm", 9, 0, X.data_ptr(), X.stride(0), W.data_ptr(), bias.data_ptr(), None, 0,
                Y.data_ptr(), Y.stride(0), M, Nn, K, 0, st)
     g()
     e0.record()

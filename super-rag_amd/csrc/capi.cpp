@@ -793,7 +793,8 @@ int sr_rerank_select_dev(const float* logits, int B, int K, int k_out, int32_t* 
   SR_API_END
 }
 
-// ---- diagnostics -----------------------------------------------------------------------------
+// ---- diagnostics (libsrmi_diag.so only: include/super_rag_mi355x_diag.h) --------------------
+#if SR_WITH_DIAG
 int sr_diag_gemm(int variant, int epi, const void* X, int64_t lda, const void* W, const float* bias,
                  const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, int device,
                  void* stream) {
@@ -866,6 +867,7 @@ int sr_diag_attention(int variant, const void* qkv, const int32_t* mask, void* c
   sr::attention_force_variant(-1);
   SR_API_END
 }
+#endif  // SR_WITH_DIAG
 
 // ---- profiling -------------------------------------------------------------------------------
 int sr_profile_enable(int on) {

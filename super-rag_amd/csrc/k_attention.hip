@@ -1209,8 +1209,9 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   SR_CHECK(tiles < (1ll << 31), "qkv_attention: too many tiles");
   // persistent: 8 XCD groups x G walkers, one 8-wave workgroup per CU (153 KiB of LDS)
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+#if SR_WITH_DIAG
   static const int diag = [] {
-    const char* e = std::getenv("SR_QA_DIAG");
+    const char* e = diag_getenv("SR_QA_DIAG");
     return e ? std::atoi(e) : 0;
   }();
   if (epi == EPI_LNF_F16 && diag == 1)
@@ -1219,7 +1220,9 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   else if (epi == EPI_LNF_F16 && diag == 2)
     hipLaunchKernelGGL((qkv_attn_kernel<true, 2>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
                        lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
-  else if (epi == EPI_LNF_F16)
+  else
+#endif
+  if (epi == EPI_LNF_F16)
     hipLaunchKernelGGL(qkv_attn_kernel<true>, grid, block, 0, stream, X, lda, W, bias, lf->colsum,
                        lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
   else

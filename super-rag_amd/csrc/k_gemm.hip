@@ -1348,9 +1348,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   half_t* const escr = lds + 2 * STAGE + wave * (GLINE ? 1024 : 2048);
   half_t* const gscr = GLINE ? escr : nullptr;
   (void)gscr;
-#ifdef SR_GEMM_PRIO_HALF  // experiment: static priority for the second-dispatched half
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
   const int nk = K / GBK;
   const int kxs = lf.x_k > 0 ? lf.x_k / GBK : nk;  // K-steps of the X operand (split weights)
   (void)kxs;
@@ -1381,9 +1378,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // buffer-resource type through its signature: hipcc then drops the host stubs of this template)
   auto stage = [&](int kt, half_t* s, int mm, int nn) {
 #if defined(__HIP_DEVICE_COMPILE__)
-#ifdef SR_GEMM_DIAG_L2ONLY  // experiment: the no-epilogue diagnostic stages tile (0, 0) only
-    if (DIAG == 2) mm = nn = 0;
-#endif
     const auto rw = panel_rsrc(W + (int64_t)nn * K, (int64_t)(N - nn < BN ? N - nn : BN) * K * 2);
     const auto rx = panel_rsrc(X + (int64_t)mm * lda, (int64_t)(M - mm < BM ? M - mm : BM) * lda * 2);
     // row-group offsets advanced in place (an opaque running value: precomputed per piece and
@@ -2038,8 +2032,11 @@ void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* l
   lf.stat_ld = r0;
   const int64_t tiles = ceil_div(n, 256);
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
-  static const bool diag_noepi = std::getenv("SR_SCAN_DIAG_NOEPI") != nullptr;  // timing only
-  auto kern = diag_noepi ? gemm_pipe_kernel<EPI_SCAN, true, 2> : gemm_pipe_kernel<EPI_SCAN, true>;
+  auto kern = gemm_pipe_kernel<EPI_SCAN, true>;
+#if SR_WITH_DIAG
+  static const bool diag_noepi = diag_getenv("SR_SCAN_DIAG_NOEPI") != nullptr;  // timing only
+  if (diag_noepi) kern = gemm_pipe_kernel<EPI_SCAN, true, 2>;
+#endif
   hipLaunchKernelGGL(kern, grid, block, 0, s, Q, ldc,
                      corpus + r0 * ldc, tau, (const void*)(live ? live + r0 : nullptr), (int64_t)0,
                      (void*)cand, (int64_t)cap, B, (int)n, (int)ldc, lf);
@@ -2062,8 +2059,11 @@ void launch_cosine_scan_gemm8(const uint8_t* corpus8, int64_t ld8, const uint8_t
   const int64_t tiles = ceil_div(n, 256);
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
   // operands as 2-byte units: K = ld8 / 2 (the staging moves bytes)
-  static const bool diag_noepi = std::getenv("SR_SCAN_DIAG_NOEPI") != nullptr;  // timing only
-  auto kern = diag_noepi ? gemm_pipe_kernel<EPI_SCAN8, true, 2> : gemm_pipe_kernel<EPI_SCAN8, true>;
+  auto kern = gemm_pipe_kernel<EPI_SCAN8, true>;
+#if SR_WITH_DIAG
+  static const bool diag_noepi = diag_getenv("SR_SCAN_DIAG_NOEPI") != nullptr;  // timing only
+  if (diag_noepi) kern = gemm_pipe_kernel<EPI_SCAN8, true, 2>;
+#endif
   hipLaunchKernelGGL(kern, grid, block, 0, s,
                      reinterpret_cast<const half_t*>(Q8), ld8 / 2,
                      reinterpret_cast<const half_t*>(corpus8 + r0 * ld8), tau,
@@ -2126,11 +2126,14 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
   SR_LAUNCH_CHECK();
 }
 
+#if SR_WITH_DIAG
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
                       int M, int N, int K, hipStream_t stream) {
   SR_CHECK(diag == 0 || diag == 2 || (diag >= 5 && diag <= 7), "ffn1_diag: diag must be 0, 2, 5, 6 or 7");
   SR_CHECK(N % 256 == 0 && M > 0, "ffn1_diag: N % 256 == 0, M > 0");
+  // diag 7 stores every tile unchecked onto rows 0..255 of Y
+  SR_CHECK(diag != 7 || (M >= 256 && ldy >= N), "ffn1_diag: diag 7 needs M >= 256, ldy >= N");
   LnFold lf;
   lf.mr = mr;
   lf.colsum = colsum;
@@ -2149,14 +2152,14 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
   // SR_FFN1_DIAG_WALKERS = walkers per XCD (1..32; default 32 = every CU): with fewer CUs storing
   // at once, a store cost that is the chip's write bandwidth shrinks, a per-CU one does not
   static const int walkers = [] {
-    const char* e = std::getenv("SR_FFN1_DIAG_WALKERS");
+    const char* e = diag_getenv("SR_FFN1_DIAG_WALKERS");
     const int w = e ? std::atoi(e) : 32;
     return w < 1 ? 1 : (w > 32 ? 32 : w);
   }();
   const dim3 grid((unsigned)(8 * std::min<int64_t>(walkers, ceil_div(tiles, 8)))), block(512);
   lf.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;  // the product walk
   {  // the product's walker de-phasing (SR_GEMM_STAGGER, launch_gemm)
-    const char* e = std::getenv("SR_GEMM_STAGGER");
+    const char* e = diag_getenv("SR_GEMM_STAGGER");
     const int st = e ? std::atoi(e) : 0;
     lf.stagger = st > 0 ? std::max(1, st * K / 768) : 0;
   }
@@ -2190,6 +2193,7 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
 #undef SR_FD
   SR_LAUNCH_CHECK();
 }
+#endif  // SR_WITH_DIAG
 
 __device__ __forceinline__ float e4m3_decode(uint32_t b) {
   const uint32_t e = (b >> 3) & 15u, m = b & 7u;
@@ -2305,6 +2309,9 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   if (v != GEMM_SMALL && N % 256 != 0) v = GEMM_SMALL;
   if (v == GEMM_PP && (K % 32 != 0 || epi >= EPI_LNF_GELU_F8 || x_k != K)) v = GEMM_PIPE;
   if (x_k != K && v >= GEMM_DIAG_NOLOAD && v != GEMM_PP) v = GEMM_PIPE;  // diagnostics: plain K
+  SR_CHECK(SR_WITH_DIAG || !(v == GEMM_DIAG_NOLOAD || v == GEMM_DIAG_NOEPI ||
+                             (v >= GEMM_DIAG_P_NOEPI && v <= GEMM_DIAG_P_STOREONLY)),
+           "gemm: timing-only variants are in the diagnostic library (libsrmi_diag.so)");
   if (fold && (v == GEMM_SMALL || v == GEMM_BIG)) v = big_tiles >= 512 ? GEMM_PIPE_PERSIST : GEMM_PIPE;
   const bool wide = (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST || v == GEMM_PP) && !out32;
   SR_CHECK(!wide || (ldy % 8 == 0 && ldr % 8 == 0), "gemm: fp16 outputs need ldy, ldr % 8 == 0");
@@ -2317,7 +2324,7 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   // (diagnostic) SR_GEMM_GROUP_M = "G" for every shape, or "N:G,N:G,..." per output width N
   static const std::vector<std::pair<int, int>> group_m_env = [] {
     std::vector<std::pair<int, int>> v;
-    const char* e = std::getenv("SR_GEMM_GROUP_M");
+    const char* e = diag_getenv("SR_GEMM_GROUP_M");
     if (!e) return v;
     std::string str(e);
     if (str.find(':') == std::string::npos) {
@@ -2341,13 +2348,14 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   // de-phasing of the persistent walkers: phase step ~1/16 of a tile (K / 96 x 512 cycles);
   // SR_GEMM_STAGGER = units of 512 cycles per phase (0 = off)
   static const int stagger_env = [] {
-    const char* e = std::getenv("SR_GEMM_STAGGER");
+    const char* e = diag_getenv("SR_GEMM_STAGGER");
     return e ? std::atoi(e) : -1;
   }();
   lfv.stagger = stagger_env >= 0 ? (stagger_env > 0 ? std::max(1, stagger_env * K / 768) : 0) : 0;
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
                                        ldr, Y, ldy, M, N, K, x_k / GBK);
+#if SR_WITH_DIAG
   } else if (v >= GEMM_DIAG_P_NOEPI && v <= GEMM_DIAG_P_STOREONLY) {
     const int64_t g = 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8));
     const dim3 grid((unsigned)g), block(512);
@@ -2368,6 +2376,7 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
     else
       hipLaunchKernelGGL((gemm_pipe_kernel<EPI_BIAS_F16, false, 2>), grid, block, 0, stream, X, lda,
                          W, bias, R, ldr, Y, ldy, M, N, K, lfv);
+#endif
   } else if (v == GEMM_PP) {
     const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 128);
     const dim3 grid((unsigned)tiles), block(256);

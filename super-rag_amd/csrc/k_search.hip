@@ -540,7 +540,7 @@ int scan_query_tiles(int B) {
   return 16;
 }
 
-static bool g_scan_legacy = std::getenv("SR_SCAN_LEGACY") != nullptr;
+static bool g_scan_legacy = diag_getenv("SR_SCAN_LEGACY") != nullptr;  // (diagnostic build only)
 
 // SR_SCAN_STREAM (read per launch: parity tests switch it): 0 (default) = threshold chunks of 65..256
 // queries on the GEMM main loop (launch_cosine_scan_gemm), 1 = on cosine_stream, 2 = cosine_stream for

@@ -11,7 +11,29 @@
 
 #include "../../include/super_rag_mi355x.h"
 
+// SR_WITH_DIAG: 1 in the diagnostic library (libsrmi_diag.so: the product sources plus the
+// sr_diag_* entry points of include/super_rag_mi355x_diag.h, timing-only kernel variants and
+// the A/B environment knobs); 0 in the product library (libsrmi.so), which exports none of them.
+#ifndef SR_WITH_DIAG
+#define SR_WITH_DIAG 0
+#endif
+#if SR_WITH_DIAG
+#include <cstdlib>
+#include "../../include/super_rag_mi355x_diag.h"
+#endif
+
 namespace sr {
+
+// A/B and timing-diagnostic environment knobs: read in the diagnostic library only (the product
+// library's knobs are listed in INTEGRATION.md and read with std::getenv where they are used).
+inline const char* diag_getenv(const char* name) {
+#if SR_WITH_DIAG
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 typedef _Float16 half_t;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));

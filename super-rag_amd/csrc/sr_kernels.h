@@ -75,10 +75,12 @@ void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 // Y = epi(X8 . W8^T) on OCP e4m3 operands: X8 [M][K] bytes (lda bytes), W8 [N][K] bytes with
 // per-row E8M0 exponents lf->wexp[N] (W = W8 * 2^(wexp - 127)); K % 128 == 0, K >= 256;
 // epi in {EPI_LNF_F16, EPI_LNF_GELU_F8, EPI_RES16_STATS(_Y8), EPI_LNR16_STATS(_Y8)}.
+#if SR_WITH_DIAG
 // Diagnostic FFN1 launches (sr_diag_ffn1): diag 0 product, 2 no epilogue, 5 math only, 6 stores only.
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
                       int M, int N, int K, hipStream_t stream);
+#endif
 void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8, const float* bias,
                      const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,
                      hipStream_t stream, const LnFold* lf);

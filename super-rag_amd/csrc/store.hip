@@ -22,7 +22,7 @@ namespace sr {
 // (schedule experiments).
 static int64_t scan_fixed_chunk() {  // SR_SCAN_CHUNK: fixed threshold-chunk rows (experiments)
   static const int64_t c = [] {
-    const char* e = std::getenv("SR_SCAN_CHUNK");
+    const char* e = diag_getenv("SR_SCAN_CHUNK");
     const long v = e ? std::strtol(e, nullptr, 10) : 0;
     return (int64_t)(v > 0 ? v : 0);
   }();
@@ -30,7 +30,7 @@ static int64_t scan_fixed_chunk() {  // SR_SCAN_CHUNK: fixed threshold-chunk row
 }
 static int64_t scan_growth_max() {
   static const int64_t g = [] {
-    const char* e = std::getenv("SR_SCAN_GROWTH");
+    const char* e = diag_getenv("SR_SCAN_GROWTH");
     const long v = e ? std::strtol(e, nullptr, 10) : 0;
     return (int64_t)(v > 0 ? v : 8);
   }();

@@ -139,18 +139,24 @@ SIGNATURES = {
     "sr_rerank_select_dev": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "sr_profile_enable": (c_int, [c_int]),
     "sr_profile_read": (c_int, [POINTER(KernelStatC), c_int, P_I32]),
+    "sr_lex_search_global_fixed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                           c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+}
+
+# The diagnostic surface (include/super_rag_mi355x_diag.h), exported by libsrmi_diag.so only:
+# single-kernel parity entry points, timing-only variants and the HBM copy yardstick.
+DIAG_SIGNATURES = {
     "sr_diag_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                              c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
+    "sr_diag_ffn1": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
     "sr_diag_attention": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_void_p]),
     "sr_diag_copy": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
-    "sr_lex_search_global_fixed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
-                                           c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "sr_diag_ffn1": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p]),
 }
 
 _lib = None
+_diag = None
 
 _gates: dict = {}
 _gates_lock = threading.Lock()
@@ -244,6 +250,48 @@ def load() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+def diag_library_path() -> str:
+    return os.environ.get("SUPER_RAG_AMD_DIAG_LIB",
+                          os.path.join(os.path.dirname(library_path()), "libsrmi_diag.so"))
+
+
+def load_diag() -> ctypes.CDLL:
+    """The diagnostic library libsrmi_diag.so (the product sources + sr_diag_*; tests of single
+    kernels, tools/, bench.py's measured peaks).  Never needed by the product path."""
+    global _diag
+    if _diag is not None:
+        return _diag
+    with _lock:
+        if _diag is not None:
+            return _diag
+        try:
+            import torch  # noqa: F401  (one HIP runtime per process, as in load())
+        except Exception:  # noqa: BLE001
+            pass
+        path = diag_library_path()
+        if not os.path.exists(path):
+            raise NativeUnavailableError(f"diagnostic library not built: {path} (`make -C super-rag_amd`)")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:
+            raise NativeUnavailableError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in {**SIGNATURES, **DIAG_SIGNATURES}.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _diag = lib
+        return lib
+
+
+def call_diag(name: str, *args) -> None:
+    """Call an sr_diag_* entry point of libsrmi_diag.so (errors from its own sr_last_error)."""
+    lib = load_diag()
+    code = getattr(lib, name)(*args)
+    if code != SR_OK:
+        msg = lib.sr_last_error()
+        raise NativeError(code, msg.decode("utf-8", "replace") if msg else "unknown error")
 
 
 def check(code: int) -> None:

@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "super_rag_mi355x.h"
+#include "super_rag_mi355x_diag.h"  // (the ASan build is the diagnostic superset)
 
 static int g_cases = 0, g_fail = 0;
 

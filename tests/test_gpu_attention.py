@@ -1,4 +1,4 @@
-"""GPU parity of the K5 attention kernels (through the C-ABI diagnostic sr_diag_attention) against
+"""GPU parity of the K5 attention kernels (through the diagnostic library's sr_diag_attention, libsrmi_diag.so) against
 a torch fp32 reference: ctx = softmax(Q K^T / sqrt(d_h) + key-padding mask) V per head, for the
 first Sq query rows of each sequence.
 
@@ -25,7 +25,7 @@ def _run(variant, B, S, Sq, heads, dh=64, seed=0, lens=None):
         lens = torch.randint(1, S + 1, (B,), device=dev, generator=g)
     mask = (torch.arange(S, device=dev)[None] < lens[:, None]).int().contiguous()
     ctx = torch.full((B * Sq, d), float("nan"), device=dev, dtype=torch.float16)
-    NT.call("sr_diag_attention", variant, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), B, S, Sq,
+    NT.call_diag("sr_diag_attention", variant, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), B, S, Sq,
             d, heads, 0, torch.cuda.current_stream().cuda_stream)
     x = qkv.float().view(B, S, 3, heads, dh)
     q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
@@ -77,7 +77,7 @@ def test_attention_k5d_persistent_walkers(S, Sq):
     outs = {}
     for variant in (3, -1):
         ctx = torch.full((B * Sq, d), float("nan"), device=dev, dtype=torch.float16)
-        NT.call("sr_diag_attention", variant, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), B, S,
+        NT.call_diag("sr_diag_attention", variant, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), B, S,
                 Sq, d, heads, 0, torch.cuda.current_stream().cuda_stream)
         outs[variant] = ctx
     torch.cuda.synchronize()

@@ -50,7 +50,7 @@ def test_ffn1_ragged_rows_and_guard_band(f8, M, N):
         wexp_p = None
     colsum = Wd.sum(1).contiguous()
     stream = torch.cuda.current_stream().cuda_stream
-    NT.call("sr_diag_ffn1", 0, 1 if f8 else 0, X.data_ptr(), K, Wop.data_ptr(), wexp_p,
+    NT.call_diag("sr_diag_ffn1", 0, 1 if f8 else 0, X.data_ptr(), K, Wop.data_ptr(), wexp_p,
             bias.data_ptr(), colsum.data_ptr(), mr.data_ptr(), Yall.data_ptr(), N, M, N, K, 0, stream)
     torch.cuda.synchronize()
     pre = mr[:, 1:2] * (Xd @ Wd.T - mr[:, 0:1] * colsum[None]) + bias[None]

@@ -1,4 +1,4 @@
-"""GPU parity of the K4 MFMA GEMM variants (through the C-ABI diagnostic entry sr_diag_gemm)
+"""GPU parity of the K4 MFMA GEMM variants (through sr_diag_gemm of the diagnostic library libsrmi_diag.so)
 against a torch fp32 reference of the same op: Y = epi(X . W^T + b (+ R)).
 
 Covers every epilogue (bias, bias+GELU(erf), +fp32 residual, tanh, +fp16 residual) on every
@@ -33,7 +33,7 @@ def _run(variant, epi, M, N, K, seed=0):
     Yall = torch.full((M + 32, N), float("nan"), device=dev,
                       dtype=torch.float32 if epi in (2, 3) else torch.float16)
     Y = Yall[:M]
-    NT.call("sr_diag_gemm", variant, epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
+    NT.call_diag("sr_diag_gemm", variant, epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
             R.data_ptr() if R is not None else None, R.stride(0) if R is not None else 0,
             Y.data_ptr(), Y.stride(0), M, N, K, 0, torch.cuda.current_stream().cuda_stream)
     ref = X.float() @ W.float().T + b
@@ -94,7 +94,7 @@ def test_gemm_split_weights_match_fp32_weights(variant, epi):
     b = torch.randn(N, device=dev, generator=g) * 0.1
     R = torch.randn(M, N, device=dev, generator=g) if epi == 2 else None
     Y = torch.full((M, N), float("nan"), device=dev, dtype=torch.float32 if epi == 2 else torch.float16)
-    NT.call("sr_diag_gemm", VARIANTS[variant] | 0x100, epi, X.data_ptr(), X.stride(0), W2.data_ptr(),
+    NT.call_diag("sr_diag_gemm", VARIANTS[variant] | 0x100, epi, X.data_ptr(), X.stride(0), W2.data_ptr(),
             b.data_ptr(), R.data_ptr() if R is not None else None, R.stride(0) if R is not None else 0,
             Y.data_ptr(), Y.stride(0), M, N, 2 * K, 0, torch.cuda.current_stream().cuda_stream)
     ref = X.double() @ W.double().T + b.double()

@@ -1,5 +1,6 @@
-"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and fails loudly (no
-silent CPU fallback) when no GPU is visible."""
+"""CPU: the C-ABI library loads, exports every symbol include/super_rag_mi355x.h declares and no
+diagnostic symbol (those are libsrmi_diag.so's, include/super_rag_mi355x_diag.h), and fails loudly
+(no silent CPU fallback) when no GPU is visible."""
 import glob
 import os
 import re
@@ -9,12 +10,18 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _declared():
-    names = set()
-    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
-        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        names |= set(re.findall(r"\b(sr_[a-z0-9_]+)\s*\(", src))
-    return names
+def _declared(header="super_rag_mi355x.h"):
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", header)).read(), flags=re.S)
+    return set(re.findall(r"\b(sr_[a-z0-9_]+)\s*\(", src))
+
+
+def _exports(path):
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if l.split()[-1].startswith("sr_")}
 
 
 def test_library_exports_every_declared_symbol():
@@ -26,6 +33,21 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     assert declared == set(_native.SIGNATURES), declared ^ set(_native.SIGNATURES)
     assert lib.sr_version() >= 100
+
+
+def test_product_library_exports_no_diagnostic_symbol():
+    # the sr_diag_* entry points (single-kernel drivers, timing-only variants,
+    # the copy yardstick) are built into libsrmi_diag.so only; the product library exports exactly
+    # the product header's functions
+    from super_rag_amd import _native
+    prod = _exports(_native.library_path())
+    assert not [n for n in prod if n.startswith("sr_diag")], prod
+    assert prod == _declared(), prod ^ _declared()
+    diag = _declared("super_rag_mi355x_diag.h")
+    assert diag == set(_native.DIAG_SIGNATURES) and all(n.startswith("sr_diag_") for n in diag)
+    assert _exports(_native.diag_library_path()) == prod | diag
+    lib = _native.load_diag()
+    assert all(hasattr(lib, n) for n in diag)
 
 
 def test_no_gpu_fails_loudly():

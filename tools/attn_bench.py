@@ -34,14 +34,14 @@ def main():
     for _ in range(3):
         for v in (0, 1, 2, 3, -1):
             try:
-                N.call("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B,
+                N.call_diag("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B,
                        a.S, a.Sq, d, a.heads, 0, st)
             except N.NativeError:  # an older library without this variant
                 continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
-                N.call("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B,
+                N.call_diag("sr_diag_attention", v, qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), a.B,
                        a.S, a.Sq, d, a.heads, 0, st)
             e1.record()
             torch.cuda.synchronize()

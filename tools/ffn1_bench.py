@@ -61,7 +61,7 @@ def main():
     colsum = Wd.sum(1).contiguous()
 
     def run(diag):
-        N.call("sr_diag_ffn1", diag, 1 if a.f8 else 0, X.data_ptr(), lda, Wop.data_ptr(), wexp_p,
+        N.call_diag("sr_diag_ffn1", diag, 1 if a.f8 else 0, X.data_ptr(), lda, Wop.data_ptr(), wexp_p,
                bias.data_ptr(), colsum.data_ptr(), mr.data_ptr(), Y.data_ptr(), ldy, M, Nn, K, 0, stream)
 
     run(0)

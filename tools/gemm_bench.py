@@ -27,7 +27,7 @@ def gemm(variant, epi, X, W, b, R, Y):
         return
     M, K = X.shape
     Nn = W.shape[0]
-    N.call("sr_diag_gemm", variant, epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
+    N.call_diag("sr_diag_gemm", variant, epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
            R.data_ptr() if R is not None else None, 0 if R is None or RES_LD0 else R.stride(0),
            Y.data_ptr(), Y.stride(0), M, Nn, K, 0, torch.cuda.current_stream().cuda_stream)
 

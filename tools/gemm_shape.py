@@ -39,7 +39,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
 
     def run():
-        N.call("sr_diag_gemm", a.variant, a.epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
+        N.call_diag("sr_diag_gemm", a.variant, a.epi, X.data_ptr(), X.stride(0), W.data_ptr(), b.data_ptr(),
                R.data_ptr() if R is not None else None, R.stride(0) if R is not None else 0,
                Y.data_ptr(), Y.stride(0), a.M, a.N, a.K, 0, st)
     run()

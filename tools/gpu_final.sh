@@ -20,7 +20,6 @@ else
   find gpurun_out/prof_$TAG -name "*.csv" -size +1M -delete
   timeout -k 10 400 python -u bench.py --workload config5 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/$TAG/bench_config5.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --fp8 3 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/$TAG/bench_fp8m3.log 2>&1 || exit 1
-  timeout -k 10 300 python -u bench.py --fp8 4 --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/$TAG/bench_fp8m4.log 2>&1 || exit 1
   timeout -k 10 400 python -u bench.py --rerank-model bge-reranker-v2-m3 --steps 5 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/$TAG/bench_v2m3.log 2>&1 || exit 1
 fi
 exit 0
