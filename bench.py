@@ -100,6 +100,10 @@ def parse():
                          "scanned in fp8, BM25 + rrf on the device, reranker in fp8 mode 3), run "
                          "after the headline with the config-4 objects freed (0 = skip)")
     ap.add_argument("--config5-warmup", type=int, default=2)
+    ap.add_argument("--v2m3-steps", type=int, default=3,
+                    help="v2m3 field of the default line: timed steps of the rerank stage alone with "
+                         "bge-reranker-v2-m3 (the reranker the reference seeds; 24 layers, 1024-d) "
+                         "in fp16 and in fp8 mode 3, after the config5 field (0 = skip)")
     a = ap.parse_args()
     if a.workload == "config5":
         as_config5(a)
@@ -289,6 +293,10 @@ def run_bench(a, mp=None):
     dt, prof = timed_steps(W, a, world, dev, dist)
     queries = world * a.batch * a.steps
     value = queries / dt
+    stage_ms = dict(W.stage_ms, note=("HIP events on the launch stream at the stage boundaries "
+                                      "of every timed step, ms per step (max over ranks); exchange "
+                                      "= C1 query all_gather + C2 list all_to_all + C3 passage "
+                                      "fetch (+ the BM25 statistics all_reduce in hybrid mode)"))
 
     # ---- recall@10 of the search stage vs exact fp32 (outside the timed region) -----------------
     recall = search_recall(W, a, dev) if world == 1 and not a.no_extras else None
@@ -337,7 +345,7 @@ def run_bench(a, mp=None):
     # ---- roofline of the dominant kernel -------------------------------------------------------
     roof = dominant_roofline(prof)
     step_ms = dt / a.steps * 1e3
-    kern = kernel_table(prof, a.steps)
+    kern = kernel_table(prof, a.steps, top=12)
     search_roof = scan_roofline(prof)
 
     # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) ----------------------------
@@ -354,6 +362,11 @@ def run_bench(a, mp=None):
         free_workload(W)
         config5 = config5_field(a, world, rank, local, dev, dist,
                                 (fidelity or {}).get("fp8_mode3"))
+
+    # ---- the reference's seeded reranker (bge-reranker-v2-m3) on the rerank stage alone ---------
+    v2m3 = None
+    if a.workload == "config4" and not a.no_extras and a.v2m3_steps > 0 and rank == 0:
+        v2m3 = v2m3_field(a, local, dev)
 
     workload = ("config4: bge-base-en embed (S=32) + exact cosine top-100 over "
                 f"{N_total} x {a.dim} fp16 corpus (row-sharded) + bge-reranker-base "
@@ -387,13 +400,113 @@ def run_bench(a, mp=None):
         "measured_peaks": peaks,
         "cpu_baseline": cpu,
         "config5": config5,
+        "v2m3": v2m3,
         "kernels": kern,
         "setup_s": round(setup_s, 1),
+        "stage_ms": stage_ms,
     }
+    # LAST: a compact summary, so a reader of the line's tail (the driver keeps the end of
+    # stdout) sees the headline, recall, fidelity verdicts, drop-in latency and the extra fields
+    line["summary"] = summary(line)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def summary(line):
+    """The line's key results in a few hundred bytes (printed last in the JSON line)."""
+    def fid(f):
+        if not f:
+            return None
+        return {m: f"{v['top10_identical_mod_ties']} top-10 identical, std/err {v['min_std_over_err']}"
+                for m, v in f.items() if isinstance(v, dict) and "top10_identical_mod_ties" in v}
+
+    def drop(d):
+        if not d or "runs" not in d:
+            return None
+        r64 = next((r for r in d["runs"] if r.get("concurrency") == 64), d["runs"][0])
+        out = {"c64_qps": r64.get("qps"), "c64_p50_ms": r64.get("p50_ms"), "c64_p99_ms": r64.get("p99_ms")}
+        mp = d.get("multi_process")
+        if mp and "qps" in mp:
+            out["multi_process"] = {"procs": mp["procs"], "qps": mp["qps"], "p50_ms": mp["p50_ms"],
+                                    "p99_ms": mp["p99_ms"]}
+        return out
+
+    c5, v2 = line.get("config5"), line.get("v2m3")
+    roof = line.get("roofline") or {}
+    return {
+        "value": line["value"], "unit": line["unit"], "n_gpus": line["n_gpus"],
+        "ms_per_step": line["ms_per_step"], "recall_at_10": line.get("recall_at_10"),
+        "stage_ms": {k: v for k, v in (line.get("stage_ms") or {}).items() if k != "note"},
+        "dominant_kernel": roof.get("kernel"), "roofline_frac": roof.get("frac"),
+        "rerank_fidelity": fid(line.get("rerank_fidelity")),
+        "drop_in": drop(line.get("drop_in")),
+        "config5": {"value": c5["value"], "ms_per_step": c5["ms_per_step"],
+                    "recall_at_10": c5.get("recall_at_10")} if c5 else None,
+        "v2m3": {k: v2.get(k) for k in ("fp16_qps", "fp8_mode3_qps", "fidelity")} if v2 else None,
+    }
+
+
+def v2m3_field(a, local, dev):
+    """bge-reranker-v2-m3 -- the reranker the reference seeds (migration/sql/model_configs_init.sql:
+    4148; XLM-R large: 24 layers, 1024-d, 16 heads, FFN 4096) -- on the rerank stage alone at the
+    bench shape: a.batch queries x a.k_cand candidates (S_pair = a.pair_len) per step, the pairs
+    packed on the device from a 1M-row synthetic passage table (SearchPipeline.rerank: pair
+    packing, cross-encoder, top-k select), seeded random weights; timed in fp16 and in fp8 mode 3
+    (a.v2m3_steps steps each after one warmup), plus its ranking fidelity on the relevance-structured
+    24-layer set (tests/golden/rerank_fidelity_v2m3.npz) in both precisions."""
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    from super_rag_amd.pipeline import SearchPipeline
+    from super_rag_amd import _native as N
+    rs = MODELS["bge-reranker-v2-m3"]
+    w = random_weights(rs, seed=13, style="hf")
+    rer = Encoder(rs, device=local, weights=w, max_tokens=a.rerank_max_tokens)
+    del w
+    out = {"model": "bge-reranker-v2-m3 (24 layers, 1024-d; seeded random weights)",
+           "workload": (f"rerank stage alone: {a.batch} queries x {a.k_cand} candidates, S_pair="
+                        f"{a.pair_len}, -> top-{a.k} (device pair packing + cross-encoder + select)"),
+           "steps": a.v2m3_steps, "warmup": 1}
+    try:
+        g = torch.Generator(device=dev)
+        g.manual_seed(17)
+        n_p = 1 << 20
+        p_tok = torch.randint(1000, rs.vocab_size, (n_p, a.passage_len), generator=g, device=dev,
+                              dtype=torch.int32)
+        p_len = torch.full((n_p,), a.passage_len, dtype=torch.int32, device=dev)
+        lq = a.q_len - 2
+        qtok = torch.randint(1000, rs.vocab_size, (a.batch, lq), generator=g, device=dev, dtype=torch.int32)
+        qlen = torch.full((a.batch,), lq, dtype=torch.int32, device=dev)
+        cand = torch.randint(0, n_p, (a.batch, a.k_cand), generator=g, device=dev, dtype=torch.int64)
+        pipe = SearchPipeline(None, rer, None, p_tok, p_len, k_candidates=a.k_cand, k_final=a.k,
+                              pair_len=a.pair_len)
+        for mode, name in ((0, "fp16"), (3, "fp8_mode3")):
+            rer.set_fp8(mode)
+            pipe.rerank(qtok, qlen, cand)
+            torch.cuda.synchronize()
+            N.profile_enable(True)
+            t0 = time.perf_counter()
+            for _ in range(a.v2m3_steps):
+                pipe.rerank(qtok, qlen, cand)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            N.profile_enable(False)
+            prof = N.profile_read()
+            out[f"{name}_qps"] = round(a.batch * a.v2m3_steps / dt, 2)
+            out[f"{name}_ms_per_step"] = round(dt / a.v2m3_steps * 1e3, 2)
+            out[f"{name}_roofline"] = {k: v for k, v in dominant_roofline(prof).items()
+                                       if k in ("kernel", "achieved", "peak", "unit", "frac")}
+        rer.set_fp8(0)
+    finally:
+        rer.close()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    fid = rerank_fidelity(rs, local, modes=((0, "fp16"), (3, "fp8_mode3")))
+    out["fidelity"] = ({m: f"{v['top10_identical_mod_ties']} top-10 identical, std/err "
+                           f"{v['min_std_over_err']}" for m, v in fid.items() if isinstance(v, dict)}
+                       if fid else None)
+    out["fidelity_detail"] = fid
+    return out
 
 
 def setup_workload(a, world, rank, local, dev):
@@ -517,17 +630,23 @@ def dominant_roofline(prof):
     return apply_pmc(roof, dom_name, prof.keys())
 
 
-def kernel_table(prof, steps):
+def kernel_table(prof, steps, top=None):
     """Per logical kernel: ms per step, launches, and its rate (TF/s against its flops, or GB/s of
-    algorithmic bytes for the memory kernels); fp8 GEMMs also as a fraction of the 5 PF/s peak."""
+    algorithmic bytes for the memory kernels); fp8 GEMMs also as a fraction of the 5 PF/s peak.
+    top: only the `top` kernels by time (the rest summed into "(others)")."""
     out = {}
-    for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["total_ms"]):
+    items = sorted(prof.items(), key=lambda kv: -kv[1]["total_ms"])
+    rest = items[top:] if top else []
+    for k, v in items[:top] if top else items:
         rate = (v["flops"] / 1e12 if v["flops"] > 0 else v["bytes"] / 1e9) / (v["total_ms"] * 1e-3)
         e = {"ms_per_step": round(v["total_ms"] / steps, 3), "launches": v["launches"],
              ("tflops" if v["flops"] > 0 else "gbs"): round(rate, 1)}
         if v["flops"] > 0 and (k.startswith("gemm_f8") or k.startswith("cosine_scan8")):
             e["frac_of_fp8_peak"] = round(rate / PEAK_F8_TFLOPS, 4)
         out[k] = e
+    if rest:
+        out["(others)"] = {"kernels": len(rest),
+                           "ms_per_step": round(sum(v["total_ms"] for _, v in rest) / steps, 3)}
     return out
 
 
@@ -564,6 +683,7 @@ def config5_field(a, world, rank, local, dev, dist, mode3_fidelity):
     W = setup_workload(a5, world, rank, local, dev)
     try:
         dt, prof = timed_steps(W, a5, world, dev, dist)
+        stage_ms5 = W.stage_ms
         recall = search_recall(W, a5, dev) if world == 1 else None
     finally:
         setup_s = W.setup_s
@@ -582,9 +702,10 @@ def config5_field(a, world, rank, local, dev, dist, mode3_fidelity):
         "corpus_rows": a5.corpus_rows, "rows_per_rank": shard_rows(a5.corpus_rows, world, rank),
         "recall_at_10": recall,
         "rerank_fp8_mode3_fidelity": mode3_fidelity,
+        "stage_ms": stage_ms5,
         "roofline": dominant_roofline(prof),
         "search_roofline": scan_roofline(prof),
-        "kernels": kernel_table(prof, a5.steps),
+        "kernels": kernel_table(prof, a5.steps, top=10),
         "setup_s": round(setup_s, 1),
     }
 
@@ -624,11 +745,13 @@ def timed_steps(W, a, world, dev, dist):
     synchronisation on both sides; the library's HIP-event profile of the timed region; the time
     is the max over ranks.  Returns (seconds, per-kernel profile)."""
     from super_rag_amd import _native as N
+    from super_rag_amd.pipeline import StageClock
     for i in range(a.warmup):
         W.pipe.run(*W.batches[i % a.batches])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    W.pipe.clock = StageClock()   # HIP events at the stage boundaries of every timed step
     N.profile_enable(True)
     torch.cuda.synchronize()
     if world > 1:
@@ -642,10 +765,18 @@ def timed_steps(W, a, world, dev, dist):
     dt = time.perf_counter() - t0
     N.profile_enable(False)
     prof = N.profile_read()
+    W.stage_ms = W.pipe.clock.read()
+    W.pipe.clock = None
     if world > 1:
         t = torch.tensor([dt], device=dev if a.dist_backend != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        # per-stage ms per step: the max over ranks of each stage (the exchange waits for the
+        # slowest rank, so its max is the critical one)
+        st = torch.tensor([W.stage_ms[k] for k in StageClock.STAGES], dtype=torch.float64,
+                          device=dev if a.dist_backend != "gloo" else "cpu")
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        W.stage_ms = {k: round(float(v), 4) for k, v in zip(StageClock.STAGES, st.tolist())}
     return dt, prof
 
 
@@ -708,7 +839,8 @@ def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
     return out
 
 
-def rerank_fidelity(rs, device):
+def rerank_fidelity(rs, device, modes=((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"),
+                                         (3, "fp8_mode3"))):
     """Ranking fidelity of the cross-encoder kernels at the bench shape (12 layers, 768-d, S_pair =
     128; bge-reranker-v2-m3's 24 layers, 1024-d with --rerank-model bge-reranker-v2-m3) on a
     DISCRIMINATIVE reranker: the relevance-structured weights of super_rag_amd/synthetic.py (the
@@ -738,7 +870,7 @@ def rerank_fidelity(rs, device):
                    f"fp32 oracle (tests/golden/{fixture})"),
            "logit_std_mean": round(float(std.mean()), 4)}
     try:
-        for mode, name in ((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"), (3, "fp8_mode3")):
+        for mode, name in modes:
             enc.set_fp8(mode)
             lg = enc.cross_score_dev(dids, dmask)[:, 0].float().cpu().numpy().reshape(ref.shape)
             err = np.abs(lg - ref).max(1)

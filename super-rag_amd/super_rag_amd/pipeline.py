@@ -21,6 +21,7 @@ all_to_all + K2 merge, so the fused candidates equal a single index's.
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 
 import torch
@@ -36,6 +37,54 @@ class PipelineResult:
     cand_rows: torch.Tensor    # [B, K] int64 search candidates (distance order)
     cand_sims: torch.Tensor    # [B, K] fp32 cosine similarity (distance = 1 - sim); rrf score
                                # of the fused candidates in hybrid mode
+
+
+class StageClock:
+    """Per-stage time of SearchPipeline.run (bench.py's stage_ms): marks at the stage boundaries,
+    each interval charged to the stage named by the mark that ends it -- embed, search (K1 / BM25
+    / K2 merge / rrf), exchange (C1 all_gather of the queries, C2 all_to_all of the per-shard lists,
+    the BM25 statistics all_reduce, C3 passage fetch) and rerank (pair packing, cross-encoder, top-k
+    select).  On device tensors a mark is a HIP event recorded on the current stream (the stream
+    every library kernel of the pipeline is launched on; an RCCL collective is ordered into it by
+    torch, so the event after a collective marks its completion); on host tensors (the gloo CPU
+    path) a perf_counter stamp.  Events are read back once, in read()."""
+
+    STAGES = ("embed", "search", "exchange", "rerank")
+
+    def __init__(self):
+        self.marks = []          # (stage, event or float) in issue order; None stage = start
+        self.steps = 0
+
+    def mark(self, stage, like=None):
+        dev = like is not None and like.is_cuda
+        if dev:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append((stage, e))
+        else:
+            self.marks.append((stage, time.perf_counter()))
+
+    def start(self, like=None):
+        self.steps += 1
+        self.mark(None, like)
+
+    def read(self) -> dict:
+        """{stage: ms per step} over the marks so far (synchronises recorded events)."""
+        tot = {s: 0.0 for s in self.STAGES}
+        prev = None
+        for stage, m in self.marks:
+            if stage is not None and prev is not None:
+                if isinstance(m, float) and isinstance(prev, float):
+                    dt = (m - prev) * 1e3
+                elif not isinstance(m, float) and not isinstance(prev, float):
+                    m.synchronize()
+                    dt = prev.elapsed_time(m)
+                else:  # (a host stamp next to an event: not comparable, not charged)
+                    dt = 0.0
+                tot[stage] += dt
+            prev = m
+        n = max(1, self.steps)
+        return {s: round(v / n, 4) for s, v in tot.items()}
 
 
 class SearchPipeline:
@@ -66,6 +115,11 @@ class SearchPipeline:
         self.exchange = self.world > 1 or bool(force_exchange)
         # passage_tok / passage_len hold only rows [shard_offset, shard_offset + len) (C3 fetch)
         self.shard_passages = bool(shard_passages) and self.exchange
+        self.clock: StageClock | None = None   # set a StageClock to time the stages of run()
+
+    def _mark(self, stage, like):
+        if self.clock is not None:
+            self.clock.mark(stage, like)
 
     def embed(self, q_ids: torch.Tensor, q_mask: torch.Tensor) -> torch.Tensor:
         return self.embedder.embed_dev(q_ids, q_mask, fp16=True)
@@ -83,8 +137,10 @@ class SearchPipeline:
         qx = q_emb.contiguous().cpu() if host else q_emb.contiguous()
         allq = torch.empty((self.world * B, q_emb.shape[1]), dtype=q_emb.dtype, device=qx.device)
         dist.all_gather_into_tensor(allq, qx, group=self.group)
-        sims, rows = self.store.search_dev(allq.to(dev) if host else allq, self.K,
-                                           row_offset=self.offset)
+        allq = allq.to(dev) if host else allq
+        self._mark("exchange", allq)                                        # C1
+        sims, rows = self.store.search_dev(allq, self.K, row_offset=self.offset)
+        self._mark("search", sims)
         return self._exchange(sims, rows, B, self.K, host, dev)
 
     def _exchange(self, sims, rows, B, k, host, dev):
@@ -97,8 +153,11 @@ class SearchPipeline:
         dist.all_to_all_single(rr, rows, group=self.group)
         if host:
             rs, rr = rs.to(dev), rr.to(dev)
-        return self.merge_fn(rs.view(self.world, B, k), rr.view(self.world, B, k), k,
-                             device=dev.index or 0)
+        self._mark("exchange", rs)                                          # C2
+        out = self.merge_fn(rs.view(self.world, B, k), rr.view(self.world, B, k), k,
+                            device=dev.index or 0)
+        self._mark("search", out[0])
+        return out
 
     def retrieve_hybrid(self, q_emb: torch.Tensor, q_tok: torch.Tensor, q_len: torch.Tensor):
         """Dense top-k_each + BM25 top-k_each (query tokens) fused by rrf -> (rrf score, rows)
@@ -125,21 +184,26 @@ class SearchPipeline:
                 dist.all_gather_into_tensor(out, x, group=self.group)
                 return out.to(dev) if host else out
             allq, toks, lens = gather(q_emb), gather(toks), gather(lens)
+            self._mark("exchange", allq)                                    # C1
             gst = self.lexical.query_stats_dev(toks, lens)
+            self._mark("search", gst)
             if host:
                 g = gst.cpu()
                 dist.all_reduce(g, group=self.group)
                 gst = g.to(dev)
             else:
                 dist.all_reduce(gst, group=self.group)
+            self._mark("exchange", gst)                                     # BM25 statistics
         sims, rows = self.store.search_dev(allq, ke, row_offset=self.offset)
         lsc, lrows = self.lexical.search_tok_dev(toks, lens, ke, gstats=gst, row_offset=self.offset)
+        self._mark("search", lsc)
         if self.exchange:
             import torch.distributed as dist
             host = dist.get_backend(self.group) == "gloo" and q_emb.is_cuda
             sims, rows = self._exchange(sims, rows, B, ke, host, dev)
             lsc, lrows = self._exchange(lsc, lrows, B, ke, host, dev)
         score, fused = rrf_fuse_dev(rows, lrows, self.K, self.rank_const)
+        self._mark("search", score)
         return score.float(), fused
 
     def passages(self, cand_rows: torch.Tensor):
@@ -174,6 +238,7 @@ class SearchPipeline:
         lq = rl.view(self.world, B * K).sum(0, dtype=self.p_len.dtype).to(dev)
         idx = torch.arange(B * K, device=dev, dtype=cand_rows.dtype).view(B, K)
         idx = torch.where(cand_rows >= 0, idx, torch.full_like(idx, -1))
+        self._mark("exchange", idx)                                         # C3
         return tq, lq, idx
 
     def rerank(self, q_tok: torch.Tensor, q_len: torch.Tensor, cand_rows: torch.Tensor):
@@ -185,13 +250,19 @@ class SearchPipeline:
         logits = self.reranker.cross_score_dev(ids, mask, types)[:, 0].view(B, self.K)
         logits = logits.masked_fill(cand_rows < 0, float("-inf"))
         idx = rerank_select_dev(logits, self.k).long()
-        return cand_rows.gather(1, idx), logits.gather(1, idx)
+        out = cand_rows.gather(1, idx), logits.gather(1, idx)
+        self._mark("rerank", out[1])
+        return out
 
     def run(self, q_ids, q_mask, q_tok, q_len) -> PipelineResult:
+        if self.clock is not None:
+            self.clock.start(q_ids)
         q = self.embed(q_ids, q_mask)
+        self._mark("embed", q)
         if self.lexical is not None:
             sims, rows = self.retrieve_hybrid(q, q_tok, q_len)
         else:
             sims, rows = self.retrieve(q)
+        self._mark("search", rows)
         final_rows, final_logits = self.rerank(q_tok, q_len, rows)
         return PipelineResult(final_rows, final_logits, rows, sims)

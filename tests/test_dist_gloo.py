@@ -237,3 +237,57 @@ def test_sharded_hybrid_retrieve_equals_single_index(world):
         s, rows = res[r]
         np.testing.assert_array_equal(rows, want_r[r * B:(r + 1) * B].numpy())
         np.testing.assert_array_equal(s, want_s[r * B:(r + 1) * B].float().numpy())
+
+
+def _clock_worker(rank, world, port, corpus, queries, p_tok, p_len, k, out_q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "super-rag_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from super_rag_amd.pipeline import SearchPipeline, StageClock
+    n = corpus.shape[0]
+    per = (n + world - 1) // world
+    r0, r1 = rank * per, min(n, (rank + 1) * per)
+    pipe = SearchPipeline(None, None, ShardStoreDouble(corpus[r0:r1]), p_tok[r0:r1].clone(),
+                          p_len[r0:r1].clone(), k_candidates=k, shard_offset=r0,
+                          merge_fn=merge_double, shard_passages=True)
+    pipe.clock = StageClock()
+    B = queries.shape[0] // world
+    mine = queries[rank * B:(rank + 1) * B]
+    for _ in range(3):                       # three steps: C1, shard search, C2, merge, C3
+        pipe.clock.start(mine)
+        _, rows = pipe.retrieve(mine)
+        pipe._mark("search", rows)
+        pipe.passages(rows)
+    out_q.put((rank, pipe.clock.read(), pipe.clock.steps))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_stage_clock_times_the_exchange_world_2():
+    # bench.py's stage_ms {embed, search, exchange, rerank} -- the exchange
+    # stage (C1 query all_gather, C2 all_to_all of the per-shard lists, C3 passage fetch) must be
+    # timed on its own and be present and positive at world 2
+    g = torch.Generator().manual_seed(6)
+    corpus = torch.randn(801, 16, generator=g)
+    queries = torch.randn(8, 16, generator=g)
+    p_tok = torch.randint(5, 3000, (801, 9), generator=g, dtype=torch.int32)
+    p_len = torch.full((801,), 9, dtype=torch.int32)
+    world = 2
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    port = 32500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_clock_worker,
+                         args=(r, world, port, corpus, queries, p_tok, p_len, 5, out_q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (st, n)) for r, st, n in (out_q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        st, n = res[r]
+        assert n == 3
+        assert set(st) == {"embed", "search", "exchange", "rerank"}
+        assert st["exchange"] > 0 and st["search"] > 0, st

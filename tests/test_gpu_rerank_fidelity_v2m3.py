@@ -9,7 +9,8 @@ fp32 oracle's logits committed in tests/golden/rerank_fidelity_v2m3.npz
                 query logit std >= RATIO_MIN x max |logit error|;
   fp8 mode 3    the same gate at RATIO_MIN_FP8 (FFN1 + FFN2 on the block-scaled fp8 MFMA).
 Twice bge-reranker-base's depth accumulates ~sqrt 2 its rounding error: fp16 measured std / err
->= 83.6 here (bge-reranker-base: >= 120), so the ratio floors sit below the base model's.
+>= 83.6 here (bge-reranker-base: >= 120), so the floors are the base model's gates (fp16 100,
+fp8 mode 3 50) scaled by 1 / sqrt 2: 70 and 35.
 """
 import os
 
@@ -19,7 +20,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 FIX = os.path.join(os.path.dirname(__file__), "golden", "rerank_fidelity_v2m3.npz")
-RATIO_MIN = 60.0       # fp16: measured >= 83.6 (max |err| 0.0068 .. 0.0105 at std 0.85 .. 1.02)
+RATIO_MIN = 70.0       # fp16: measured >= 83.6 (max |err| 0.0068 .. 0.0105 at std 0.85 .. 1.02)
 RATIO_MIN_FP8 = 35.0
 TIE_BAND = 0.01
 
