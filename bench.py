@@ -343,10 +343,11 @@ def run_bench(a, mp=None):
             drop_in["multi_process"] = mp.collect()
 
     # ---- roofline of the dominant kernel -------------------------------------------------------
-    roof = dominant_roofline(prof)
+    wl = "config5" if a.workload == "config5" and a.fp8 == 3 else None
+    roof = dominant_roofline(prof, wl)
     step_ms = dt / a.steps * 1e3
     kern = kernel_table(prof, a.steps, top=12)
-    search_roof = scan_roofline(prof)
+    search_roof = scan_roofline(prof, wl)
 
     # ---- CPU baseline: the oracle on a bounded sample (rank 0, N=1) ----------------------------
     cpu = None
@@ -608,7 +609,7 @@ def search_recall(W, a, dev, nq=32):
     return hit / (nq * a.k)
 
 
-def dominant_roofline(prof):
+def dominant_roofline(prof, workload=None):
     """Roofline record of the kernel with the largest total time: ALGORITHMIC flops (or bytes)
     of its launches / their summed HIP-event durations against the spec peak (5 PF/s for the fp8
     GEMMs, 2.5 PF/s f16, 8 TB/s HBM), with the PMC traffic of the committed summary."""
@@ -627,7 +628,7 @@ def dominant_roofline(prof):
                  "per_launch": (f"{dom['flops'] / dom['launches']:.4g} FLOP" if roof["bound"] == "mfma"
                                 else f"{dom['bytes'] / dom['launches']:.4g} B"),
                  "algorithmic_B_per_launch": round(dom["bytes"] / dom["launches"])})
-    return apply_pmc(roof, dom_name, prof.keys())
+    return apply_pmc(roof, dom_name, prof.keys(), workload=workload)
 
 
 def kernel_table(prof, steps, top=None):
@@ -650,7 +651,7 @@ def kernel_table(prof, steps, top=None):
     return out
 
 
-def scan_roofline(prof):
+def scan_roofline(prof, workload=None):
     """K1 (cosine_scan*) against HBM: the scans' algorithmic bytes / their time, and the ceiling
     max(bytes / 8 TB/s, flop / MFMA peak) (at B = 256 the scan sits at the ridge)."""
     scan = {k: v for k, v in prof.items() if k.startswith("cosine_scan")}
@@ -661,7 +662,8 @@ def scan_roofline(prof):
     search_roof = {"bound": "hbm", "achieved": round(sb / (sm * 1e-3) / 1e9, 1),
                    "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(sb / (sm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
-    apply_pmc(search_roof, "cosine_scan", prof.keys())
+    apply_pmc(search_roof, "cosine_scan8" if "cosine_scan8" in scan else "cosine_scan", prof.keys(),
+              workload=workload)
     search_roof.pop("pmc_provenance", None)  # (the same record as roofline's)
     mfma_s = sum(v["flops"] / ((PEAK_F8_TFLOPS if k.startswith("cosine_scan8") else PEAK_F16_TFLOPS) * 1e12)
                  for k, v in scan.items())
@@ -703,8 +705,8 @@ def config5_field(a, world, rank, local, dev, dist, mode3_fidelity):
         "recall_at_10": recall,
         "rerank_fp8_mode3_fidelity": mode3_fidelity,
         "stage_ms": stage_ms5,
-        "roofline": dominant_roofline(prof),
-        "search_roofline": scan_roofline(prof),
+        "roofline": dominant_roofline(prof, "config5"),
+        "search_roofline": scan_roofline(prof, "config5"),
         "kernels": kernel_table(prof, a5.steps, top=10),
         "setup_s": round(setup_s, 1),
     }
@@ -973,7 +975,17 @@ def _pmc_name(k):
     return PMC_ALIASES.get(k, k)
 
 
-def pmc_provenance(run_kernels, root=ROOT):
+def pmc_kernels(d, workload=None):
+    """The per-kernel records of a PMC summary for a workload: config 4 (the default bench) at the
+    top level, config 5's fp8 path under workloads.config5 (tools/pmc_traffic.py)."""
+    if d is None:
+        return {}
+    if workload in (None, "config4"):
+        return d.get("kernels", {})
+    return d.get("workloads", {}).get(workload, {}).get("kernels", {})
+
+
+def pmc_provenance(run_kernels, root=ROOT, workload=None):
     """Which PMC summary the roofline's `traffic` / `pmc_*` fields come from and whether it
     describes THIS run: the summary's commit and native-source fingerprint (recorded on the box by
     tools/profile_round.sh) against the running tree's, and the kernels timed here against the
@@ -986,7 +998,7 @@ def pmc_provenance(run_kernels, root=ROOT):
     if d is None:
         return None
     mine = {_pmc_name(k) for k in run_kernels}
-    theirs = {_pmc_name(k) for k in d.get("kernels", {})}
+    theirs = {_pmc_name(k) for k in pmc_kernels(d, workload)}
     fp = d.get("source_sha256")
     src_match = None if fp is None else fp == source_fingerprint(root)
     missing = sorted(mine - theirs)
@@ -995,21 +1007,21 @@ def pmc_provenance(run_kernels, root=ROOT):
         reasons.append("native sources differ from the profiled tree")
     if missing:
         reasons.append(f"kernels timed here but absent from the summary: {missing}")
-    return {"file": path, "commit": d.get("commit"), "source_sha256": fp,
+    return {"file": path, "workload": workload or "config4", "commit": d.get("commit"), "source_sha256": fp,
             "source_match": src_match, "kernel_set_match": not missing,
             "stale": bool(reasons), "stale_reasons": reasons}
 
 
-def pmc_record(kernel, root=ROOT):
+def pmc_record(kernel, root=ROOT, workload=None):
     """The kernel's record in the newest committed PMC summary (tools/pmc_traffic.py), or None."""
     _, d = pmc_file(root)
     if d is None:
         return None
-    ks = {_pmc_name(k): v for k, v in d["kernels"].items()}
+    ks = {_pmc_name(k): v for k, v in pmc_kernels(d, workload).items()}
     return ks.get(_pmc_name(kernel))
 
 
-def pmc_traffic(kernel, root=ROOT):
+def pmc_traffic(kernel, root=ROOT, workload=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes over this same bench command, gfx950 fetch correction applied).
@@ -1017,19 +1029,20 @@ def pmc_traffic(kernel, root=ROOT):
     path, d = pmc_file(root)
     if d is None:
         return None, None
-    k = pmc_record(kernel, root)
+    k = pmc_record(kernel, root, workload)
     if not k:
         return None, None
-    return k["traffic_B"], (f"{path}: fetch {k['fetch_B']} B + write "
+    where = f"{path}" + (f" [workloads.{workload}]" if workload not in (None, "config4") else "")
+    return k["traffic_B"], (f"{where}: fetch {k['fetch_B']} B + write "
                             f"{k['write_B']} B per launch (mean over {k['launches']} launches)")
 
 
-def apply_pmc(roof, kernel, run_kernels, root=ROOT):
+def apply_pmc(roof, kernel, run_kernels, root=ROOT, workload=None):
     """Fill roof["traffic"] (+ pmc clock / utilisation) from the PMC summary, with its provenance;
     a stale summary's numbers move to roof["stale_pmc"] and traffic stays null."""
-    traffic, src = pmc_traffic(kernel, root)
-    rec = pmc_record(kernel, root)
-    prov = pmc_provenance(run_kernels, root)
+    traffic, src = pmc_traffic(kernel, root, workload)
+    rec = pmc_record(kernel, root, workload)
+    prov = pmc_provenance(run_kernels, root, workload)
     roof["pmc_provenance"] = prov
     fields = {"traffic": traffic, "traffic_source": src}
     if rec and rec.get("clock_ghz") and roof.get("bound") == "mfma":
@@ -1038,6 +1051,9 @@ def apply_pmc(roof, kernel, run_kernels, root=ROOT):
         fields["pmc_clock_ghz"] = rec["clock_ghz"]
         fields["pmc_mfma_util"] = rec.get("mfma_util")
         fields["peak_at_held_clock"] = round(roof["peak"] * rec["clock_ghz"] / 2.4, 1)
+    if rec and rec.get("traffic_B") and roof.get("algorithmic_B_per_launch"):
+        # PMC traffic over the algorithmic bytes (> 1: re-reads beyond L2)
+        fields["traffic_over_algorithmic"] = round(rec["traffic_B"] / roof["algorithmic_B_per_launch"], 3)
     if prov and prov["stale"]:
         roof["traffic"] = None
         roof["stale_pmc"] = fields

@@ -142,3 +142,34 @@ def test_dropin_procs_release_and_collect(tmp_path):
     assert r["procs"] == 3 and r["qps"] == 303.0 and r["requests"] == 300
     assert r["p50_ms"] == 20.0 and r["p99_ms"] == 30.0
     assert not os.path.exists(mp.dir)
+
+
+def test_config5_workload_section(tmp_path):
+    """the config-5 field's roofline reads its own section of the summary
+    (workloads.config5: the fp8 path's kernels), never config 4's per-launch means of the same
+    kernel names; a summary without the section leaves it stale."""
+    root = _tree(tmp_path, ["gemm_a", "qkv_attention"], None)
+    sha = bench.source_fingerprint(root)
+    path = os.path.join(root, "profiles/r99_pmc_traffic.json")
+    with open(path) as f:
+        d = json.load(f)
+    d["source_sha256"] = sha
+    with open(path, "w") as f:
+        json.dump(d, f)
+    run5 = ["gemm_f8_lnfold_gelu_out8", "qkv_attention", "cosine_scan8"]
+    roof = {"bound": "mfma", "peak": 5000.0, "algorithmic_B_per_launch": 500}
+    bench.apply_pmc(roof, "gemm_f8_lnfold_gelu_out8", run5, root, workload="config5")
+    assert roof["traffic"] is None and roof["pmc_provenance"]["stale"]
+    d["workloads"] = {"config5": {"kernels": {k: {"launches": 2, "fetch_B": 700, "write_B": 300,
+                                                  "traffic_B": 1000, "clock_ghz": 1.9,
+                                                  "mfma_util": 0.6} for k in run5}}}
+    with open(path, "w") as f:
+        json.dump(d, f)
+    roof = {"bound": "mfma", "peak": 5000.0, "algorithmic_B_per_launch": 500}
+    bench.apply_pmc(roof, "qkv_attention", run5, root, workload="config5")
+    assert roof["traffic"] == 1000 and not roof["pmc_provenance"]["stale"]
+    assert roof["pmc_provenance"]["workload"] == "config5"
+    assert roof["traffic_over_algorithmic"] == 2.0 and roof["pmc_mfma_util"] == 0.6
+    roof4 = {"bound": "mfma", "peak": 2500.0}
+    bench.apply_pmc(roof4, "qkv_attention", ["gemm_a", "qkv_attention"], root)
+    assert roof4["traffic"] == 120          # config 4 keeps the top-level records

@@ -24,3 +24,12 @@ timeout -k 10 600 rocprofv3 -i tools/pmc_write.txt -d $OUT/write -o run --output
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_write.log 2>&1
 timeout -k 10 600 rocprofv3 -i tools/pmc_mfma.txt -d $OUT/mfma -o run --output-format csv -- \
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $OUT/bench_mfma.log 2>&1
+# 4. the same trace + three PMC passes over config 5's fp8 path (the line's config5 field: bge-m3
+#    embed, fp8 scan, BM25 + rrf, reranker in fp8 mode 3) -> $OUT/c5 (pmc_traffic.py: workloads.config5)
+C5="python3 bench.py --workload config5 --fp8 3 --no-cpu-baseline --no-extras"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/c5/trace -o run --output-format csv -- \
+  $C5 --steps 3 --warmup 1 > $OUT/c5_bench_trace.log 2>&1
+for P in fetch write mfma; do
+  timeout -k 10 600 rocprofv3 -i tools/pmc_$P.txt -d $OUT/c5/$P -o run --output-format csv -- \
+    $C5 --steps 1 --warmup 1 > $OUT/c5_bench_$P.log 2>&1
+done
