@@ -34,7 +34,7 @@ PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_F16_TFLOPS = 2500.0    # dense fp16/bf16 MFMA spec (no sparsity)
 PEAK_F8_TFLOPS = 5000.0     # dense fp8 MFMA spec (no sparsity)
 # compute dtype of the line per reranker precision mode (bench --fp8)
-FP8_DTYPES = {0: "f16", 1: "f16+fp8ffn", 2: "f16+fp8gemm", 3: "f16+fp8mlp"}
+FP8_DTYPES = {0: "f16", 1: "f16+fp8ffn", 2: "f16+fp8gemm", 3: "f16+fp8mlp", 5: "f16+fp8mlp+o"}
 
 
 def parse():
@@ -84,10 +84,11 @@ def parse():
     ap.add_argument("--fp8-ffn", action="store_true",
                     help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
                          "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
-    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3),
+    ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3, 5),
                     help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
-                         "e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16 "
-                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp)")
+                         "e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16, 5 = 3 "
+                         "+ the O-projection on e4m3 attention outputs (dtype f16+fp8ffn / "
+                         "f16+fp8gemm / f16+fp8mlp / f16+fp8mlp+o)")
     ap.add_argument("--replicate-passages", action="store_true",
                     help="N > 1: keep the whole passage token table on every rank (default: each "
                          "rank holds its shard's rows, the candidates' rows are fetched per batch, "
@@ -445,7 +446,8 @@ def summary(line):
         "drop_in": drop(line.get("drop_in")),
         "config5": {"value": c5["value"], "ms_per_step": c5["ms_per_step"],
                     "recall_at_10": c5.get("recall_at_10")} if c5 else None,
-        "v2m3": {k: v2.get(k) for k in ("fp16_qps", "fp8_mode3_qps", "fidelity")} if v2 else None,
+        "v2m3": {k: v2.get(k) for k in ("fp16_qps", "fp8_mode3_qps", "fp8_mode5_qps", "fidelity")}
+        if v2 else None,
     }
 
 
@@ -481,7 +483,7 @@ def v2m3_field(a, local, dev):
         cand = torch.randint(0, n_p, (a.batch, a.k_cand), generator=g, device=dev, dtype=torch.int64)
         pipe = SearchPipeline(None, rer, None, p_tok, p_len, k_candidates=a.k_cand, k_final=a.k,
                               pair_len=a.pair_len)
-        for mode, name in ((0, "fp16"), (3, "fp8_mode3")):
+        for mode, name in ((0, "fp16"), (3, "fp8_mode3"), (5, "fp8_mode5")):
             rer.set_fp8(mode)
             pipe.rerank(qtok, qlen, cand)
             torch.cuda.synchronize()
@@ -502,7 +504,7 @@ def v2m3_field(a, local, dev):
         rer.close()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-    fid = rerank_fidelity(rs, local, modes=((0, "fp16"), (3, "fp8_mode3")))
+    fid = rerank_fidelity(rs, local, modes=((0, "fp16"), (3, "fp8_mode3"), (5, "fp8_mode5")))
     out["fidelity"] = ({m: f"{v['top10_identical_mod_ties']} top-10 identical, std/err "
                            f"{v['min_std_over_err']}" for m, v in fid.items() if isinstance(v, dict)}
                        if fid else None)
@@ -842,7 +844,7 @@ def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
 
 
 def rerank_fidelity(rs, device, modes=((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"),
-                                         (3, "fp8_mode3"))):
+                                         (3, "fp8_mode3"), (5, "fp8_mode5"))):
     """Ranking fidelity of the cross-encoder kernels at the bench shape (12 layers, 768-d, S_pair =
     128; bge-reranker-v2-m3's 24 layers, 1024-d with --rerank-model bge-reranker-v2-m3) on a
     DISCRIMINATIVE reranker: the relevance-structured weights of super_rag_amd/synthetic.py (the

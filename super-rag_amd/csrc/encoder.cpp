@@ -186,8 +186,11 @@ static bool kvfree_cls_enabled() {
 void Encoder::set_fp8(int mode) {
   // mode 4 (QKV in fp8 on normalised e4m3 rows) was measured and rejected (DESIGN.md, round 4:
   // std / err 2.0, top-10 identical on 1 / 8 queries): the diagnostic library only
-  SR_CHECK(mode >= 0 && mode <= 3 || (SR_WITH_DIAG && mode == 4),
-           "encoder: fp8 mode must be 0 .. 3 (mode 4 is in the diagnostic library only)");
+  // mode 5 = mode 3 + the O-projection of the fused (K5c) layers on the block-scaled fp8 MFMA:
+  // K5c writes the attention output as e4m3 (a convex combination of V rows: no scale needed),
+  // the O-projection weight rows are e4m3 with one E8M0 exponent each
+  SR_CHECK((mode >= 0 && mode <= 3) || mode == 5 || (SR_WITH_DIAG && mode == 4),
+           "encoder: fp8 mode must be 0 .. 3 or 5 (mode 4 is in the diagnostic library only)");
   if (mode) {
     SR_CHECK(fold_enabled(), "encoder: fp8 modes need the LN-folded fp16-residual path");
     SR_CHECK(cfg_.intermediate % 128 == 0 && cfg_.intermediate >= 256 &&
@@ -227,6 +230,12 @@ void Encoder::prepare_fold(hipStream_t s) {
                                L.w1e.as<uint8_t>(), s);
       launch_colsum_fp8(L.w1_8.as<uint8_t>(), L.w1e.as<uint8_t>(), (int)F, (int)D,
                         L.c1_8.as<float>(), s);
+    }
+    if (fp8_ == 5) {
+      L.wo_8.reserve((size_t)D * D);
+      L.woe.reserve((size_t)D);
+      launch_quantize_rows_fp8(L.wo.as<half_t>(), (int)D, (int)D, L.wo_8.as<uint8_t>(),
+                               L.woe.as<uint8_t>(), s);
     }
     L.b2_f.reserve((size_t)D * sizeof(float));  // FFN2 bias + beta of LN1 (rebuilt residual)
     launch_vec_add(L.b2.as<float>(), L.ln1b.as<float>(), L.b2_f.as<float>(), (int)D, s);
@@ -371,6 +380,10 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
       // NORMALISED rows (u - mu) rstd (its own pass after the row statistics; unfused)
       const bool ffn1_8 = fp8_ >= 2, qkv_8 = fp8_ == 2 || fp8_ == 4, qkv_norm8 = fp8_ == 4;
       const bool fuse_qa = fused_qkv_attention_enabled() && !qkv_8 && qkv_attention_supported(S, d, H);
+      // mode 5: the fused layers' ctx as e4m3 (in the FFN buffer, dead until this layer's FFN1)
+      // and their O-projection on the fp8 MFMA
+      const bool o8 = fp8_ == 5 && fuse_qa;
+      uint8_t* ctx8 = reinterpret_cast<uint8_t*>(ffn);
       // (qkv_8: mode 2 keeps the e4m3 QKV path in every layer)
       const bool kvfree = cls_only && !qkv_8 && kvfree_cls_enabled() && layers_.size() > 1 &&
                           cls_attn_fold_supported(S, d, H) && layers_.back().wk_bd.p != nullptr;
@@ -384,10 +397,10 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
           lq.colsum = L.cqkv.as<float>();
           if (l == 0)
             launch_qkv_attention(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr,
-                                 cmask, ctx, nb, S, d, H, s);
+                                 cmask, ctx, nb, S, d, H, s, o8 ? ctx8 : nullptr);
           else
             launch_qkv_attention(EPI_LNF_F16, U, d, L.wqkv_f.as<half_t>(), L.dqkv.as<float>(), &lq,
-                                 cmask, ctx, nb, S, d, H, s);
+                                 cmask, ctx, nb, S, d, H, s, o8 ? ctx8 : nullptr);
         } else if (l == 0) {
           launch_gemm(EPI_BIAS_F16, U, d, L.wqkv.as<half_t>(), L.bqkv.as<float>(), nullptr, 0, qkv,
                       3 * d, M, 3 * d, d, s);
@@ -451,9 +464,15 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
         lo.y8 = ffn1_8 ? u8 : nullptr;  // e4m3 copy of u1 for the fp8 FFN1
         const int eo = ffn1_8 ? (l == 0 ? EPI_RES16_STATS_Y8 : EPI_LNR16_STATS_Y8)
                                  : (l == 0 ? EPI_RES16_STATS : EPI_LNR16_STATS);
-        launch_gemm(eo, ctx, d, L.wo.as<half_t>(),
-                    (l == 0 ? L.bo : L.bo_f).as<float>(), U, last ? (int64_t)S * d : d, Uo, d, Mr,
-                    d, d, s, &lo);
+        if (o8 && !last) {  // e4m3 ctx (K5c) x e4m3 W_o rows on the block-scaled fp8 MFMA
+          lo.wexp = L.woe.as<uint8_t>();
+          launch_gemm_f8w(eo, ctx8, d, L.wo_8.as<uint8_t>(), (l == 0 ? L.bo : L.bo_f).as<float>(), U,
+                          d, Uo, d, Mr, d, d, s, &lo);
+        } else {
+          launch_gemm(eo, ctx, d, L.wo.as<half_t>(),
+                      (l == 0 ? L.bo : L.bo_f).as<float>(), U, last ? (int64_t)S * d : d, Uo, d, Mr,
+                      d, d, s, &lo);
+        }
         launch_ln_stats_finalize(sA, nparts, cfg_.ln_eps, Mr, mA, s);
         // FFN1 on LN1(u1) folded; FFN2 + residual LN1(u1) -> u2 (in place) + partials sB
         LnFold l1;

@@ -804,8 +804,11 @@ __device__ __forceinline__ half8 qa_frag(const half_t* t, int row, int chunk) {
   } while (0)
 
 // DIAG (timing experiments only, wrong results): 1 = no K-loop (epilogue + attention on zero
-// accumulators), 2 = no attention (the K-loop and the LDS epilogue only)
-template <bool LNF, int DIAG = 0>
+// accumulators), 2 = no attention (the K-loop and the LDS epilogue only).
+// CTX8: ctx is written as OCP e4m3 bytes (fp8 mode 5: the O-projection's operand on the
+// block-scaled fp8 MFMA), 8 B per lane store instead of 16 -- same store count, so the vmcnt
+// bookkeeping below is unchanged.
+template <bool LNF, int DIAG = 0, bool CTX8 = false>
 __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const float* __restrict__ colsum, const float* __restrict__ mr,
@@ -1101,15 +1104,24 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         const int q = m0 + sq * 128 + qw + 16 * u + (lane & 15);
 #pragma unroll
         for (int p2 = 0; p2 < 2; ++p2) {
-          half8 hv;
+          float cv[8];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[u][2 * p2][r]),
                                                              __float_as_uint(o[u][2 * p2 + 1][r]), false, false);
-            hv[r] = (half_t)(__uint_as_float(sw[0]) * inv);
-            hv[4 + r] = (half_t)(__uint_as_float(sw[1]) * inv);
+            cv[r] = __uint_as_float(sw[0]) * inv;
+            cv[4 + r] = __uint_as_float(sw[1]) * inv;
           }
-          *reinterpret_cast<half8*>(ctx + (int64_t)q * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2)) = hv;
+          const int64_t co = (int64_t)q * d + h * DH + 32 * p2 + 16 * odd + 4 * (g & 2);
+          if constexpr (CTX8) {
+            const uint2 b8{e4m3x4(cv[0], cv[1], cv[2], cv[3]), e4m3x4(cv[4], cv[5], cv[6], cv[7])};
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(ctx) + co) = b8;
+          } else {
+            half8 hv;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) hv[r] = (half_t)cv[r];
+            *reinterpret_cast<half8*>(ctx + co) = hv;
+          }
         }
       }
     }  // attend
@@ -1193,7 +1205,7 @@ bool qkv_attention_supported(int S, int d, int heads) {
 
 void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                           const LnFold* lf, const int32_t* mask, half_t* ctx, int B, int S, int d,
-                          int heads, hipStream_t stream) {
+                          int heads, hipStream_t stream, uint8_t* ctx8) {
   SR_CHECK(qkv_attention_supported(S, d, heads), "qkv_attention: needs S == 128 and d_h == 64");
   SR_CHECK(epi == EPI_BIAS_F16 || (epi == EPI_LNF_F16 && lf && lf->mr && lf->colsum && lf->stat_ld == 1),
            "qkv_attention: epilogue EPI_BIAS_F16 or EPI_LNF_F16 (row statistics + column sums)");
@@ -1202,7 +1214,7 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   const int64_t M = (int64_t)B * S;
   SR_CHECK(M < (1ll << 31) / 3, "qkv_attention: too many tokens");
   const double flops = 2.0 * M * 3.0 * d * d + 4.0 * B * heads * (double)S * S * 64;
-  const double bytes = 2.0 * M * d * 2 + 2.0 * 3 * d * (double)d + 4.0 * M;
+  const double bytes = 2.0 * M * d + (ctx8 ? 1.0 : 2.0) * M * d + 2.0 * 3 * d * (double)d + 4.0 * M;
   ProfScope prof("qkv_attention", stream, flops, bytes);
   const float scale_log2 = 1.4426950408889634f / 8.0f;
   const int64_t tiles = ceil_div(M, 256) * heads;
@@ -1222,7 +1234,15 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
                        lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
   else
 #endif
-  if (epi == EPI_LNF_F16)
+  if (ctx8) {  // fp8 mode 5: e4m3 ctx for the O-projection on the block-scaled fp8 MFMA
+    half_t* c8 = reinterpret_cast<half_t*>(ctx8);
+    if (epi == EPI_LNF_F16)
+      hipLaunchKernelGGL((qkv_attn_kernel<true, 0, true>), grid, block, 0, stream, X, lda, W, bias,
+                         lf->colsum, lf->mr, mask, c8, (int)M, d, heads, scale_log2);
+    else
+      hipLaunchKernelGGL((qkv_attn_kernel<false, 0, true>), grid, block, 0, stream, X, lda, W, bias,
+                         nullptr, nullptr, mask, c8, (int)M, d, heads, scale_log2);
+  } else if (epi == EPI_LNF_F16)
     hipLaunchKernelGGL(qkv_attn_kernel<true>, grid, block, 0, stream, X, lda, W, bias, lf->colsum,
                        lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
   else

@@ -107,10 +107,11 @@ void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* l
 // sequence; ctx rows are laid out [B][Sq][d].
 // K5c (k_attention.hip): ctx = attention(epi(X . Wqkv^T)) without the QKV activation in HBM;
 // epi = EPI_BIAS_F16 or EPI_LNF_F16 (lf: row statistics mr, column sums colsum).  S == 128, d_h == 64.
+// ctx8 != nullptr: ctx is written there as OCP e4m3 bytes instead ([B*S, d], fp8 mode 5).
 bool qkv_attention_supported(int S, int d, int heads);
 void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                           const LnFold* lf, const int32_t* mask, half_t* ctx, int B, int S, int d,
-                          int heads, hipStream_t stream);
+                          int heads, hipStream_t stream, uint8_t* ctx8 = nullptr);
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
                       int d, int heads, hipStream_t stream);
 void attention_force_variant(int v);  // test hook: -1 auto, 0 = 64-key-tile kernel, 1 = K5b, 2 = K5b with 8 waves

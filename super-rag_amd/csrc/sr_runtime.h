@@ -199,6 +199,7 @@ class Encoder {
     // fp8 modes: e4m3 copies of w2h (FFN) and of the folded w1_f / wqkv_f (all), their per-row
     // exponents and the folded column sums of the quantised weights
     DevBuf w2_8, w2e, w1_8, w1e, c1_8, wqkv8, wqkve, cqkv8;
+    DevBuf wo_8, woe;  // fp8 mode 5: e4m3 rows of the O-projection weight + their E8M0 exponents
     // K/V-free CLS-only last layer: block-diagonal K / V weights, zero bias (H*D)
     DevBuf wk_bd, wv_bd, zb;
   };

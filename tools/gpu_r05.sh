@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-5 GPU validation, tag $1, parts $2 (comma list):
+#   c3     test_config3 with its printed error figures (-s)
+#   tests  the whole -m gpu suite
+#   smoke  __graft_entry__.smoke()
+#   bench  the driver's default bench (20 / 5)
+#   prof   tools/profile_round.sh (rocprofv3 trace + PMC, config 4 and config 5's fp8 path)
+TAG=${1:?tag}; PARTS=${2:-tests,smoke,bench}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG
+for P in ${PARTS//,/ }; do
+  case $P in
+    c3) timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -k config3 -x -v -s --timeout 240 --timeout-method thread > gpurun_out/$TAG/c3.log 2>&1 || exit 1 ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=15 > gpurun_out/$TAG/gpu_tests.log 2>&1 || exit 1 ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$TAG/smoke.log 2>&1 || exit 1 ;;
+    bench) timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$TAG/bench_20x5.log 2>&1 || exit 1 ;;
+    modes) for M in 3 5; do
+             timeout -k 10 300 python -u bench.py --fp8 $M --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/$TAG/bench_fp8m$M.log 2>&1 || exit 1
+             timeout -k 10 400 python -u bench.py --workload config5 --fp8 $M --steps 10 --warmup 3 --no-extras > gpurun_out/$TAG/bench_c5_fp8m$M.log 2>&1 || exit 1
+           done ;;
+    prof) rm -rf gpurun_out/prof_$TAG && bash tools/profile_round.sh $TAG > gpurun_out/$TAG/profile_round.log 2>&1 || exit 1
+          python3 tools/pmc_traffic.py gpurun_out/prof_$TAG gpurun_out/$TAG/${TAG}_pmc_traffic.json > gpurun_out/$TAG/pmc_traffic.log 2>&1 || exit 1
+          python3 tools/rocprof_vs_bench.py gpurun_out/prof_$TAG > gpurun_out/$TAG/rocprof_vs_bench.txt 2>&1 || exit 1
+          cp gpurun_out/prof_$TAG/trace/run_kernel_stats.csv gpurun_out/$TAG/${TAG}_rocprof_kernel_stats.csv
+          cp gpurun_out/prof_$TAG/c5/trace/run_kernel_stats.csv gpurun_out/$TAG/${TAG}_c5_rocprof_kernel_stats.csv 2>/dev/null
+          find gpurun_out/prof_$TAG -name "*.csv" -size +1M -delete ;;
+    *) echo "unknown part $P"; exit 2 ;;
+  esac
+done
+exit 0
