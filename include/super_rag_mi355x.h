@@ -208,7 +208,10 @@ int sr_lex_search_dev(sr_lex* x, const int64_t* qoff, const int32_t* qterms, int
                       const sr_lex_global* global, float* out_score, int64_t* out_rows,
                       int64_t row_offset, void* stream);
 /* Device-resident queries (the batched hybrid pipeline: query tokens already in HBM, no host copy
- * and no synchronisation).  tok: B x Lq int32 device (row stride Lq), qlen: B int32 device.
+ * of the queries).  Asynchronous on `stream` when the batch fits one worst-case query group
+ * (B x Lq x max df keys within the 2 GiB key budget, B <= 1024); a larger batch is grouped by the
+ * queries' actual candidate caps, computed on the device and read back ONCE (one blocking
+ * hipStreamSynchronize on `stream`, which also waits for work queued before it).  tok: B x Lq int32 device (row stride Lq), qlen: B int32 device.
  * sr_lex_query_stats_dev writes out_stats[0] = live rows, [1] = summed document length, [2 + q Lq +
  * i] = live df of query q's i-th token (0 past qlen[q]): 2 + B Lq int64 on the device, the vector a
  * row-sharded corpus sums over its shards (one all-reduce).  sr_lex_search_tok_dev = sr_lex_search_dev

@@ -47,6 +47,15 @@ int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, co
                  const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
                  int N, int K, int device, void* stream);
 
+/* Diagnostic: the residual + row-statistics GEMM epilogue (EPI_RES16_STATS, the encoders'
+ * O-projection / FFN2 of layer 0) on device buffers: Y = fp16(X W^T + bias + R) (X M x K fp16, W
+ * N x K fp16, bias N fp32, R / Y M x N fp16, row strides ldr / ldy, N % 256 == 0) and per row m and
+ * 128-column span s the partials stat_out[(m * N / 128 + s) * 2 + {0, 1}] = (sum, M2) of the fp16
+ * outputs of that span (the LayerNorm statistics ln_stats_finalize combines). */
+int sr_diag_gemm_stats(const void* X, int64_t lda, const void* W, const float* bias, const void* R,
+                       int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, float* stat_out,
+                       int device, void* stream);
+
 /* Diagnostic: device-to-device copy of `bytes` (multiple of 16) with 16-byte lanes, the HBM
  * yardstick bench.py reports beside the spec peak (no reference counterpart). */
 int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream);

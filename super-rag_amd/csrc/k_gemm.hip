@@ -751,18 +751,31 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       } else {
         // one pass: sum and sum of squares of the fp16 values (1: fp32 add + fma per value, 2:
         // v_dot2c_f32_f16 per value pair -- the products of fp16 values are exact in fp32), then
-        // M2 = sq - sum^2 / 128 per 128-column span (fp32; the span's values are 128 different
-        // hidden dimensions, so sq / 128 is never within a few ulps of mean^2)
+        // M2 = sq - sum^2 / 128 per 128-column span.
+        // Mode 2 takes the squares around a PIVOT c, the row's first value in the span (lane
+        // m & 15's hv[0][0], shared by a shuffle): sq = sum (x - c)^2 with x - c in fp16 (exact by
+        // Sterbenz whenever x is within a factor 2 of c, i.e. exactly in the large-offset rows
+        // where sq - sum^2 / 128 would cancel; else rounded to 2^-11 of |x - c|), the sum stays
+        // the exact sum of x, and M2 = sq - (sum - 128 c)^2 / 128 (rows with mean >>
+        // std lost every digit of M2 to the cancellation; tests/test_gpu_gemm.py
+        // test_stats_epilogue_large_offset_rows)
         float sq = 0.f;
+        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+        h2v c2 = {(_Float16)0.f, (_Float16)0.f};
+        if constexpr (SR_GEMM_STATS_MODE == 2) {
+          const _Float16 c = __builtin_bit_cast(
+              _Float16, (unsigned short)__shfl(__builtin_bit_cast(unsigned short, hv[0][0]), lane & 15, 64));
+          c2 = h2v{c, c};
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           if constexpr (SR_GEMM_STATS_MODE == 2) {
-            typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 #pragma unroll
             for (int r = 0; r < 8; r += 2) {
               const h2v x2 = {hv[p][r], hv[p][r + 1]};
+              const h2v d2 = x2 - c2;
               sum = __builtin_amdgcn_fdot2(x2, h2v{(_Float16)1.f, (_Float16)1.f}, sum, false);
-              sq = __builtin_amdgcn_fdot2(x2, x2, sq, false);
+              sq = __builtin_amdgcn_fdot2(d2, d2, sq, false);
             }
           } else {
 #pragma unroll
@@ -777,7 +790,8 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         sq += __shfl_xor(sq, 16, 64);
         sum += __shfl_xor(sum, 32, 64);
         sq += __shfl_xor(sq, 32, 64);
-        m2 = fmaxf(fmaf(-sum * (1.f / 128.f), sum, sq), 0.f);
+        const float sp = SR_GEMM_STATS_MODE == 2 ? fmaf(-128.f, (float)c2[0], sum) : sum;
+        m2 = fmaxf(fmaf(-sp * (1.f / 128.f), sp, sq), 0.f);
       }
       if (g == 0 && (!CHECK || m_row < M)) {
         float2 st;

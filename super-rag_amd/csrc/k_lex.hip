@@ -52,6 +52,9 @@ constexpr int LEX_RB = SR_LEX_RB;      // rows per accumulation block (32 KiB of
 constexpr int LEX_THREADS = 512;
 constexpr float LEX_SCALE = 65536.f;   // fixed-point unit of the accumulated score
 constexpr int64_t LEX_KEY_BUDGET = (int64_t)1 << 28;  // candidate keys per query block (2 GiB)
+// term ids are dense vocabulary indices (lexical.Vocab, or a model's token ids: <= 250,002); the
+// device offset table holds vocab + 1 int64, so 2^26 ids bound it at 512 MiB
+constexpr int32_t kLexMaxVocab = (int32_t)1 << 26;
 
 struct LexTerm {  // one distinct term of one query
   int64_t start;  // first posting of the term
@@ -556,7 +559,7 @@ void LexIndex::add(const int64_t* off, const int32_t* terms, const int32_t* tf, 
     SR_CHECK(off[i + 1] >= off[i], "lex.add: off must be non-decreasing");
     SR_CHECK(dl[i] >= 0, "lex.add: negative document length");
     for (int64_t p = off[i]; p < off[i + 1]; ++p) {
-      SR_CHECK(terms[p] >= 0, "lex.add: negative term id");
+      SR_CHECK(terms[p] >= 0 && terms[p] < kLexMaxVocab, "lex.add: term id out of range [0, 2^26)");
       SR_CHECK(tf[p] >= 1, "lex.add: term frequency must be >= 1");
       val[(size_t)p] = ((uint64_t)(rows_ + i) << 32) | (uint32_t)tf[p];
       vocab_ = std::max<int64_t>(vocab_, (int64_t)terms[p] + 1);
@@ -1058,14 +1061,17 @@ LexIndex* LexIndex::load(const char* path, int device) {
   }
   std::fclose(f);
   if (!ok) throw Error(SR_ERR_IO, std::string("lex.load: not a valid lexical snapshot: ") + path);
-  // contents the kernels index by: document lengths >= 0, terms >= 0, postings in row order with
-  // rows < n_rows and tf >= 1 (a corrupt posting would address past the device arrays)
+  // contents the kernels index by: document lengths >= 0, terms in [0, kLexMaxVocab) (a term id
+  // sizes the device offset table: a corrupt one near 2^31 asked for ~16 GiB), postings
+  // in row order with rows < n_rows and tf >= 1 (a corrupt posting would address past the device
+  // arrays)
   for (int64_t r = 0; r < rows && ok; ++r) ok = dl[(size_t)r] >= 0;
   int64_t prev = 0;
   for (int64_t i = 0; i < P && ok; ++i) {
     const int64_t row = (int64_t)(fv[(size_t)i] >> 32);
     const uint32_t tf = (uint32_t)(fv[(size_t)i] & 0xffffffffu);
-    ok = ft[(size_t)i] >= 0 && row < rows && row >= prev && tf >= 1 && tf < (1u << 31);
+    ok = ft[(size_t)i] >= 0 && ft[(size_t)i] < kLexMaxVocab && row < rows && row >= prev && tf >= 1 &&
+         tf < (1u << 31);
     prev = row;
   }
   if (!ok) throw Error(SR_ERR_IO, std::string("lex.load: corrupt postings in ") + path);

@@ -265,7 +265,10 @@ class NativeLexIndex:
         """BM25 top-k of device-resident queries (query i = tok[i, :qlen[i]], term ids) -> device
         (score [B, k] fp32, rows [B, k] int64 + row_offset); gstats: the all-reduced
         query_stats_dev vector of a row-sharded corpus, or None for this index's own statistics.
-        Identical results to search_dev on the same queries, without the host round trip."""
+        Identical results to search_dev on the same queries, without a host copy of the queries;
+        asynchronous unless the batch exceeds one worst-case query group (B x Lq x max df keys
+        over the 2 GiB budget, or B > 1024): then the device-computed per-query caps are read back
+        once (one synchronisation of `stream`) to size the groups."""
         import torch
         tok, qlen = _dev_i32(tok), _dev_i32(qlen)
         B, Lq = tok.shape

@@ -186,6 +186,9 @@ int main(int argc, char** argv) {
   lex_case("postings out of row order", [](Lex& x) { std::swap(x.fv[1], x.fv[2]); });
   lex_case("zero term frequency", [](Lex& x) { x.fv[0] = 0; });
   lex_case("negative term id", [](Lex& x) { x.ft[1] = -5; });
+  // a term id sizes the device offset table (vocab + 1 int64): near 2^31 it asked for ~16 GiB
+  lex_case("huge term id", [](Lex& x) { x.ft[1] = 0x7ffffff0; });
+  lex_case("term id 2^26", [](Lex& x) { x.ft[2] = 1 << 26; });
   lex_case("negative document length", [](Lex& x) { x.dl[1] = -1; });
   lex_case("k1 NaN", [](Lex& x) { x.k1 = std::numeric_limits<float>::quiet_NaN(); });
   lex_case("b infinite", [](Lex& x) { x.b = std::numeric_limits<float>::infinity(); });

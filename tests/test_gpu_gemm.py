@@ -110,3 +110,40 @@ def test_gemm_split_weights_match_fp32_weights(variant, epi):
     assert err <= out_round + 2e-5, f"{variant} epi{epi}: {err:.3e}"
     if epi == 2:   # fp32 output: the split is visibly more exact than fp16 weights
         assert err < 0.1 * err_h, (err, err_h)
+
+
+@pytest.mark.parametrize("offset", [0.0, 40.0, -300.0])
+@pytest.mark.parametrize("M", [600, 4096])
+def test_stats_epilogue_large_offset_rows(offset, M):
+    """the *_STATS epilogues' one-pass span partials (sum, M2) feed every folded
+    LayerNorm.  M2 = sq - sum^2 / 128 lost every digit on rows whose mean >> std; with the pivot
+    (the span's first value) the partials must match a two-pass fp64 computation on the SAME fp16
+    outputs for rows with |mean| / std up to ~600, and stay exact-ish for centred rows."""
+    import numpy as np
+    import torch
+    from super_rag_amd import _native as NT
+    dev = torch.device("cuda", 0)
+    N, K = 768, 256
+    g = torch.Generator(device=dev).manual_seed(int(M + abs(offset)))
+    X = (torch.randn(M, K, device=dev, generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device=dev, generator=g) * 0.02).half()
+    b = torch.full((N,), offset, device=dev) + torch.randn(N, device=dev, generator=g) * 0.1
+    # residual rows: a per-row offset on top (some rows at 3x the common offset), spread ~0.5
+    R = (torch.randn(M, N, device=dev, generator=g) * 0.5
+         + offset * 2.0 * (torch.arange(M, device=dev) % 3 == 0).float()[:, None]).half()
+    Y = torch.empty(M, N, device=dev, dtype=torch.float16)
+    st = torch.full((M, N // 128, 2), float("nan"), device=dev)
+    NT.call_diag("sr_diag_gemm_stats", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(), N,
+                 Y.data_ptr(), N, M, N, K, st.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    y = Y.double().cpu().numpy().reshape(M, N // 128, 128)
+    s = st.double().cpu().numpy()
+    mean = y.mean(-1)
+    m2 = ((y - mean[..., None]) ** 2).sum(-1)
+    ref = X.float() @ W.float().T + b + R.float()
+    assert (Y.float() - ref).abs().max().item() <= 2e-3 * max(1.0, ref.abs().max().item())
+    np.testing.assert_allclose(s[..., 0], y.sum(-1), rtol=1e-6, atol=1e-3)
+    rel = np.abs(s[..., 1] - m2) / m2
+    ratio = np.abs(mean) / np.sqrt(m2 / 128)
+    print(f"offset {offset}: max |mean|/std {ratio.max():.0f}, max rel M2 err {rel.max():.2e}")
+    assert rel.max() <= 2e-3, rel.max()
