@@ -90,7 +90,7 @@ def main():
             ms = e0.elapsed_time(e1) / a.reps
             res[d].append((fl / ms / 1e9, ms))
     names = {0: "product", 2: "main loop only", 5: "math, no stores", 6: "stores, no math",
-             7: "stores to tile 0"}
+             7: "stores to tile 0", 8: "one storer (OST)"}
     for d in diags:
         v = sorted(res[d])
         tf, ms = v[len(v) // 2]

@@ -23,6 +23,9 @@ for P in ${PARTS//,/ }; do
           cp gpurun_out/prof_$TAG/trace/run_kernel_stats.csv gpurun_out/$TAG/${TAG}_rocprof_kernel_stats.csv
           cp gpurun_out/prof_$TAG/c5/trace/run_kernel_stats.csv gpurun_out/$TAG/${TAG}_c5_rocprof_kernel_stats.csv 2>/dev/null
           find gpurun_out/prof_$TAG -name "*.csv" -size +1M -delete ;;
+    ffn1) timeout -k 10 300 python -u tools/ffn1_bench.py --diags ${FFN1_DIAGS:-0,8,2} --rounds 3 > gpurun_out/$TAG/ffn1.log 2>&1 || exit 1
+          timeout -k 10 300 python -u tools/ffn1_bench.py --M 1638400 --diags ${FFN1_DIAGS:-0,8,2} --rounds 3 > gpurun_out/$TAG/ffn1_1638k.log 2>&1 || exit 1 ;;
+    ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
 done
