@@ -85,10 +85,10 @@ def parse():
                     help="reranker in the opt-in fp8 FFN precision mode (e4m3 FFN activations, "
                          "block-scaled fp8 MFMA for FFN2); reported with dtype f16+fp8ffn")
     ap.add_argument("--fp8", type=int, default=0, choices=(0, 1, 2, 3, 5),
-                    help="reranker fp8 precision mode: 1 = --fp8-ffn, 2 = also FFN1 and QKV on "
-                         "e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16, 5 = 3 "
-                         "+ the O-projection on e4m3 attention outputs (dtype f16+fp8ffn / "
-                         "f16+fp8gemm / f16+fp8mlp / f16+fp8mlp+o)")
+                    help="reranker fp8 precision mode: 1 = --fp8-ffn (FFN2), 2 = also FFN1 and QKV "
+                         "on e4m3 residual copies, 3 = FFN1 + FFN2 fp8 with QKV + attention fp16 "
+                         "(dtype f16+fp8ffn / f16+fp8gemm / f16+fp8mlp); the rejected mode 5 (3 + "
+                         "the O-projection on e4m3 ctx) only with SUPER_RAG_AMD_LIB=<libsrmi_diag.so>")
     ap.add_argument("--replicate-passages", action="store_true",
                     help="N > 1: keep the whole passage token table on every rank (default: each "
                          "rank holds its shard's rows, the candidates' rows are fetched per batch, "
@@ -446,8 +446,7 @@ def summary(line):
         "drop_in": drop(line.get("drop_in")),
         "config5": {"value": c5["value"], "ms_per_step": c5["ms_per_step"],
                     "recall_at_10": c5.get("recall_at_10")} if c5 else None,
-        "v2m3": {k: v2.get(k) for k in ("fp16_qps", "fp8_mode3_qps", "fp8_mode5_qps", "fidelity")}
-        if v2 else None,
+        "v2m3": {k: v2.get(k) for k in ("fp16_qps", "fp8_mode3_qps", "fidelity")} if v2 else None,
     }
 
 
@@ -483,7 +482,7 @@ def v2m3_field(a, local, dev):
         cand = torch.randint(0, n_p, (a.batch, a.k_cand), generator=g, device=dev, dtype=torch.int64)
         pipe = SearchPipeline(None, rer, None, p_tok, p_len, k_candidates=a.k_cand, k_final=a.k,
                               pair_len=a.pair_len)
-        for mode, name in ((0, "fp16"), (3, "fp8_mode3"), (5, "fp8_mode5")):
+        for mode, name in ((0, "fp16"), (3, "fp8_mode3")):
             rer.set_fp8(mode)
             pipe.rerank(qtok, qlen, cand)
             torch.cuda.synchronize()
@@ -504,7 +503,7 @@ def v2m3_field(a, local, dev):
         rer.close()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-    fid = rerank_fidelity(rs, local, modes=((0, "fp16"), (3, "fp8_mode3"), (5, "fp8_mode5")))
+    fid = rerank_fidelity(rs, local, modes=((0, "fp16"), (3, "fp8_mode3")))
     out["fidelity"] = ({m: f"{v['top10_identical_mod_ties']} top-10 identical, std/err "
                            f"{v['min_std_over_err']}" for m, v in fid.items() if isinstance(v, dict)}
                        if fid else None)
@@ -844,7 +843,7 @@ def search_b32(store, centers, n_total, r0, r1, dim, dev, reps=10):
 
 
 def rerank_fidelity(rs, device, modes=((0, "fp16"), (1, "fp8_mode1"), (2, "fp8_mode2"),
-                                         (3, "fp8_mode3"), (5, "fp8_mode5"))):
+                                         (3, "fp8_mode3"))):
     """Ranking fidelity of the cross-encoder kernels at the bench shape (12 layers, 768-d, S_pair =
     128; bge-reranker-v2-m3's 24 layers, 1024-d with --rerank-model bge-reranker-v2-m3) on a
     DISCRIMINATIVE reranker: the relevance-structured weights of super_rag_amd/synthetic.py (the

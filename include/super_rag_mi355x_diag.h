@@ -56,6 +56,15 @@ int sr_diag_gemm_stats(const void* X, int64_t lda, const void* W, const float* b
                        int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, float* stat_out,
                        int device, void* stream);
 
+/* Diagnostic: the fp16 FFN1 of sr_diag_ffn1 with in-kernel s_memtime phase stamps (diag 9: the
+ * product epilogue, 10: its math without the global stores).  stamps: device uint64 [grid x 8
+ * waves x 8] = per wave [tile transitions, cycles of: K-step 0 (tile start -> its barrier),
+ * K-step 1, the rest of the K-loop, the epilogue, the transition wait + barrier, K-steps per
+ * tile, 0] (grid = 8 x min(32, tiles / 8) persistent workgroups). */
+int sr_diag_ffn1_stamps(int diag, const void* X, int64_t lda, const void* W, const float* bias,
+                        const float* colsum, const float* mr, void* Y, int64_t ldy, int M, int N,
+                        int K, uint64_t* stamps, int device, void* stream);
+
 /* Diagnostic: device-to-device copy of `bytes` (multiple of 16) with 16-byte lanes, the HBM
  * yardstick bench.py reports beside the spec peak (no reference counterpart). */
 int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream);

@@ -855,6 +855,23 @@ int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, co
   SR_API_END
 }
 
+int sr_diag_ffn1_stamps(int diag, const void* X, int64_t lda, const void* W, const float* bias,
+                        const float* colsum, const float* mr, void* Y, int64_t ldy, int M, int N,
+                        int K, uint64_t* stamps, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(colsum);
+  SR_NONNULL(mr);
+  SR_NONNULL(Y);
+  SR_NONNULL(stamps);
+  sr::DeviceGuard g(device);
+  sr::launch_ffn1_diag(diag, false, X, lda, W, nullptr, bias, colsum, mr, Y, ldy, M, N, K,
+                       reinterpret_cast<hipStream_t>(stream), stamps);
+  SR_API_END
+}
+
 int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* stream) {
   SR_API_BEGIN
   SR_NONNULL(src);

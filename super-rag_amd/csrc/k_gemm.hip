@@ -75,11 +75,6 @@
                               // 8 stores per wave instead of 16, but the scratch exchange costs
                               // more: 1,551 -> 1,447 TF/s, profiles/r04_ffn1_epilogue/)
 #endif
-#ifndef SR_GEMM_ONE_STORER
-#define SR_GEMM_ONE_STORER 0  // persistent fp16 FFN1: one wave group stores the whole tile (the
-                              // other's rows handed over through the LDS scratch) and the other
-                              // issues all K-loop staging (see gemm_pipe_kernel, OST)
-#endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
@@ -821,17 +816,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 // Same outputs and the same 16 stores per wave either way.
 // DMODE (timing diagnostics, wrong results): 5 = the math (and the scratch exchange) without the
 // global stores, 6 = the stores of the raw accumulators without the math.
-// OST (one storer, fp16 line path only): both wave groups compute their rows and write them to
-// their scratch; the group-1 wave then stores its own 16 x 64 block AND its group-0 partner's
-// (same rows, the previous 128 columns: pscr), between two barriers per row group, so group 0
-// issues no global store at all (its vmcnt holds only the K-loop staging it owns).
-template <int EPI, bool CHECK, bool PERM, class Pre = NoPre, int DMODE = 0, bool OST = false>
+template <int EPI, bool CHECK, bool PERM, class Pre = NoPre, int DMODE = 0>
 __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, int mw0, int lane,
                                                 int M, const float* __restrict__ bias,
                                                 void* __restrict__ Y, int64_t ldy, const LnFold& lf,
                                                 const float2* __restrict__ gtab, half_t* __restrict__ scr,
-                                                const Pre& pre = Pre{}, int grp = 0,
-                                                const half_t* __restrict__ pscr = nullptr) {
+                                                const Pre& pre = Pre{}) {
   constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;
   static_assert(EPI == EPI_LNF_GELU_F16 || OUT8, "store_tile_gelu: LN-folded FFN1 epilogues");
   const int g = lane >> 4, odd = g & 1;
@@ -938,39 +928,6 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
         }
         const int row0 = mw0 + j * 16;
         const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldy * 2 : (int64_t)16 * ldy * 2;
-        if constexpr (OST && DMODE == 0) {
-          // every wave's block is in its scratch; group 1 stores its partner's block, then its own
-          SR_WAITCNT(63, 0);
-          __builtin_amdgcn_s_barrier();
-          if (grp == 1) {
-            const char* const psb = reinterpret_cast<const char*>(pscr);
-            const auto rp = panel_rsrc(reinterpret_cast<const half_t*>(Y) + (int64_t)row0 * ldy + nw0 - 128 + 64 * h, nb);
-            const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(Y) + (int64_t)row0 * ldy + nw0 + 64 * h, nb);
-            half8 o[4];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              o[q] = *reinterpret_cast<const half8*>(psb + rofs + q * 1024);
-              o[2 + q] = *reinterpret_cast<const half8*>(sb + rofs + q * 1024);
-            }
-#if defined(__HIP_DEVICE_COMPILE__)
-            typedef int v4i __attribute__((ext_vector_type(4)));
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o[q]), rp, gofs + q * g8, 0, SR_GEMM_ST_AUX);
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o[2 + q]), ry, gofs + q * g8, 0, SR_GEMM_ST_AUX);
-#else
-            (void)rp;
-            (void)ry;
-            (void)o;
-#endif
-          }
-          // the scratch reads are done before any wave overwrites its scratch (next row group)
-          SR_WAITCNT(63, 0);
-          __builtin_amdgcn_s_barrier();
-          continue;
-        }
         const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(Y) + (int64_t)row0 * ldy + nw0 + 64 * h, nb);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -1154,19 +1111,16 @@ struct PipeEpi {
   // (the fp8-output FFN1 epilogue through its scratch: 8 x 16-B stores, 16 rows x 64 B each)
   static constexpr int NSTORE = (EPI == EPI_LNF_GELU_F8 && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE8 && SR_GEMM_GELU_LUT)
                                     ? 8 : WIDE ? 16 : 32;
-  template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre,
-            bool OST = false>
+  template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
                                              int N, const float* __restrict__ bias,
                                              const void* __restrict__ R, int64_t ldr,
                                              void* __restrict__ Y, int64_t ldy, const LnFold& lf,
                                              half_t* __restrict__ scr = nullptr,
                                              const float2* __restrict__ gtab = nullptr,
-                                             const Pre& pre = Pre{}, int grp = 0,
-                                             const half_t* __restrict__ pscr = nullptr) {
+                                             const Pre& pre = Pre{}) {
     if constexpr (WIDE && GLUT && SR_GEMM_GELU_V2 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
-      store_tile_gelu<EPI, CHECK, PERM, Pre, 0, OST>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre,
-                                                     grp, pscr);
+      store_tile_gelu<EPI, CHECK, PERM, Pre>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre);
     else if constexpr (WIDE)
       store_tile_wide<EPI, CHECK, LINE, GLUT, PERM, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
     else
@@ -1351,7 +1305,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
                         (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
   // GLUT: the FFN1 epilogues' 8 KiB erf table (gelu2_lut) past the stages / line scratch
-  constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || DIAG == 8) &&
+  // STAMP (diagnostic library: sr_diag_ffn1 diag 9 = the product epilogue, 10 = its math without
+  // the stores): per-wave s_memtime phase sums of every tile -- K-step 0, K-step 1, the rest of
+  // the K-loop, the epilogue, the tile transition -- stored once at the end (lf.y8 as uint64 [8]
+  // per wave); the stamps themselves cost a lgkmcnt(0) right behind a barrier
+  constexpr bool STAMP = DIAG == 9 || DIAG == 10;
+  constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
   constexpr int GTAB = SR_GEMM_GELU_V2 ? GELU_NT + 1 : GELU_TAB;  // float2 entries
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
@@ -1367,16 +1326,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
   // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
   constexpr bool LATE = SR_GEMM_LATE_STAGE && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
-  // OST (one storer; persistent fp16 FFN1): fixed roles instead of K-step parity.  Group 0 issues
-  // every in-loop staging burst (K-step kt + 2 in K-step kt) and the next tile's K-step 0; group 1
-  // issues only the next tile's K-step 1 (before the epilogue) and ALL the epilogue's global
-  // stores (store_tile_gelu<OST>: group 0's rows reach it through the LDS scratch).  With parity
-  // roles, the first staging burst after the epilogue (K-step 2, in K-step 0) sat behind its own
-  // wave's 16 stores in the in-order vmcnt, so the end of K-step 1 waited for the stores' write
-  // completion; now group 1's stores drain under the whole next tile (its waits count them) and
-  // group 0 never has a store outstanding.
-  constexpr bool OST = PERSIST && GLINE && !F8 && (DIAG == 8 || (DIAG == 0 && SR_GEMM_ONE_STORER));
-  constexpr int NST1 = OST ? 2 * PipeEpi<EPI>::NSTORE : PipeEpi<EPI>::NSTORE;  // group 1's stores
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -1418,9 +1367,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   half_t* const escr = lds + 2 * STAGE + wave * (GLINE ? 1024 : 2048);
   half_t* const gscr = GLINE ? escr : nullptr;
   (void)gscr;
-  // OST: the group-0 partner's scratch (same X rows wm, the W half wn = 0)
-  half_t* const pscr = OST ? lds + 2 * STAGE + (wave & 3) * 1024 : nullptr;
-  (void)pscr;
   const int nk = K / GBK;
   const int kxs = lf.x_k > 0 ? lf.x_k / GBK : nk;  // K-steps of the X operand (split weights)
   (void)kxs;
@@ -1506,6 +1452,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   }
   __builtin_amdgcn_s_barrier();
   bool stores_pending = false;  // 32 unchecked epilogue stores of the previous tile in flight
+  // STAMP: last stamp and the phase sums, 32-bit (wave-uniform: readfirstlane keeps them in SGPRs)
+  uint32_t st_t0 = 0, st_sum[6] = {0, 0, 0, 0, 0, 0};
+  if constexpr (STAMP) st_t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+  auto stamp = [&](int phase) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memtime();
+      st_sum[phase] = __builtin_amdgcn_readfirstlane(st_sum[phase] + (t1 - st_t0));
+      st_t0 = t1;
+    }
+  };
 
   // One K-step.  SN: 0 none, 1 stage kt+2 of this tile, 2 stage K-steps 0/1 of tile (mn, nn).
   // RN: read kt+1's p0 fragments.  The barrier waits vmcnt(0), or vmcnt(32) when `lenient` (the
@@ -1547,22 +1503,19 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aY[i], bY[j], acc[i][j], 0, 0, 0);
     SR_INTERLEAVE(4);
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
-    if constexpr (OST) {
-      // group 1's outstanding ops are its stores (younger than the K-step-1 pieces it owns at
-      // kt = 0): it waits only for those pieces; group 0 owns every other staging burst
-      if (grp == 1 && stores_pending) {
-        SR_WAITCNT(NST1, 0);
-      } else
-        SR_WAITCNT(0, 0);
-    } else if (lenient) {
+    if (lenient) {
       SR_WAITCNT(PipeEpi<EPI>::NSTORE, 0);
     } else
       SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMP) {
+      if (kt <= 1) stamp(kt);  // phase 0: tile start -> K-step 0's barrier; 1: -> K-step 1's
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // (group (kt & 1) stages K-step kt + 2 in one burst while the partner wave of every SIMD,
-    // from the other group, runs its MFMAs; OST: always group 0)
-    if (SN == 1 && DIAG != 1 && grp == (OST ? 0 : (kt & 1))) stage(kt + 2, cur, m0, n0);
+    // from the other group, runs its MFMAs)
+    if (SN == 1 && DIAG != 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
     if (SN == 2 && !LATE) {
       if (more_) {
         if (grp == 0)
@@ -1703,14 +1656,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 
     // (EPI_SCAN issues a data-dependent number of atomics / stores: never counted as pending)
     const bool full = !SCAN && m0 + BM <= M;
+    stamp(2);  // phase 2: the rest of the K-loop
     if constexpr (DIAG == 7) {  // the FFN1 epilogue with every tile's stores folded onto tile (0, 0)
       store_tile_gelu<EPI, false, PERMW, NoPre, 0>(acc, wn * 128, wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
-    } else if constexpr (DIAG == 5 || DIAG == 6) {  // FFN1 epilogue without its stores / its math
+    } else if constexpr (DIAG == 5 || DIAG == 6 || DIAG == 10) {  // FFN1 epilogue without its stores / its math
       static_assert(GLUT && SR_GEMM_GELU_V2, "DIAG 5 / 6: the FFN1 epilogue");
+      constexpr int DM = DIAG == 10 ? 5 : DIAG;
       if (full)
-        store_tile_gelu<EPI, false, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
+        store_tile_gelu<EPI, false, PERMW, NoPre, DM>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
       else
-        store_tile_gelu<EPI, true, PERMW, NoPre, DIAG>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
+        store_tile_gelu<EPI, true, PERMW, NoPre, DM>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
     } else if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
       const int g = lane >> 4, odd = g & 1;
       const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
@@ -1777,27 +1732,38 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                          R, ldr, Y, ldy, lf, escr, gtab, pre);
     } else if (full) {
-      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW, NoPre, OST>(
-          acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, NoPre{}, grp, pscr);
+      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                        R, ldr, Y, ldy, lf, escr, gtab);
     } else {
-      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW, NoPre, OST>(
-          acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, NoPre{}, grp, pscr);
+      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
+                                                       R, ldr, Y, ldy, lf, escr, gtab);
     }
+    stamp(3);  // phase 3: the epilogue (math, scratch, store issue)
     if (!more) break;
     // next tile: K-step 0 (group 0's 16 glds) landed; younger: the epilogue's NSTORE stores
     // (group 1: its K-step 1 glds too, awaited in K-step 0).  Unchecked tiles: wait for all.
-    // OST: group 0 has no store (it waits for its K-step 0 pieces), group 1 nothing yet
     if (!full)
       SR_WAITCNT(0, 15);
     else if (grp == 0)  // (group 1: its K-step 1 glds too, awaited in K-step 0)
-      SR_WAITCNT(OST ? 0 : PipeEpi<EPI>::NSTORE, 15);
+      SR_WAITCNT(PipeEpi<EPI>::NSTORE, 15);
     else
-      SR_WAITCNT(NST1 + 16, 15);
+      SR_WAITCNT(PipeEpi<EPI>::NSTORE + 16, 15);
     __builtin_amdgcn_s_barrier();
+    stamp(4);  // phase 4: the tile transition (the next tile's K-step 0 wait + barrier)
+    if constexpr (STAMP) st_sum[5] = __builtin_amdgcn_readfirstlane(st_sum[5] + 1);
     stores_pending = full;
     t = t_next;
     m0 = m0n;
     n0 = n0n;
+  }
+  if constexpr (STAMP) {  // [transitions, K-step 0, K-step 1, rest of K-loop, epilogue, transition, 0, 0]
+    if (lane == 0 && lf.y8) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(lf.y8) + ((int64_t)blockIdx.x * 8 + wave) * 8;
+      o[0] = st_sum[5];
+      for (int i = 0; i < 5; ++i) o[1 + i] = (uint64_t)st_sum[i];
+      o[6] = (uint64_t)nk;
+      o[7] = 0;
+    }
   }
 }
 
@@ -2210,15 +2176,18 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
 #if SR_WITH_DIAG
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
-                      int M, int N, int K, hipStream_t stream) {
-  SR_CHECK(diag == 0 || diag == 2 || (diag >= 5 && diag <= 8), "ffn1_diag: diag must be 0, 2, 5, 6, 7 or 8");
+                      int M, int N, int K, hipStream_t stream, uint64_t* stamps) {
+  SR_CHECK(diag == 0 || diag == 2 || (diag >= 5 && diag <= 7) || diag == 9 || diag == 10,
+           "ffn1_diag: diag must be 0, 2, 5, 6, 7, 9 or 10");
   SR_CHECK(N % 256 == 0 && M > 0, "ffn1_diag: N % 256 == 0, M > 0");
   // diag 7 stores every tile unchecked onto rows 0..255 of Y
   SR_CHECK(diag != 7 || (M >= 256 && ldy >= N), "ffn1_diag: diag 7 needs M >= 256, ldy >= N");
+  SR_CHECK((diag != 9 && diag != 10) || (stamps && !f8), "ffn1_diag: diag 9 / 10 need a stamp buffer (fp16)");
   LnFold lf;
   lf.mr = mr;
   lf.colsum = colsum;
   lf.wexp = wexp;
+  lf.y8 = reinterpret_cast<uint8_t*>(stamps);  // (STAMP diagnostics only; FFN1 has no e4m3 copy)
   if (diag == 0) {
     if (f8)
       launch_gemm_f8w(EPI_LNF_GELU_F8, reinterpret_cast<const uint8_t*>(X), lda,
@@ -2264,12 +2233,10 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
       SR_FD(5)
     } else if (diag == 6) {
       SR_FD(6)
-    } else if (diag == 8) {  // the product epilogue with the one-storer roles (OST; fp16 only)
-      if (f8) {
-        SR_FD(0)
-      } else {
-        SR_FD(8)
-      }
+    } else if (diag == 9) {
+      SR_FD(9)
+    } else if (diag == 10) {
+      SR_FD(10)
     } else {
       SR_FD(7)
     }

@@ -79,7 +79,7 @@ void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 // Diagnostic FFN1 launches (sr_diag_ffn1): diag 0 product, 2 no epilogue, 5 math only, 6 stores only.
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
-                      int M, int N, int K, hipStream_t stream);
+                      int M, int N, int K, hipStream_t stream, uint64_t* stamps = nullptr);
 #endif
 void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8, const float* bias,
                      const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,

@@ -153,6 +153,9 @@ DIAG_SIGNATURES = {
     "sr_diag_attention": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_void_p]),
     "sr_diag_copy": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "sr_diag_ffn1_stamps": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int,
+                                    c_void_p]),
     "sr_diag_gemm_stats": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                    c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int,
                                    c_void_p]),

@@ -314,11 +314,11 @@ class Encoder:
 
     def set_fp8(self, mode: int) -> None:
         """Opt-in fp8 precision mode (LN-folded fp16-residual encoders, e.g. cross-encoders):
-        1 = FFN (e4m3 FFN activations, FFN2 on the block-scaled fp8 MFMA), 2 = also FFN1 and QKV
-        of layers >= 1 on e4m3 copies of the residual sums, 3 = FFN1 and FFN2 as in 2 with QKV +
-        attention in fp16 (fused), 5 = 3 plus the O-projection of the fused layers on the fp8 MFMA
-        (K5c writes the attention output as e4m3), 0 = fp16 (sr_encoder_set_fp8).  (Mode 4, QKV
-        in fp8 on normalised rows, was measured and rejected: the diagnostic library only.)"""
+        1 = FFN2 on the block-scaled fp8 MFMA (e4m3 FFN activations), 2 = also FFN1 and the QKV
+        of layers >= 1 on e4m3 copies of the residual sums (faster, ranks worse), 3 = FFN1 and
+        FFN2 as in 2 with QKV + attention in fp16 (fused), 0 = fp16 (sr_encoder_set_fp8).  Modes
+        4 (QKV on normalised e4m3 rows) and 5 (mode 3 + the O-projection on e4m3 attention
+        outputs) failed the ranking fidelity gates: diagnostic library only."""
         N.call("sr_encoder_set_fp8", self._h, int(mode))
 
     def set_fp8_ffn(self, on: bool = True) -> None:

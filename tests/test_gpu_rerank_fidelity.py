@@ -93,7 +93,7 @@ def test_oracle_on_the_gpu_reproduces_the_fixture(fidelity):
     assert np.abs(g[:, 0].reshape(-1, 100) - ref[:2]).max() <= 1e-4
 
 
-@pytest.mark.parametrize("mode", [3, 5])
+@pytest.mark.parametrize("mode", [3])
 def test_fp8_mode3_ranks_like_the_oracle(fidelity, mode):
     """Config 5's fp8 reranker path (mode 3: FFN1 + FFN2 on the block-scaled fp8 MFMA, QKV +
     attention fp16; mode 5: also the O-projection of the K5c layers on e4m3 ctx) gated as the fp16
@@ -159,10 +159,10 @@ def test_pipeline_rerank_path_ranks_like_the_oracle(fidelity):
         assert np.abs(logits[b] - ref[b][got_j]).max() * RATIO_MIN <= std[b], b
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 5])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_fp8_modes_top10_agreement(fidelity, mode):
-    """The opt-in fp8 precision modes (1: FFN2 on e4m3; 2: also FFN1 and QKV; 3: FFN1 + FFN2, QKV
-    fp16; 5: 3 + the O-projection on e4m3 ctx) against the fp32
+    """The product fp8 precision modes (1: FFN2 on e4m3; 2: also FFN1 and QKV; 3: FFN1 + FFN2, QKV
+    fp16) against the fp32
     oracle on the same discriminative set: agreement is reported; the floor only catches a broken
     mode (seeded-random weights could not tell these apart at all: 0.55 overlap vs fp16)."""
     enc, ids, mask, ref, _, _ = fidelity

@@ -7,8 +7,7 @@ fp32 oracle's logits committed in tests/golden/rerank_fidelity_v2m3.npz
 (tests/golden/gen_rerank_fidelity.py --model bge-reranker-v2-m3):
   fp16          top-10 identical to the oracle's modulo ties within 1 % of the logit std, and per
                 query logit std >= RATIO_MIN x max |logit error|;
-  fp8 mode 3    the same gate at RATIO_MIN_FP8 (FFN1 + FFN2 on the block-scaled fp8 MFMA);
-  fp8 mode 5    the same gate as mode 3 (mode 3 + the O-projection on e4m3 attention outputs).
+  fp8 mode 3    the same gate at RATIO_MIN_FP8 (FFN1 + FFN2 on the block-scaled fp8 MFMA).
 Twice bge-reranker-base's depth accumulates ~sqrt 2 its rounding error: fp16 measured std / err
 >= 83.6 here (bge-reranker-base: >= 120), so the floors are the base model's gates (fp16 100,
 fp8 mode 3 50) scaled by 1 / sqrt 2: 70 and 35.
@@ -55,7 +54,7 @@ def _gate(lg, ref, ratio, label):
     assert (std >= ratio * err).all(), (std / err)
 
 
-@pytest.mark.parametrize("mode", [0, 3, 5])
+@pytest.mark.parametrize("mode", [0, 3])
 def test_v2m3_reranker_ranks_like_the_oracle(fidelity_v2m3, mode):
     enc, ids, mask, ref = fidelity_v2m3
     enc.set_fp8(mode)

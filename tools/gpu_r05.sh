@@ -13,7 +13,7 @@ for P in ${PARTS//,/ }; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=15 > gpurun_out/$TAG/gpu_tests.log 2>&1 || exit 1 ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$TAG/smoke.log 2>&1 || exit 1 ;;
     bench) timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$TAG/bench_20x5.log 2>&1 || exit 1 ;;
-    modes) for M in 3 5; do
+    modes) for M in 3; do
              timeout -k 10 300 python -u bench.py --fp8 $M --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/$TAG/bench_fp8m$M.log 2>&1 || exit 1
              timeout -k 10 400 python -u bench.py --workload config5 --fp8 $M --steps 10 --warmup 3 --no-extras > gpurun_out/$TAG/bench_c5_fp8m$M.log 2>&1 || exit 1
            done ;;
@@ -25,6 +25,8 @@ for P in ${PARTS//,/ }; do
           find gpurun_out/prof_$TAG -name "*.csv" -size +1M -delete ;;
     ffn1) timeout -k 10 300 python -u tools/ffn1_bench.py --diags ${FFN1_DIAGS:-0,8,2} --rounds 3 > gpurun_out/$TAG/ffn1.log 2>&1 || exit 1
           timeout -k 10 300 python -u tools/ffn1_bench.py --M 1638400 --diags ${FFN1_DIAGS:-0,8,2} --rounds 3 > gpurun_out/$TAG/ffn1_1638k.log 2>&1 || exit 1 ;;
+    stamps) timeout -k 10 300 python -u tools/ffn1_stamps.py > gpurun_out/$TAG/ffn1_stamps.log 2>&1 || exit 1 ;;
+    v5) SUPER_RAG_AMD_LIB=$PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so timeout -k 10 400 python -u bench.py --workload config5 --fp8 5 --steps 10 --warmup 3 --no-extras > gpurun_out/$TAG/bench_c5_fp8m5_diaglib.log 2>&1 || exit 1 ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
