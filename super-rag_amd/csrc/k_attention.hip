@@ -813,7 +813,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const float* __restrict__ colsum, const float* __restrict__ mr,
     const int32_t* __restrict__ mask, half_t* __restrict__ ctx, int M, int d, int heads,
-    float scale_log2) {
+    float scale_log2, int hg) {
   constexpr int DH = 64;
   constexpr int IMG = 3 * QA_BM * DH;  // Q, K, V images (96 KiB)
   // LDS: the images, then one K-step buffer (PB) past them; odd K-steps use PA = the first 56 KiB
@@ -835,7 +835,13 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     t = lo + (blockIdx.x >> 3);
     if (t >= t_end || t_step <= 0) return;
   }
-  int h = t % heads, m0 = (t / heads) * QA_BM;
+  // tile t -> (head group, panel, head in the group), head fastest: the heads are walked in groups
+  // of hg (hg = heads: every head of a panel in turn), so an XCD's ~32 concurrent tiles need the W
+  // slices of hg heads and ~32 / hg X panels at a time
+  const int pg = panels * hg;
+  auto tile_h = [&](int tt) __attribute__((always_inline)) { return (tt / pg) * hg + (tt % pg) % hg; };
+  auto tile_m = [&](int tt) __attribute__((always_inline)) { return ((tt % pg) / hg) * QA_BM; };
+  int h = tile_h(t), m0 = tile_m(t);
   const int K = d, nk = K / 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1004,7 +1010,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     __syncthreads();
     const int t_next = t + t_step;
     const bool more = t_next < t_end;
-    const int h_n = t_next % heads, m0_n = (t_next / heads) * QA_BM;
+    const int h_n = tile_h(t_next), m0_n = tile_m(t_next);
     if (more && grp == 0) stage(0, PB, m0_n, h_n);  // the next tile's K-step 0 lands during attention
 
     // ---- attention: waves 4s .. 4s+3 own sequence s of the panel, 32 queries each ----
@@ -1221,6 +1227,14 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   SR_CHECK(tiles < (1ll << 31), "qkv_attention: too many tiles");
   // persistent: 8 XCD groups x G walkers, one 8-wave workgroup per CU (153 KiB of LDS)
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+  // head groups of the tile walk (hg | heads): hg = heads walks every head of a panel in turn
+  int hg = heads;
+#if SR_WITH_DIAG
+  if (const char* e = diag_getenv("SR_QA_HGROUP")) {
+    const int v = std::atoi(e);
+    if (v > 0 && heads % v == 0) hg = v;
+  }
+#endif
 #if SR_WITH_DIAG
   static const int diag = [] {
     const char* e = diag_getenv("SR_QA_DIAG");
@@ -1228,26 +1242,26 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   }();
   if (epi == EPI_LNF_F16 && diag == 1)
     hipLaunchKernelGGL((qkv_attn_kernel<true, 1>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
-                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
   else if (epi == EPI_LNF_F16 && diag == 2)
     hipLaunchKernelGGL((qkv_attn_kernel<true, 2>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
-                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
   else
 #endif
   if (ctx8) {  // fp8 mode 5: e4m3 ctx for the O-projection on the block-scaled fp8 MFMA
     half_t* c8 = reinterpret_cast<half_t*>(ctx8);
     if (epi == EPI_LNF_F16)
       hipLaunchKernelGGL((qkv_attn_kernel<true, 0, true>), grid, block, 0, stream, X, lda, W, bias,
-                         lf->colsum, lf->mr, mask, c8, (int)M, d, heads, scale_log2);
+                         lf->colsum, lf->mr, mask, c8, (int)M, d, heads, scale_log2, hg);
     else
       hipLaunchKernelGGL((qkv_attn_kernel<false, 0, true>), grid, block, 0, stream, X, lda, W, bias,
-                         nullptr, nullptr, mask, c8, (int)M, d, heads, scale_log2);
+                         nullptr, nullptr, mask, c8, (int)M, d, heads, scale_log2, hg);
   } else if (epi == EPI_LNF_F16)
     hipLaunchKernelGGL(qkv_attn_kernel<true>, grid, block, 0, stream, X, lda, W, bias, lf->colsum,
-                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2);
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
   else
     hipLaunchKernelGGL(qkv_attn_kernel<false>, grid, block, 0, stream, X, lda, W, bias, nullptr,
-                       nullptr, mask, ctx, (int)M, d, heads, scale_log2);
+                       nullptr, mask, ctx, (int)M, d, heads, scale_log2, hg);
   SR_LAUNCH_CHECK();
 }
 

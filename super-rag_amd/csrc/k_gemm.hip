@@ -75,6 +75,14 @@
                               // 8 stores per wave instead of 16, but the scratch exchange costs
                               // more: 1,551 -> 1,447 TF/s, profiles/r04_ffn1_epilogue/)
 #endif
+#ifndef SR_GEMM_RES_PREFETCH
+#define SR_GEMM_RES_PREFETCH 1  // residual epilogues: row group j + 1's residual loaded before row
+                                // group j's stores (store_tile_wide, RPF)
+#endif
+#ifndef SR_GEMM_GELU_CSTL
+#define SR_GEMM_GELU_CSTL 1  // FFN1 epilogues: bias / colsum / row statistics from LDS (staged by
+                             // LDS-DMA during the K-loop), no global load inside the epilogue
+#endif
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
@@ -461,6 +469,31 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   // (recomputed per row group from a fresh lane id: hoisted over the whole epilogue, the four
   // offsets spilled the residual epilogues at 256 VGPRs)
   constexpr bool BUFST = LINE && SR_GEMM_WIDE_BUFST;
+  // RPF: row group j + 1's residual rows are loaded BEFORE row group j's line stores are issued.
+  // vmcnt is in order: loaded after them (as before), the wait for the next residual also waited
+  // for the previous row group's stores to complete -- four write-completion round trips per
+  // tile with every CU storing at once (the ISA showed vmcnt(0) after each row group's loads).
+  constexpr bool RPF = (RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD && SR_GEMM_RES_PREFETCH;
+  half8 rA[RPF ? 4 : 1], rB[RPF ? 4 : 1];
+  auto load_res = [&](half8 (&r)[RPF ? 4 : 1], int j) __attribute__((always_inline)) {
+    if constexpr (RPF) {
+      const int ln0 = lane_id_here(), l16 = ln0 & 15, l4 = ln0 >> 4;
+      const uint32_t bo = (uint32_t)((l16 * (int)ldr + 16 * (l4 & 1) + 4 * (l4 & 2)) * 2);
+      const int row0 = mw0 + j * 16;
+      const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
+      const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        r[p] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rr, bo + 64 * p, 0, 0));
+#else
+        (void)rr;
+        (void)bo;
+#endif
+      }
+    }
+  };
+  if constexpr (RPF) load_res(rA, 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     uint32_t bo_res = 0, bo_wr = 0, bo_rd = 0, bo_st = 0;
@@ -478,7 +511,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     if (!LINE && CHECK && m_row >= M) continue;
     const int m = (LINE && CHECK && m_row >= M) ? M - 1 : m_row;
     half8 r16[(RESN || LNR) ? 4 : 1];
-    if constexpr ((RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD) {
+    if constexpr (RPF) {
+      half8 (&rc)[4] = (j & 1) ? rB : rA;
+      if (j < 3) load_res((j & 1) ? rA : rB, j + 1);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) r16[p] = rc[p];
+    } else if constexpr ((RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD) {
       const int row0 = mw0 + j * 16;
       const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
       const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);
@@ -816,28 +854,46 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 // Same outputs and the same 16 stores per wave either way.
 // DMODE (timing diagnostics, wrong results): 5 = the math (and the scratch exchange) without the
 // global stores, 6 = the stores of the raw accumulators without the math.
-template <int EPI, bool CHECK, bool PERM, class Pre = NoPre, int DMODE = 0>
+// CST: the tile's bias / column sums / row statistics come from the LDS table the K-loop staged
+// (cst: [256 bias][256 colsum][256 x (mu, rstd)] of the tile; ln0 / lm0 = the wave's column / row
+// offset in the tile) instead of global loads: no vmcnt wait inside the epilogue, so its line
+// stores drain while the next row groups compute.
+template <int EPI, bool CHECK, bool PERM, class Pre = NoPre, int DMODE = 0, bool CST = false>
 __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, int mw0, int lane,
                                                 int M, const float* __restrict__ bias,
                                                 void* __restrict__ Y, int64_t ldy, const LnFold& lf,
                                                 const float2* __restrict__ gtab, half_t* __restrict__ scr,
-                                                const Pre& pre = Pre{}) {
+                                                const Pre& pre = Pre{}, const float* __restrict__ cst = nullptr,
+                                                int ln0 = 0, int lm0 = 0) {
   constexpr bool OUT8 = EPI == EPI_LNF_GELU_F8;
   static_assert(EPI == EPI_LNF_GELU_F16 || OUT8, "store_tile_gelu: LN-folded FFN1 epilogues");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
+  const int clane = ln0 + 16 * odd + 4 * (g & 2);  // CST: the same column in the tile's table
+  (void)clane;
   float2 mrj[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    int m = mw0 + j * 16 + (lane & 15);
-    m = (CHECK && m >= M) ? M - 1 : m;
-    mrj[j] = *reinterpret_cast<const float2*>(lf.mr + (int64_t)m * lf.stat_ld * 2);
+    if constexpr (CST) {
+      mrj[j] = *reinterpret_cast<const float2*>(cst + 512 + 2 * (lm0 + j * 16 + (lane & 15)));
+    } else {
+      int m = mw0 + j * 16 + (lane & 15);
+      m = (CHECK && m >= M) ? M - 1 : m;
+      mrj[j] = *reinterpret_cast<const float2*>(lf.mr + (int64_t)m * lf.stat_ld * 2);
+    }
   }
   auto load_consts = [&](float4v (&d)[4], int p) __attribute__((always_inline)) {
-    d[0] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p);
-    d[1] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p + 4);
-    d[2] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p);
-    d[3] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p + 4);
+    if constexpr (CST) {
+      d[0] = *reinterpret_cast<const float4v*>(cst + clane + 32 * p);
+      d[1] = *reinterpret_cast<const float4v*>(cst + clane + 32 * p + 4);
+      d[2] = *reinterpret_cast<const float4v*>(cst + 256 + clane + 32 * p);
+      d[3] = *reinterpret_cast<const float4v*>(cst + 256 + clane + 32 * p + 4);
+    } else {
+      d[0] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p);
+      d[1] = *reinterpret_cast<const float4v*>(bias + nlane + 32 * p + 4);
+      d[2] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p);
+      d[3] = *reinterpret_cast<const float4v*>(lf.colsum + nlane + 32 * p + 4);
+    }
   };
   // the 8 outputs of (column group p, row group j): columns nlane + 32 p + 0..7 of row j
   auto gelu8 = [&](float (&v)[8], int p, int j, const float4v (&cst)[4]) __attribute__((always_inline)) {
@@ -1111,16 +1167,19 @@ struct PipeEpi {
   // (the fp8-output FFN1 epilogue through its scratch: 8 x 16-B stores, 16 rows x 64 B each)
   static constexpr int NSTORE = (EPI == EPI_LNF_GELU_F8 && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE8 && SR_GEMM_GELU_LUT)
                                     ? 8 : WIDE ? 16 : 32;
-  template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre>
+  template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre,
+            bool CST = false>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
                                              int N, const float* __restrict__ bias,
                                              const void* __restrict__ R, int64_t ldr,
                                              void* __restrict__ Y, int64_t ldy, const LnFold& lf,
                                              half_t* __restrict__ scr = nullptr,
                                              const float2* __restrict__ gtab = nullptr,
-                                             const Pre& pre = Pre{}) {
+                                             const Pre& pre = Pre{}, const float* __restrict__ cst = nullptr,
+                                             int ln0 = 0, int lm0 = 0) {
     if constexpr (WIDE && GLUT && SR_GEMM_GELU_V2 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
-      store_tile_gelu<EPI, CHECK, PERM, Pre>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre);
+      store_tile_gelu<EPI, CHECK, PERM, Pre, 0, CST>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre,
+                                                     cst, ln0, lm0);
     else if constexpr (WIDE)
       store_tile_wide<EPI, CHECK, LINE, GLUT, PERM, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
     else
@@ -1320,9 +1379,21 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 &&
                          ((SR_GEMM_GELU_LINE && EPI == EPI_LNF_GELU_F16) ||
                           (SR_GEMM_GELU_LINE8 && EPI == EPI_LNF_GELU_F8));
+  // CSTL: the FFN1 epilogue's per-tile constants -- bias and column sums of the tile's 256 columns,
+  // (mu, rstd) of its 256 rows: 4 KiB -- reach LDS by LDS-DMA during the tile's K-loop (group 1,
+  // with its K-step 3 burst) instead of as global loads inside the epilogue: vmcnt is in order, so
+  // the epilogue's constant loads made it wait for the next tile's in-flight K-step 0 / 1 pieces,
+  // and the second half's for the first half's 8 line STORES (write completion, the whole chip
+  // storing at once) -- measured in-kernel as an epilogue of 11.2k cycles with stores vs 4.4k
+  // without (profiles/r05c/ffn1_stamps.log)
+  constexpr bool CSTL = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_CSTL;
   __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
-                                                     (SCAN ? 512 : 0) + (GLUT ? 4 * GTAB : 0)];
-  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0));
+                                                     (CSTL ? 2048 : 0) + (SCAN ? 512 : 0) +
+                                                     (GLUT ? 4 * GTAB : 0)];
+  float* const cst = reinterpret_cast<float*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0));
+  (void)cst;
+  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
+                                                 (CSTL ? 2048 : 0));
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
   // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
   constexpr bool LATE = SR_GEMM_LATE_STAGE && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
@@ -1421,6 +1492,33 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #endif
   };
 
+  // CSTL: group 1's 4 waves stage the tile's epilogue constants, one 1 KiB piece each: bias and
+  // column sums of columns [nn, nn + 256), (mu, rstd) of rows [mm, mm + 256) (two pieces; rows past
+  // M read as zero and are never stored).  Issued at the top of every tile (the previous tile's
+  // epilogue, the last reader, ended before the transition barrier), younger than group 1's
+  // K-step 1 pieces and epilogue stores: K-step 0's lenient wait counts the 4 pieces too, the end
+  // of K-step 1 (vmcnt(0)) awaits them, the epilogue reads them 10+ K-steps later (persistent FFN1
+  // launches keep nk >= 4, host-checked).  (Issued from inside the K-step loop under a runtime kt
+  // test, the staging code spilled 12-96 B at 256 VGPRs.)
+  auto stage_cst = [&](int mm, int nn) __attribute__((always_inline)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // (the lane offset re-derived here: a hoisted one stayed live through the K-loop and spilled)
+    const uint32_t lo = (uint32_t)lane_id_here() * 16u;
+    if (w4 < 2) {
+      const float* src = w4 == 0 ? bias : lf.colsum;
+      const auto r = panel_rsrc(reinterpret_cast<const half_t*>(src + nn), 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(cst + 256 * w4), 16, lo, 0, 0, 0);
+    } else {
+      const int r0 = mm + 128 * (w4 - 2);
+      // (wave-uniform, kept scalar: a VALU clamp put the descriptor in VGPRs, spilled at 256 VGPRs
+      // and its reload's vmcnt(0) waited for the epilogue's stores at every tile's top)
+      const int nrow = __builtin_amdgcn_readfirstlane(max(0, min(128, M - r0)));
+      const auto r = panel_rsrc(reinterpret_cast<const half_t*>(lf.mr + (int64_t)r0 * 2), (int64_t)nrow * 8);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(cst + 512 + 256 * (w4 - 2)), 16, lo, 0, 0, 0);
+    }
+#endif
+  };
+
   float4v acc[8][4];
   half8 aX[4], aY[4], bX[4], bY[4];
   int8v f0[2], f1[2], fb[4];  // fp8 path: A row pairs (ping-pong) and B
@@ -1504,7 +1602,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     SR_INTERLEAVE(4);
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
     if (lenient) {
-      SR_WAITCNT(PipeEpi<EPI>::NSTORE, 0);
+      if (CSTL && grp == 1)  // (+ the 4 constant pieces issued at the tile's top)
+        SR_WAITCNT(PipeEpi<EPI>::NSTORE + 4, 0);
+      else
+        SR_WAITCNT(PipeEpi<EPI>::NSTORE, 0);
     } else
       SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
@@ -1610,6 +1711,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   };
 
   for (;;) {
+    if (CSTL && grp == 1) stage_cst(m0, n0);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1658,14 +1760,17 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     const bool full = !SCAN && m0 + BM <= M;
     stamp(2);  // phase 2: the rest of the K-loop
     if constexpr (DIAG == 7) {  // the FFN1 epilogue with every tile's stores folded onto tile (0, 0)
-      store_tile_gelu<EPI, false, PERMW, NoPre, 0>(acc, wn * 128, wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
+      store_tile_gelu<EPI, false, PERMW, NoPre, 0, CSTL>(acc, wn * 128, wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr,
+                                                        NoPre{}, cst, wn * 128, wm * 64);
     } else if constexpr (DIAG == 5 || DIAG == 6 || DIAG == 10) {  // FFN1 epilogue without its stores / its math
       static_assert(GLUT && SR_GEMM_GELU_V2, "DIAG 5 / 6: the FFN1 epilogue");
       constexpr int DM = DIAG == 10 ? 5 : DIAG;
       if (full)
-        store_tile_gelu<EPI, false, PERMW, NoPre, DM>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
+        store_tile_gelu<EPI, false, PERMW, NoPre, DM, CSTL>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf,
+                                                            gtab, gscr, NoPre{}, cst, wn * 128, wm * 64);
       else
-        store_tile_gelu<EPI, true, PERMW, NoPre, DM>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr);
+        store_tile_gelu<EPI, true, PERMW, NoPre, DM, CSTL>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf,
+                                                           gtab, gscr, NoPre{}, cst, wn * 128, wm * 64);
     } else if constexpr (DIAG == 4) {  // stores only: acc -> fp16, wide layout, no bias / activation
       const int g = lane >> 4, odd = g & 1;
       const int nl = n0 + wn * 128 + 16 * odd + 4 * (g & 2);
@@ -1732,11 +1837,13 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
                                                          R, ldr, Y, ldy, lf, escr, gtab, pre);
     } else if (full) {
-      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                        R, ldr, Y, ldy, lf, escr, gtab);
+      PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW, NoPre, CSTL>(
+          acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, NoPre{}, cst, wn * 128,
+          wm * 64);
     } else {
-      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                       R, ldr, Y, ldy, lf, escr, gtab);
+      PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW, NoPre, CSTL>(
+          acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, NoPre{}, cst, wn * 128,
+          wm * 64);
     }
     stamp(3);  // phase 3: the epilogue (math, scratch, store issue)
     if (!more) break;
@@ -2134,6 +2241,7 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
   SR_CHECK(lf && lf->wexp, "gemm_f8w: the weight rows' exponents (LnFold.wexp)");
   SR_CHECK((stats && !lnr) || lf->mr, "gemm_f8w: LN-folded operand needs its row statistics");
   SR_CHECK(stats || lf->colsum, "gemm_f8w: LNF needs colsum");
+  SR_CHECK(epi != EPI_LNF_GELU_F8 || lf->stat_ld == 1, "gemm_f8w: FFN1 reads consecutive row statistics");
   SR_CHECK(!lnr || lf->gamma, "gemm_f8w: LNR needs the LayerNorm weight");
   SR_CHECK(!stats || lf->stat_out, "gemm_f8w: stat_out");
   SR_CHECK(!y8 || lf->y8, "gemm_f8w: the e4m3-copy epilogues need LnFold.y8");
@@ -2146,7 +2254,8 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
                  (double)M * K + (double)N * K + (out_b + res_b + (y8 ? 1.0 : 0.0)) * (double)M * N);
   const LnFold lfv = *lf;
   const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
-  const bool persist = tiles >= 512;
+  // (the FFN1 epilogue's constants are staged during K-step 1 of a persistent tile: nk >= 4)
+  const bool persist = tiles >= 512 && (epi != EPI_LNF_GELU_F8 || K / 2 >= 4 * 64);
   const dim3 grid(persist ? (unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8))) : (unsigned)tiles);
   // operands as 2-byte units: K / 2, lda / 2 (the staging moves bytes)
   const half_t* x = reinterpret_cast<const half_t*>(X8);
@@ -2198,6 +2307,7 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
     return;
   }
   SR_CHECK(!f8 || (wexp && K % 128 == 0), "ffn1_diag: fp8 needs wexp, K % 128 == 0");
+  SR_CHECK((f8 ? K / 2 : K) >= 4 * 64, "ffn1_diag: the persistent FFN1 needs >= 4 K-steps");
   const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
   // SR_FFN1_DIAG_WALKERS = walkers per XCD (1..32; default 32 = every CU): with fewer CUs storing
   // at once, a store cost that is the chip's write bandwidth shrinks, a per-CU one does not
@@ -2339,6 +2449,8 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
            "gemm: LN-folded operand needs its row statistics");
   SR_CHECK(!(epi == EPI_LNF_F16 || epi == EPI_LNF_GELU_F16 || epi == EPI_LNF_GELU_F8) || lf->colsum,
            "gemm: LNF needs colsum");
+  SR_CHECK(!(epi == EPI_LNF_GELU_F16 || epi == EPI_LNF_GELU_F8) || lf->stat_ld == 1,
+           "gemm: the FFN1 epilogues read consecutive row statistics (stat_ld 1)");
   SR_CHECK(!(epi == EPI_LNR16_STATS || epi == EPI_LNR16_STATS_Y8) || lf->gamma,
            "gemm: LNR needs the LayerNorm weight");
   SR_CHECK(!(epi == EPI_RES16_STATS || epi == EPI_LNR16_STATS || epi == EPI_RES16_STATS_Y8 ||
@@ -2453,7 +2565,9 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
     }
 #undef SR_PP_CASE
   } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
-    const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK;
+    // (the FFN1 epilogues stage their constants during K-step 1 of a persistent tile: nk >= 4)
+    const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK &&
+                         ((epi != EPI_LNF_GELU_F16 && epi != EPI_LNF_GELU_F8) || K >= 4 * GBK);
     // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)
     const int64_t g = persist ? 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8)) : big_tiles;
     SR_CHECK(!persist || (g % 8 == 0 && g >= 8), "gemm: persistent grid must be a multiple of 8");
