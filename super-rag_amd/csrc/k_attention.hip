@@ -1248,7 +1248,8 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
                        lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
   else
 #endif
-  if (ctx8) {  // fp8 mode 5: e4m3 ctx for the O-projection on the block-scaled fp8 MFMA
+#if SR_WITH_DIAG
+  if (ctx8) {  // fp8 mode 5 (diagnostic library): e4m3 ctx for the O-projection on the fp8 MFMA
     half_t* c8 = reinterpret_cast<half_t*>(ctx8);
     if (epi == EPI_LNF_F16)
       hipLaunchKernelGGL((qkv_attn_kernel<true, 0, true>), grid, block, 0, stream, X, lda, W, bias,
@@ -1256,7 +1257,11 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
     else
       hipLaunchKernelGGL((qkv_attn_kernel<false, 0, true>), grid, block, 0, stream, X, lda, W, bias,
                          nullptr, nullptr, mask, c8, (int)M, d, heads, scale_log2, hg);
-  } else if (epi == EPI_LNF_F16)
+  } else
+#else
+  SR_CHECK(!ctx8, "qkv_attention: the e4m3 ctx output (fp8 mode 5) is in the diagnostic library only");
+#endif
+  if (epi == EPI_LNF_F16)
     hipLaunchKernelGGL(qkv_attn_kernel<true>, grid, block, 0, stream, X, lda, W, bias, lf->colsum,
                        lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
   else

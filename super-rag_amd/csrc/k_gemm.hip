@@ -75,10 +75,6 @@
                               // 8 stores per wave instead of 16, but the scratch exchange costs
                               // more: 1,551 -> 1,447 TF/s, profiles/r04_ffn1_epilogue/)
 #endif
-#ifndef SR_GEMM_RES_PREFETCH
-#define SR_GEMM_RES_PREFETCH 1  // residual epilogues: row group j + 1's residual loaded before row
-                                // group j's stores (store_tile_wide, RPF)
-#endif
 #ifndef SR_GEMM_GELU_CSTL
 #define SR_GEMM_GELU_CSTL 1  // FFN1 epilogues: bias / colsum / row statistics from LDS (staged by
                              // LDS-DMA during the K-loop), no global load inside the epilogue
@@ -469,31 +465,6 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   // (recomputed per row group from a fresh lane id: hoisted over the whole epilogue, the four
   // offsets spilled the residual epilogues at 256 VGPRs)
   constexpr bool BUFST = LINE && SR_GEMM_WIDE_BUFST;
-  // RPF: row group j + 1's residual rows are loaded BEFORE row group j's line stores are issued.
-  // vmcnt is in order: loaded after them (as before), the wait for the next residual also waited
-  // for the previous row group's stores to complete -- four write-completion round trips per
-  // tile with every CU storing at once (the ISA showed vmcnt(0) after each row group's loads).
-  constexpr bool RPF = (RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD && SR_GEMM_RES_PREFETCH;
-  half8 rA[RPF ? 4 : 1], rB[RPF ? 4 : 1];
-  auto load_res = [&](half8 (&r)[RPF ? 4 : 1], int j) __attribute__((always_inline)) {
-    if constexpr (RPF) {
-      const int ln0 = lane_id_here(), l16 = ln0 & 15, l4 = ln0 >> 4;
-      const uint32_t bo = (uint32_t)((l16 * (int)ldr + 16 * (l4 & 1) + 4 * (l4 & 2)) * 2);
-      const int row0 = mw0 + j * 16;
-      const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
-      const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-        r[p] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rr, bo + 64 * p, 0, 0));
-#else
-        (void)rr;
-        (void)bo;
-#endif
-      }
-    }
-  };
-  if constexpr (RPF) load_res(rA, 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     uint32_t bo_res = 0, bo_wr = 0, bo_rd = 0, bo_st = 0;
@@ -511,12 +482,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     if (!LINE && CHECK && m_row >= M) continue;
     const int m = (LINE && CHECK && m_row >= M) ? M - 1 : m_row;
     half8 r16[(RESN || LNR) ? 4 : 1];
-    if constexpr (RPF) {
-      half8 (&rc)[4] = (j & 1) ? rB : rA;
-      if (j < 3) load_res((j & 1) ? rA : rB, j + 1);
-#pragma unroll
-      for (int p = 0; p < 4; ++p) r16[p] = rc[p];
-    } else if constexpr ((RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD) {
+    if constexpr ((RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD) {
       const int row0 = mw0 + j * 16;
       const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
       const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);

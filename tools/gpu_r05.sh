@@ -4,6 +4,7 @@
 #   tests  the whole -m gpu suite
 #   smoke  __graft_entry__.smoke()
 #   bench  the driver's default bench (20 / 5)
+#   dropin tools/gpu_dropin_mp.sh ($DROPIN_PROCS x $DROPIN_C) + its pooled summary
 #   prof   tools/profile_round.sh (rocprofv3 trace + PMC, config 4 and config 5's fp8 path)
 TAG=${1:?tag}; PARTS=${2:-tests,smoke,bench}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG
@@ -29,6 +30,8 @@ for P in ${PARTS//,/ }; do
     v5) SUPER_RAG_AMD_LIB=$PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so timeout -k 10 400 python -u bench.py --workload config5 --fp8 5 --steps 10 --warmup 3 --no-extras > gpurun_out/$TAG/bench_c5_fp8m5_diaglib.log 2>&1 || exit 1 ;;
     ab) L=super-rag_amd/super_rag_amd/lib_ab
         timeout -k 10 900 bash tools/ab_bench.sh $TAG ${AB_LIBS:-$L/libsrmi_base.so $L/libsrmi_cstl.so $L/libsrmi_rpf.so} > gpurun_out/$TAG/ab.log 2>&1 || exit 1 ;;
+    dropin) rm -rf gpurun_out/dropin_mp && timeout -k 10 1000 bash tools/gpu_dropin_mp.sh || exit 1
+            python3 tools/dropin_mp_summary.py gpurun_out/dropin_mp > gpurun_out/$TAG/dropin_mp.txt 2>&1 || exit 1 ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
