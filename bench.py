@@ -75,8 +75,11 @@ def parse():
                     help="drop_in field: chunks in the connector collection it searches")
     ap.add_argument("--dropin-procs", type=int, default=4,
                     help="drop_in field: also run this many serving processes on the GPU together "
-                         "(C = 64 callers each; started before this process touches the GPU, "
-                         "released after the timed region; 0 / 1 = skip)")
+                         "(started before this process touches the GPU, released after the timed "
+                         "region; 0 / 1 = skip)")
+    ap.add_argument("--dropin-mp-concurrency", default="32,64",
+                    help="drop_in field: callers per serving process of the multi-process run, one "
+                         "measured window each (all processes together)")
     ap.add_argument("--workload", default="config4", choices=["config4", "config5"],
                     help="config4 (default, the BASELINE metric) or config5: bge-m3 embed, 6.25M x "
                          "1024 rows per GPU scanned in fp8, BM25 over the passage tokens fused by "
@@ -188,7 +191,8 @@ def main():
     mp = None
     if ("WORLD_SIZE" not in os.environ or os.environ.get("WORLD_SIZE") == "1") and not a.no_extras \
             and a.dropin_seconds > 0 and a.dropin_procs > 1 and a.workload == "config4":
-        mp = DropinProcs(a.dropin_procs, a.dropin_rows, a.dropin_seconds)
+        mp = DropinProcs(a.dropin_procs, a.dropin_rows, a.dropin_seconds,
+                         concurrency=[int(c) for c in a.dropin_mp_concurrency.split(",")])
     try:
         run_bench(a, mp)
     finally:
@@ -198,18 +202,23 @@ def main():
 
 class DropinProcs:
     """N serving processes of the drop-in per-request path on this GPU (tools/bench_dropin.py, one
-    collection, models and coalescers each, C = 64 closed-loop callers each), started as child
-    processes before the bench initialises the GPU; release() lets them set up and measure the
-    same window together, collect() sums their throughput and pools their request latencies."""
+    collection, models and coalescers each), started as child processes before the bench
+    initialises the GPU; release() lets them set up and measure together -- one window per
+    callers-per-process value C, every process starting window i at the same wall-clock time --
+    and collect() sums their throughput and pools their request latencies per window.
+    Closed-loop callers obey Little's law: mean latency = callers / throughput, so N x C callers
+    at X q/s wait N C / X on average whatever the batching policy (4 x 64 at ~420 q/s: ~610 ms)."""
 
-    def __init__(self, n, rows, seconds, script=None):
+    def __init__(self, n, rows, seconds, concurrency=(32, 64), script=None):
         import tempfile
         self.dir = tempfile.mkdtemp(prefix="sr_dropin_")
         self.go = os.path.join(self.dir, "go.json")
+        self.conc = list(concurrency)
         self.procs = []
         for i in range(n):
             cmd = [sys.executable, "-u", script or os.path.join(ROOT, "tools", "bench_dropin.py"),
-                   "--rows", str(rows), "--concurrency", "64", "--seconds", str(seconds),
+                   "--rows", str(rows), "--concurrency", *map(str, self.conc),
+                   "--seconds", str(seconds),
                    "--go-file", self.go, "--lat-out", os.path.join(self.dir, f"lat{i}")]
             out = open(os.path.join(self.dir, f"p{i}.json"), "w")
             err = open(os.path.join(self.dir, f"p{i}.err"), "w")
@@ -236,17 +245,25 @@ class DropinProcs:
                     tail = f.read()[-600:]
                 return {"error": f"serving process {i} exited {rc}: {tail}"}
             with open(out.name) as f:
-                runs.append(json.loads(f.read().strip().splitlines()[-1])["runs"][0])
-            lats.append(np.load(os.path.join(self.dir, f"lat{i}_c64.npy")))
-        lat = np.concatenate(lats)
-        return {"procs": len(runs), "concurrency_per_proc": 64,
-                "qps": round(sum(r["qps"] for r in runs), 1),
-                "per_proc_qps": [r["qps"] for r in runs],
+                runs.append(json.loads(f.read().strip().splitlines()[-1])["runs"])
+            lats.append([np.load(os.path.join(self.dir, f"lat{i}_c{c}.npy")) for c in self.conc])
+        windows = []
+        for w, c in enumerate(self.conc):
+            rw = [r[w] for r in runs]
+            lat = np.concatenate([lt[w] for lt in lats])
+            qps = sum(r["qps"] for r in rw)
+            windows.append({
+                "concurrency_per_proc": c, "callers": c * len(rw), "qps": round(qps, 1),
+                "per_proc_qps": [r["qps"] for r in rw],
                 "p50_ms": round(float(np.percentile(lat, 50)), 1),
                 "p99_ms": round(float(np.percentile(lat, 99)), 1),
-                "requests": int(sum(r["requests"] for r in runs)),
-                "seconds": max(r["seconds"] for r in runs),
-                "rerank_mean_batch": [r["coalesced"].get("rerank", {}).get("mean_batch") for r in runs]}
+                "mean_ms": round(float(lat.mean()), 1),
+                "littles_law_mean_ms": round(c * len(rw) / qps * 1e3, 1) if qps else None,
+                "requests": int(sum(r["requests"] for r in rw)),
+                "seconds": max(r["seconds"] for r in rw),
+                "rerank_mean_batch": [r["coalesced"].get("rerank", {}).get("mean_batch") for r in rw]})
+        return {"procs": len(runs), "windows": windows,
+                "note": "closed-loop callers: mean latency = callers / q/s (Little's law)"}
 
     def stop(self):
         for p, out, err in self.procs:
@@ -337,9 +354,9 @@ def run_bench(a, mp=None):
         drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds)
         drop_in["pipeline_qps_same_box"] = round(value, 2)
         if mp is not None:
-            # N serving processes on this GPU, C = 64 callers each, measured together (this
-            # process idle meanwhile): the per-process host cost (~5 ms of Python per request)
-            # spread over N interpreters
+            # N serving processes on this GPU, C callers each (one window per C), measured
+            # together (this process idle meanwhile): the per-process host cost (~5 ms of Python
+            # per request) spread over N interpreters
             mp.release()
             drop_in["multi_process"] = mp.collect()
 
@@ -430,9 +447,10 @@ def summary(line):
         r64 = next((r for r in d["runs"] if r.get("concurrency") == 64), d["runs"][0])
         out = {"c64_qps": r64.get("qps"), "c64_p50_ms": r64.get("p50_ms"), "c64_p99_ms": r64.get("p99_ms")}
         mp = d.get("multi_process")
-        if mp and "qps" in mp:
-            out["multi_process"] = {"procs": mp["procs"], "qps": mp["qps"], "p50_ms": mp["p50_ms"],
-                                    "p99_ms": mp["p99_ms"]}
+        if mp and "windows" in mp:
+            out["multi_process"] = {f"{mp['procs']}x{w['concurrency_per_proc']}":
+                                    {"qps": w["qps"], "p50_ms": w["p50_ms"], "p99_ms": w["p99_ms"]}
+                                    for w in mp["windows"]}
         return out
 
     c5, v2 = line.get("config5"), line.get("v2m3")
@@ -450,7 +468,7 @@ def summary(line):
     }
 
 
-def v2m3_field(a, local, dev):
+def v2m3_field(a, local, dev, fidelity=True):
     """bge-reranker-v2-m3 -- the reranker the reference seeds (migration/sql/model_configs_init.sql:
     4148; XLM-R large: 24 layers, 1024-d, 16 heads, FFN 4096) -- on the rerank stage alone at the
     bench shape: a.batch queries x a.k_cand candidates (S_pair = a.pair_len) per step, the pairs
@@ -503,6 +521,8 @@ def v2m3_field(a, local, dev):
         rer.close()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    if not fidelity:
+        return out
     fid = rerank_fidelity(rs, local, modes=((0, "fp16"), (3, "fp8_mode3")))
     out["fidelity"] = ({m: f"{v['top10_identical_mod_ties']} top-10 identical, std/err "
                            f"{v['min_std_over_err']}" for m, v in fid.items() if isinstance(v, dict)}

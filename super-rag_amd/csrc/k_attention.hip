@@ -1227,8 +1227,14 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
   SR_CHECK(tiles < (1ll << 31), "qkv_attention: too many tiles");
   // persistent: 8 XCD groups x G walkers, one 8-wave workgroup per CU (153 KiB of LDS)
   const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
-  // head groups of the tile walk (hg | heads): hg = heads walks every head of a panel in turn
+  // head groups of the tile walk (hg | heads): the walk takes every panel with heads [0, hg), then
+  // every panel with [hg, 2 hg), ...  An XCD's ~32 concurrent tiles then need ~32 / hg X panels
+  // (256 x d fp16) and hg W slices (192 x d fp16) in its 4 MiB L2: the divisor of heads that
+  // minimises 32 * 256 / hg + 192 hg (hg = 6 of 12 heads: 1,011 -> 1,033 TF/s and +0.9 % end to
+  // end against hg = heads; hg = 4 -5 %, profiles/r05_k5c_hgroup/)
   int hg = heads;
+  for (int v = 1; v <= heads; ++v)
+    if (heads % v == 0 && 8192.0 / v + 192.0 * v <= 8192.0 / hg + 192.0 * hg) hg = v;
 #if SR_WITH_DIAG
   if (const char* e = diag_getenv("SR_QA_HGROUP")) {
     const int v = std::atoi(e);

@@ -117,7 +117,8 @@ def test_parse_defaults_and_config5_field_args(monkeypatch):
 def test_dropin_procs_release_and_collect(tmp_path):
     """bench.DropinProcs with a stand-in serving script (no GPU): the children wait for the go
     file, start at its common time, and collect() sums their throughput and pools the latencies
-    of all of them for p50 / p99."""
+    of all of them for p50 / p99, one window per callers-per-process value, with Little's law's
+    mean beside the measured one."""
     script = tmp_path / "fake_dropin.py"
     script.write_text(
         "import argparse, json, os, sys, time\n"
@@ -125,23 +126,50 @@ def test_dropin_procs_release_and_collect(tmp_path):
         "sys.path.insert(0, %r)\n"
         "from tools.bench_dropin import wait_for_go\n"
         "ap = argparse.ArgumentParser()\n"
-        "for a in ('--rows', '--concurrency', '--seconds', '--go-file', '--lat-out'): ap.add_argument(a)\n"
+        "for a in ('--rows', '--seconds', '--go-file', '--lat-out'): ap.add_argument(a)\n"
+        "ap.add_argument('--concurrency', type=int, nargs='+')\n"
         "a = ap.parse_args()\n"
+        "assert a.concurrency == [32, 64]\n"
         "t0 = wait_for_go(a.go_file, timeout_s=60)\n"
         "assert abs(t0 - time.time()) < 30\n"
         "i = int(a.lat_out[-1])\n"
-        "np.save(a.lat_out + '_c64.npy', np.full(100, 10.0 * (i + 1), np.float32))\n"
-        "print(json.dumps({'runs': [{'qps': 100.0 + i, 'requests': 100, 'seconds': 1.0, 'p50_ms': 1, 'p99_ms': 2,\n"
-        "                            'coalesced': {'rerank': {'mean_batch': 4.0}}}]}))\n" % bench.ROOT)
-    mp = bench.DropinProcs(3, 100, 1.0, script=str(script))
+        "runs = []\n"
+        "for w, c in enumerate(a.concurrency):\n"
+        "    np.save(a.lat_out + '_c%%d.npy' %% c, np.full(100, 10.0 * (i + 1) * (w + 1), np.float32))\n"
+        "    runs.append({'qps': 100.0 + i, 'requests': 100, 'seconds': 1.0, 'p50_ms': 1, 'p99_ms': 2,\n"
+        "                 'coalesced': {'rerank': {'mean_batch': 4.0}}})\n"
+        "print(json.dumps({'runs': runs}))\n" % bench.ROOT)
+    mp = bench.DropinProcs(3, 100, 1.0, concurrency=(32, 64), script=str(script))
     try:
         mp.release(delay_s=0.5)
         r = mp.collect(timeout_s=120)
     finally:
         mp.stop()
-    assert r["procs"] == 3 and r["qps"] == 303.0 and r["requests"] == 300
-    assert r["p50_ms"] == 20.0 and r["p99_ms"] == 30.0
+    assert r["procs"] == 3 and len(r["windows"]) == 2
+    w32, w64 = r["windows"]
+    assert w32["concurrency_per_proc"] == 32 and w32["callers"] == 96
+    assert w32["qps"] == 303.0 and w32["requests"] == 300
+    assert w32["p50_ms"] == 20.0 and w32["p99_ms"] == 30.0 and w32["mean_ms"] == 20.0
+    assert w64["p50_ms"] == 40.0 and w64["littles_law_mean_ms"] == round(192 / 303.0 * 1e3, 1)
+    s = bench.summary({"value": 1, "unit": "q", "n_gpus": 1, "ms_per_step": 1,
+                       "drop_in": {"runs": [{"concurrency": 64, "qps": 9, "p50_ms": 1, "p99_ms": 2}],
+                                   "multi_process": r}})
+    assert s["drop_in"]["multi_process"]["3x32"]["qps"] == 303.0
     assert not os.path.exists(mp.dir)
+
+
+def test_dropin_windows_start_together():
+    """tools/bench_dropin._windows: with a common start time, window i begins at start + i
+    (seconds + gap) in every process; without one, immediately."""
+    import time
+    from tools.bench_dropin import WINDOW_GAP_S, _windows
+    t0 = time.time() + 0.3
+    seen = []
+    for c in _windows([16, 32], 0.2, t0):
+        seen.append((c, time.time()))
+    assert [c for c, _ in seen] == [16, 32]
+    assert seen[0][1] >= t0 and seen[1][1] >= t0 + 0.2 + WINDOW_GAP_S
+    assert [c for c in _windows([8], 5.0, 0.0)] == [8]
 
 
 def test_config5_workload_section(tmp_path):

@@ -169,6 +169,20 @@ def wait_for_go(path: str, timeout_s: float = 1800.0) -> float:
         return float(json.load(f)["start_at"])
 
 
+WINDOW_GAP_S = 4.0
+
+
+def _windows(concurrency, seconds: float, start_at: float):
+    """Yield each concurrency at its window's start: with a common start time (several serving
+    processes on one GPU) window i starts at start_at + i (seconds + WINDOW_GAP_S) in every
+    process, so the processes measure every window together."""
+    for i, c in enumerate(concurrency):
+        t = start_at + i * (seconds + WINDOW_GAP_S) if start_at > 0 else 0.0
+        if t > time.time():
+            time.sleep(t - time.time())
+        yield c
+
+
 def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16,
         start_at: float = 0.0, lat_out: str | None = None) -> dict:
     col_id = "dropin"
@@ -179,15 +193,14 @@ def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup
     queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
     # warm up: models resident, kernels compiled, coalescers created
     measure(min(warmup, max(concurrency)), 3.0, col_id, queries)
-    if start_at > time.time():  # several serving processes on one GPU: measure together
-        time.sleep(start_at - time.time())
     out = {"path": ("execute_search_flow (collection_service.py:229-366) -> pack vector_search / "
                     "merge / rerank runners -> EmbeddingService.embed_query + connector.search + "
                     "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
                     "(synthetic weights, hashing tokenizer); vector_topk 100, S_pair <= 128"),
            "rows": rows, "setup_s": round(setup, 1),
            "runs": [measure(c, seconds, col_id, queries,
-                            lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None)) for c in concurrency],
+                            lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None))
+                    for c in _windows(concurrency, seconds, start_at)],
            "reference_orchestration_ms_per_query": 5.14}
     return out
 

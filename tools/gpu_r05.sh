@@ -21,6 +21,8 @@ for P in ${PARTS//,/ }; do
     prof) rm -rf gpurun_out/prof_$TAG && bash tools/profile_round.sh $TAG > gpurun_out/$TAG/profile_round.log 2>&1 || exit 1
           python3 tools/pmc_traffic.py gpurun_out/prof_$TAG gpurun_out/$TAG/${TAG}_pmc_traffic.json > gpurun_out/$TAG/pmc_traffic.log 2>&1 || exit 1
           python3 tools/rocprof_vs_bench.py gpurun_out/prof_$TAG > gpurun_out/$TAG/rocprof_vs_bench.txt 2>&1 || exit 1
+          (cd tools && python3 -c "import sys; from rocprof_vs_bench import split_by_predecessor as s; s(sys.argv[1])" \
+             ../gpurun_out/prof_$TAG/c5/trace/run_kernel_trace.csv) > gpurun_out/$TAG/c5_split.txt 2>&1 || exit 1
           cp gpurun_out/prof_$TAG/trace/run_kernel_stats.csv gpurun_out/$TAG/${TAG}_rocprof_kernel_stats.csv
           cp gpurun_out/prof_$TAG/c5/trace/run_kernel_stats.csv gpurun_out/$TAG/${TAG}_c5_rocprof_kernel_stats.csv 2>/dev/null
           find gpurun_out/prof_$TAG -name "*.csv" -size +1M -delete ;;
@@ -32,6 +34,12 @@ for P in ${PARTS//,/ }; do
         timeout -k 10 900 bash tools/ab_bench.sh $TAG ${AB_LIBS:-$L/libsrmi_base.so $L/libsrmi_cstl.so $L/libsrmi_rpf.so} > gpurun_out/$TAG/ab.log 2>&1 || exit 1 ;;
     dropin) rm -rf gpurun_out/dropin_mp && timeout -k 10 1000 bash tools/gpu_dropin_mp.sh || exit 1
             python3 tools/dropin_mp_summary.py gpurun_out/dropin_mp > gpurun_out/$TAG/dropin_mp.txt 2>&1 || exit 1 ;;
+    v2ab) D=$PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so
+          for r in 1 2; do for hg in 0 16 4; do
+            env SUPER_RAG_AMD_LIB=$D $( [ $hg -gt 0 ] && echo SR_QA_HGROUP=$hg ) timeout -k 10 300 \
+              python -u tools/v2m3_bench.py --v2m3-steps 3 > gpurun_out/$TAG/v2m3_hg${hg}_r$r.log 2>&1 || exit 1
+            echo "hg=$hg r$r $(tail -1 gpurun_out/$TAG/v2m3_hg${hg}_r$r.log)" >> gpurun_out/$TAG/v2ab.txt
+          done; done ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac

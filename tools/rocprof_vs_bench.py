@@ -29,6 +29,31 @@ def main():
         bavg = v["ms_per_step"] * b["steps"] / v["launches"]
         r = tot[k] / n[k] if n[k] else float("nan")
         print(f"{k:28s} {r:10.4f} {n[k]:8d} {bavg:9.4f} {v['launches']:8d} {r / bavg:6.3f}")
+    split_by_predecessor(f"{src}/trace/run_kernel_trace.csv")
+
+
+def split_by_predecessor(path, top=6):
+    """One logical kernel serves several GEMMs of a layer (the residual + statistics GEMM is both
+    the O-projection, after the attention, and FFN2, after FFN1): its launches split by the kernel
+    launched before it on the same queue, with the mean duration of each group."""
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = logical(r["Kernel_Name"])
+            if k:
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k,
+                             r.get("Queue_Id", r.get("Stream_Id", "0"))))
+    rows.sort()
+    prev, tot, n = {}, defaultdict(float), Counter()
+    for t0, t1, k, q in rows:
+        key = (k, prev.get(q, "-"))
+        tot[key] += (t1 - t0) * 1e-6
+        n[key] += 1
+        prev[q] = k
+    print()
+    print("launches split by the kernel before them on the same queue (mean ms, total ms)")
+    for key in sorted(tot, key=lambda x: -tot[x])[:top * 2]:
+        print(f"{key[0]:28s} after {key[1]:28s} {n[key]:6d} x {tot[key] / n[key]:8.4f} ms = {tot[key]:9.2f} ms")
 
 
 if __name__ == "__main__":
