@@ -1335,6 +1335,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // the K-loop, the epilogue, the tile transition -- stored once at the end (lf.y8 as uint64 [8]
   // per wave); the stamps themselves cost a lgkmcnt(0) right behind a barrier
   constexpr bool STAMP = DIAG == 9 || DIAG == 10;
+  // global store instructions per wave the epilogue leaves in flight (the diagnostics without
+  // stores leave none: their waits must not let the next tile's staging loads through)
+  constexpr int NST = (DIAG == 5 || DIAG == 10) ? 0 : PipeEpi<EPI>::NSTORE;
   constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
   constexpr int GTAB = SR_GEMM_GELU_V2 ? GELU_NT + 1 : GELU_TAB;  // float2 entries
@@ -1569,9 +1572,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
     if (lenient) {
       if (CSTL && grp == 1)  // (+ the 4 constant pieces issued at the tile's top)
-        SR_WAITCNT(PipeEpi<EPI>::NSTORE + 4, 0);
+        SR_WAITCNT(NST + 4, 0);
       else
-        SR_WAITCNT(PipeEpi<EPI>::NSTORE, 0);
+        SR_WAITCNT(NST, 0);
     } else
       SR_WAITCNT(0, 0);
     __builtin_amdgcn_s_barrier();
@@ -1818,9 +1821,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     if (!full)
       SR_WAITCNT(0, 15);
     else if (grp == 0)  // (group 1: its K-step 1 glds too, awaited in K-step 0)
-      SR_WAITCNT(PipeEpi<EPI>::NSTORE, 15);
+      SR_WAITCNT(NST, 15);
     else
-      SR_WAITCNT(PipeEpi<EPI>::NSTORE + 16, 15);
+      SR_WAITCNT(NST + 16, 15);
     __builtin_amdgcn_s_barrier();
     stamp(4);  // phase 4: the tile transition (the next tile's K-step 0 wait + barrier)
     if constexpr (STAMP) st_sum[5] = __builtin_amdgcn_readfirstlane(st_sum[5] + 1);
