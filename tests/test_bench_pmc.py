@@ -201,3 +201,16 @@ def test_config5_workload_section(tmp_path):
     roof4 = {"bound": "mfma", "peak": 2500.0}
     bench.apply_pmc(roof4, "qkv_attention", ["gemm_a", "qkv_attention"], root)
     assert roof4["traffic"] == 120          # config 4 keeps the top-level records
+
+
+def test_logical_names_of_the_fp8_gemm_kernels():
+    """tools/pmc_traffic.logical: the F8IN instantiations (4th template argument true) carry the
+    bench's gemm_f8_* names, so config 5's PMC section matches its timed kernels."""
+    sys.path.insert(0, os.path.join(bench.ROOT, "tools"))
+    from pmc_traffic import logical
+    k = "_ZN2sr12_GLOBAL__N_116gemm_pipe_kernelILi{}ELb1ELi0ELb{}EEEvPKDF16_lS3_PKfPKvlPvliiiNS_6LnFoldE"
+    assert logical(k.format(11, 1)) == "gemm_f8_lnfold_gelu_out8"
+    assert logical(k.format(8, 1)) == "gemm_f8_lnres16_stats"
+    assert logical(k.format(8, 0)) == "gemm_f16_lnres16_stats"
+    assert logical(k.format(6, 0)) == "gemm_f16_lnfold_gelu"
+    assert logical("_ZN2sr12_GLOBAL__N_115qkv_attn_kernelILb1ELi0ELb0EEEvPKDF16_") == "qkv_attention"

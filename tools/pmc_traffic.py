@@ -45,7 +45,8 @@ def logical(name):
     m = re.search(r"gemm_\w*?kernelILi(\d+)E(\w*)", name)
     if m:
         base = EPI_NAMES.get(int(m.group(1)), f"gemm_epi{m.group(1)}")
-        if m.group(2).startswith("Lb") and m.group(2)[3:].startswith("Li0ELb1E"):  # F8IN variant
+        # template <EPI, PERSIST, DIAG, F8IN>: "...ILi<EPI>ELb<P>ELi<D>ELb1E" is the F8IN variant
+        if re.match(r"Lb[01]ELi\d+ELb1E", m.group(2)):
             base = base.replace("gemm_f16_", "gemm_f8_")
         return base
     m = re.search(r"\d+([a-z0-9_]+?)_kernel", name) or re.search(r"::(\w+?)_kernel", name)
