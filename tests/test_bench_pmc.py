@@ -206,6 +206,7 @@ def test_config5_workload_section(tmp_path):
 def test_logical_names_of_the_fp8_gemm_kernels():
     """tools/pmc_traffic.logical: the F8IN instantiations (4th template argument true) carry the
     bench's gemm_f8_* names, so config 5's PMC section matches its timed kernels."""
+    import sys
     sys.path.insert(0, os.path.join(bench.ROOT, "tools"))
     from pmc_traffic import logical
     k = "_ZN2sr12_GLOBAL__N_116gemm_pipe_kernelILi{}ELb1ELi0ELb{}EEEvPKDF16_lS3_PKfPKvlPvliiiNS_6LnFoldE"
