@@ -82,10 +82,6 @@
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
-#ifndef SR_GEMM_STAGE_ILV
-#define SR_GEMM_STAGE_ILV 0  // fp16 K-loop: the staging group issues its 16 LDS-DMA pieces one per
-                             // p3 MFMA instead of as one burst in front of them (A/B builds)
-#endif
 
 namespace sr {
 
@@ -1469,7 +1465,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // column sums of columns [nn, nn + 256), (mu, rstd) of rows [mm, mm + 256) (two pieces; rows past
   // M read as zero and are never stored).  Issued at the top of every tile (the previous tile's
   // epilogue, the last reader, ended before the transition barrier), younger than group 1's
-  // K-step 1 pieces and epilogue stores: K-step 0's lenient wait counts the 4 pieces too, the end
+  // K-step 1 pieces and epilogue stores: K-step 0's lenient wait counts the wave's piece too, the end
   // of K-step 1 (vmcnt(0)) awaits them, the epilogue reads them 10+ K-steps later (persistent FFN1
   // launches keep nk >= 4, host-checked).  (Issued from inside the K-step loop under a runtime kt
   // test, the staging code spilled 12-96 B at 256 VGPRs.)
@@ -1534,46 +1530,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     }
   };
 
-  // ILV p3 of the staging wave: A[4..7] x B' (k 32..63) with K-step kt2's 16 pieces (8 W, 8 X,
-  // the order and offsets of stage()) one after each MFMA, and (RN) the next K-step's p0 fragments
-  // read after every other MFMA
-  auto p3_ilv = [&](int kt2, half_t* s, bool RN, const half_t* nxt, bool stg) __attribute__((always_inline)) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const auto rw = panel_rsrc(W + (int64_t)n0 * K, (int64_t)(N - n0 < BN ? N - n0 : BN) * K * 2);
-    const auto rx = panel_rsrc(X + (int64_t)m0 * lda, (int64_t)(M - m0 < BM ? M - m0 : BM) * lda * 2);
-    const int kx = kt2 >= kxs ? kt2 - kxs : kt2;
-    int sw = w4 * 8 * 16 * K + kt2 * GBK * 2, sx = w4 * 8 * 16 * (int)lda + kx * GBK * 2;
-#endif
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = q >> 2, j = q & 3;
-      acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aX[i], bY[j], acc[4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#if defined(__HIP_DEVICE_COMPILE__)
-      if (!stg) {
-      } else if (q < 8) {
-        asm volatile("" : "+s"(sw));
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, SR_LDS(s + (w4 * 8 + q) * 8 * GBK), 16,
-                                                 vbw[q & 1], sw, 0, 0);
-        if (q < 7) sw += (PERMW ? perm_row_off(q + 1) - perm_row_off(q) : 8) * 2 * K;
-      } else {
-        asm volatile("" : "+s"(sx));
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, SR_LDS(s + BN * GBK + (w4 * 8 + q - 8) * 8 * GBK), 16,
-                                                 vbx[q & 1], sx, 0, 0);
-        sx += 16 * (int)lda;
-      }
-#endif
-      if (RN && (q & 1)) {
-        const int r = q >> 1;
-        if (r < 4)
-          aY[r] = read_frag(nxt, arow + 16 * r, c0);
-        else
-          bX[r - 4] = read_frag(nxt + BN * GBK, brow + 16 * (r - 4), c0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
   // One K-step.  SN: 0 none, 1 stage kt+2 of this tile, 2 stage K-steps 0/1 of tile (mn, nn).
   // RN: read kt+1's p0 fragments.  The barrier waits vmcnt(0), or vmcnt(32) when `lenient` (the
   // only younger VMEM ops are the previous tile's epilogue stores).
@@ -1615,8 +1571,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     SR_INTERLEAVE(4);
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
     if (lenient) {
-      if (CSTL && grp == 1)  // (+ the 4 constant pieces issued at the tile's top)
-        SR_WAITCNT(NST + 4, 0);
+      if (CSTL && grp == 1)  // (+ the wave's one constant piece issued at the tile's top)
+        SR_WAITCNT(NST + 1, 0);
       else
         SR_WAITCNT(NST, 0);
     } else
@@ -1629,9 +1585,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     }
     // (group (kt & 1) stages K-step kt + 2 in one burst while the partner wave of every SIMD,
     // from the other group, runs its MFMAs)
-    // ILV: the staging wave issues its pieces between its own p3 MFMAs instead (one piece per
-    // MFMA, the next K-step's fragment reads on every other one)
-    if (!SR_GEMM_STAGE_ILV && SN == 1 && DIAG != 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
+    // (interleaving the 16 pieces one per p3 MFMA instead measured -2.3 % on the main loop and
+    // -3.5 % end to end: profiles/r05_stage_ilv/)
+    if (SN == 1 && DIAG != 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
     if (SN == 2 && !LATE) {
       if (more_) {
         if (grp == 0)
@@ -1639,10 +1595,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         else
           stage(1, lds + STAGE, mn, nn);
       }
-    }
-    if (SR_GEMM_STAGE_ILV) {
-      p3_ilv(kt + 2, cur, RN, nxt, SN == 1 && DIAG != 1 && grp == (kt & 1));
-      return;
     }
     // p3: A[4..7] x B' (k 32..63); reads K-step kt+1's p0 operands
     if (RN) {
