@@ -82,6 +82,11 @@
 #ifndef SR_GEMM_LINE_STORE
 #define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
 #endif
+#ifndef SR_GEMM_RES_HALF
+#define SR_GEMM_RES_HALF 1  // persistent residual + statistics epilogues in half-tile order: their
+                            // constants from an LDS table, a 2 KiB line scratch, row group j + 1's
+                            // residual loaded before row group j's stores (store_tile_res)
+#endif
 
 namespace sr {
 
@@ -1124,6 +1129,172 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
   }
 }
 
+// The persistent residual + statistics epilogues (EPI_RES16_STATS / EPI_LNR16_STATS and their
+// e4m3-copy forms) in half-tile order, the FFN1 epilogue's layout:
+//   * bias, the residual's LayerNorm weight and the tile's row statistics come from the LDS table
+//     the K-loop staged (cst: [256 bias][256 gamma][256 x (mu, rstd)]), no global constant loads;
+//   * half h (column groups 2h, 2h + 1) outer, row group j inner: the 16 rows x 64 columns pass
+//     through the wave's 2 KiB line scratch and leave as whole 128-B lines (2 stores per (h, j));
+//   * the residual of step s + 1 = (h, j) + 1 is loaded before step s's stores, so its wait (vmcnt
+//     counts in issue order) does not also wait for those stores; step 0's is loaded before the
+//     next tile's staging burst (pre), so the first wait does not wait for the 16 pieces either;
+//   * the row's sum / M2 partials accumulate over both halves in the order of store_tile_wide
+//     (same fp16 outputs, same partials bit for bit).
+// Register budget: the tile's 128 accumulators + 32 constants of one half + 2 x 8 residual.
+template <int EPI, bool CHECK, bool PERM, class Pre = NoPre>
+__device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M, int N,
+                                               const void* __restrict__ R, int64_t ldr,
+                                               void* __restrict__ Y, int64_t ldy, const LnFold& lf,
+                                               half_t* __restrict__ scr, const Pre& pre,
+                                               const float* __restrict__ cst, int ln0, int lm0) {
+  constexpr bool Y8 = EPI == EPI_RES16_STATS_Y8 || EPI == EPI_LNR16_STATS_Y8;
+  constexpr bool LNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
+  static_assert(LNR || EPI == EPI_RES16_STATS || EPI == EPI_RES16_STATS_Y8, "store_tile_res: residual epilogues");
+  static_assert(PERM, "store_tile_res: the W tile staged in perm32 order (8 consecutive columns per lane)");
+  static_assert(SR_GEMM_STATS_MODE == 2, "store_tile_res: pivoted one-pass statistics");
+  const int g = lane >> 4, odd = g & 1;
+  const int clane = ln0 + 16 * odd + 4 * (g & 2);  // the lane's column in the tile's table (+ 32 p)
+  // lane-constant byte offsets: the residual segment of row (lane & 15) (+ 64 B per column group),
+  // the scratch write / read-back and the row-group store offsets of store_tile_gelu
+  const int lid = lane_id_here();
+  const uint32_t bo_res = (uint32_t)(((lid & 15) * (int)ldr + 16 * ((lid >> 4) & 1) + 4 * ((lid >> 4) & 2)) * 2);
+  const uint32_t wofs = (uint32_t)((lid & 15) * 128 + (((2 * ((lid >> 4) & 1) + (lid >> 5)) ^ (lid & 7)) << 4));
+  const uint32_t rofs = (uint32_t)((lid >> 3) * 128 + (((lid & 7) ^ (lid >> 3)) << 4));
+  const uint32_t gofs = (uint32_t)(((lid >> 3) * (int)ldy + (lid & 7) * 8) * 2);
+  const uint32_t g8 = (uint32_t)(8 * ldy * 2);
+  char* const sb = reinterpret_cast<char*>(scr);
+  auto load_res = [&](half8 (&r)[2], int st) __attribute__((always_inline)) {
+    const int h = st >> 2, row0 = mw0 + (st & 3) * 16;
+    const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
+    const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);
+#if defined(__HIP_DEVICE_COMPILE__)
+    r[0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rr, bo_res + 128 * h, 0, 0));
+    r[1] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rr, bo_res + 128 * h + 64, 0, 0));
+#else
+    (void)rr;
+#endif
+  };
+  half8 rA[2], rB[2];
+  load_res(rA, 0);
+  if constexpr (!std::is_same<Pre, NoPre>::value) {
+    __builtin_amdgcn_sched_barrier(0);
+    pre();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float4v bc[2][2], gc[2][2];  // bias / gamma of column groups 2h, 2h + 1
+  float ssum[4], ssq[4];
+  _Float16 piv[4];
+#pragma unroll
+  for (int st = 0; st < 8; ++st) {
+    const int h = st >> 2, j = st & 3;
+    if (j == 0) {
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int p = 2 * h + pp;
+        bc[pp][0] = *reinterpret_cast<const float4v*>(cst + clane + 32 * p);
+        bc[pp][1] = *reinterpret_cast<const float4v*>(cst + clane + 32 * p + 4);
+        if constexpr (LNR) {
+          gc[pp][0] = *reinterpret_cast<const float4v*>(cst + 256 + clane + 32 * p);
+          gc[pp][1] = *reinterpret_cast<const float4v*>(cst + 256 + clane + 32 * p + 4);
+        }
+      }
+    }
+    half8 (&rc)[2] = (st & 1) ? rB : rA;
+    if (st < 7) load_res((st & 1) ? rA : rB, st + 1);
+    float mu = 0.f, rstd = 1.f;
+    if constexpr (LNR) {
+      const float2 mr = *reinterpret_cast<const float2*>(cst + 512 + 2 * (lm0 + j * 16 + (lane & 15)));
+      mu = mr.x;
+      rstd = mr.y;
+    }
+    half8 hv[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int p = 2 * h + pp;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[2 * p][j][r] + bc[pp][0][r];
+        v[4 + r] = acc[2 * p + 1][j][r] + bc[pp][1][r];
+      }
+      if constexpr (LNR) {
+        const float nmr = -mu * rstd;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = fmaf(fmaf((float)rc[pp][r], rstd, nmr), gc[pp][0][r], v[r]);
+          v[4 + r] = fmaf(fmaf((float)rc[pp][4 + r], rstd, nmr), gc[pp][1][r], v[4 + r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] += (float)rc[pp][r];
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) hv[pp][r] = (half_t)v[r];
+      *reinterpret_cast<half8*>(sb + (wofs ^ (uint32_t)(pp << 6))) = hv[pp];
+    }
+    // statistics: pivot = the row's first value in the wave's 128-column span (column group 0,
+    // lane m & 15), sums over the column groups in order 0..3 (store_tile_wide's order)
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    if (h == 0) {
+      piv[j] = __builtin_bit_cast(_Float16, (unsigned short)__shfl(__builtin_bit_cast(unsigned short, hv[0][0]),
+                                                                    lane & 15, 64));
+      ssum[j] = 0.f;
+      ssq[j] = 0.f;
+    }
+    const h2v c2 = {piv[j], piv[j]};
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        const h2v x2 = {hv[pp][r], hv[pp][r + 1]};
+        const h2v d2 = x2 - c2;
+        ssum[j] = __builtin_amdgcn_fdot2(x2, h2v{(_Float16)1.f, (_Float16)1.f}, ssum[j], false);
+        ssq[j] = __builtin_amdgcn_fdot2(d2, d2, ssq[j], false);
+      }
+    // read back as 8 rows x 128 B per instruction and store (rows past M dropped by the range)
+    const int row0 = mw0 + j * 16;
+    const int64_t nr = CHECK ? (int64_t)max(0, min(16, M - row0)) : 16;
+    const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(Y) + (int64_t)row0 * ldy + nw0 + 64 * h, nr * ldy * 2);
+    const auto r8 = panel_rsrc(reinterpret_cast<const half_t*>(Y8 ? lf.y8 + (int64_t)row0 * ldy + nw0 + 64 * h : nullptr),
+                               Y8 ? nr * ldy : 0);
+    (void)r8;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const half8 o = *reinterpret_cast<const half8*>(sb + rofs + q * 1024);
+#if defined(__HIP_DEVICE_COMPILE__)
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, SR_GEMM_WST_AUX);
+      if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
+        typedef int v2i __attribute__((ext_vector_type(2)));
+        const v2i q8 = {(int)e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]),
+                        (int)e4m3x4((float)o[4], (float)o[5], (float)o[6], (float)o[7])};
+        __builtin_amdgcn_raw_buffer_store_b64(q8, r8, (gofs >> 1) + q * (g8 >> 1), 0, 0);
+      }
+#else
+      (void)o;
+      (void)ry;
+#endif
+    }
+    if (h == 1) {
+      float sum = ssum[j], sq = ssq[j];
+      sum += __shfl_xor(sum, 16, 64);
+      sq += __shfl_xor(sq, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      const float sp = fmaf(-128.f, (float)piv[j], sum);
+      const float m2 = fmaxf(fmaf(-sp * (1.f / 128.f), sp, sq), 0.f);
+      const int m_row = row0 + (lane & 15);
+      if (g == 0 && (!CHECK || m_row < M)) {
+        float2 stv;
+        stv.x = sum;
+        stv.y = m2;
+        *reinterpret_cast<float2*>(lf.stat_out + ((int64_t)m_row * (N >> 7) + (nw0 >> 7)) * 2) = stv;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // One epilogue for the pipelined kernels; NSTORE = global store instructions per wave on the
 // unchecked path (the persistent kernel's counted vmcnt relies on it: extra stores, such as the
 // statistics of the *_STATS epilogues, only make its waits stricter).
@@ -1146,6 +1317,9 @@ struct PipeEpi {
     if constexpr (WIDE && GLUT && SR_GEMM_GELU_V2 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
       store_tile_gelu<EPI, CHECK, PERM, Pre, 0, CST>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre,
                                                      cst, ln0, lm0);
+    else if constexpr (WIDE && CST && (EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS ||
+                                       EPI == EPI_RES16_STATS_Y8 || EPI == EPI_LNR16_STATS_Y8))
+      store_tile_res<EPI, CHECK, PERM, Pre>(acc, nw0, mw0, lane, M, N, R, ldr, Y, ldy, lf, scr, pre, cst, ln0, lm0);
     else if constexpr (WIDE)
       store_tile_wide<EPI, CHECK, LINE, GLUT, PERM, Pre>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf, scr, gtab, pre);
     else
@@ -1356,16 +1530,29 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // storing at once) -- measured in-kernel as an epilogue of 11.2k cycles with stores vs 4.4k
   // without (profiles/r05c/ffn1_stamps.log)
   constexpr bool CSTL = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_CSTL;
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
-                                                     (CSTL ? 2048 : 0) + (SCAN ? 512 : 0) +
+  // RHALF: the persistent residual + statistics epilogues in half-tile order (store_tile_res): a
+  // 2 KiB line scratch per wave and the same 4 KiB constants table ([256 bias][256 gamma][256 x
+  // (mu, rstd)]; RES16: the bias only), the next tile's staging issued from inside the epilogue
+  constexpr bool RESEPI = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS || EPI == EPI_RES16_STATS_Y8 ||
+                          EPI == EPI_LNR16_STATS_Y8;
+  constexpr bool RLNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
+  // (the LNR epilogues on fp16 operands only: the RES16 and fp8-operand instantiations spilled
+  // 12-36 B in this form and RES16 measured 907 -> 860 TF/s, profiles/r05_res_half/)
+  constexpr bool RHALF = SR_GEMM_RES_HALF && RLNR && !F8IN && LINE && PERSIST && SR_GEMM_WIDE_BUFST &&
+                         SR_GEMM_PERMW && SR_GEMM_STATS_MODE == 2;
+  constexpr bool CSTX = CSTL || RHALF;              // an epilogue constants table in LDS
+  constexpr int NCST = CSTL ? 4 : RHALF ? (RLNR ? 4 : 1) : 0;  // its 1 KiB pieces (one per wave)
+  constexpr int LSCR = LINE ? (RHALF ? 8 * 1024 : 8 * 2048) : 0;
+  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0) +
+                                                     (CSTX ? 2048 : 0) + (SCAN ? 512 : 0) +
                                                      (GLUT ? 4 * GTAB : 0)];
-  float* const cst = reinterpret_cast<float*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0));
+  float* const cst = reinterpret_cast<float*>(lds + 2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0));
   (void)cst;
-  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + (LINE ? 8 * 2048 : 0) + (GLINE ? 8 * 1024 : 0) +
-                                                 (CSTL ? 2048 : 0));
+  float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0) +
+                                                 (CSTX ? 2048 : 0));
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
   // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
-  constexpr bool LATE = SR_GEMM_LATE_STAGE && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
+  constexpr bool LATE = (SR_GEMM_LATE_STAGE || RHALF) && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -1404,7 +1591,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wm = wave & 3;
   // the epilogue's per-wave scratch: LINE 4 KiB / GLINE 2 KiB (nothing else uses it)
-  half_t* const escr = lds + 2 * STAGE + wave * (GLINE ? 1024 : 2048);
+  half_t* const escr = lds + 2 * STAGE + wave * ((GLINE || RHALF) ? 1024 : 2048);
   half_t* const gscr = GLINE ? escr : nullptr;
   (void)gscr;
   const int nk = K / GBK;
@@ -1473,8 +1660,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #if defined(__HIP_DEVICE_COMPILE__)
     // (the lane offset re-derived here: a hoisted one stayed live through the K-loop and spilled)
     const uint32_t lo = (uint32_t)lane_id_here() * 16u;
-    if (w4 < 2) {
-      const float* src = w4 == 0 ? bias : lf.colsum;
+    if (w4 >= NCST) {
+    } else if (w4 < 2) {  // bias; column sums (FFN1) or the residual's LayerNorm weight (RHALF)
+      const float* src = w4 == 0 ? bias : CSTL ? lf.colsum : lf.gamma;
       const auto r = panel_rsrc(reinterpret_cast<const half_t*>(src + nn), 1024);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(cst + 256 * w4), 16, lo, 0, 0, 0);
     } else {
@@ -1571,7 +1759,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     SR_INTERLEAVE(4);
     // K-step kt+1 landed (all waves) and buffer kt&1 is no longer read: restage it
     if (lenient) {
-      if (CSTL && grp == 1)  // (+ the wave's one constant piece issued at the tile's top)
+      if (NCST && grp == 1 && w4 < NCST)  // (+ the wave's one constant piece issued at the tile's top)
         SR_WAITCNT(NST + 1, 0);
       else
         SR_WAITCNT(NST, 0);
@@ -1682,7 +1870,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   };
 
   for (;;) {
-    if (CSTL && grp == 1) stage_cst(m0, n0);
+    if (NCST && grp == 1) stage_cst(m0, n0);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1802,11 +1990,13 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
         }
       };
       if (full)
-        PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                          R, ldr, Y, ldy, lf, escr, gtab, pre);
+        PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW, decltype(pre), CSTX>(
+            acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, pre, cst, wn * 128,
+            wm * 64);
       else
-        PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias,
-                                                         R, ldr, Y, ldy, lf, escr, gtab, pre);
+        PipeEpi<EPI_OUT>::template run<true, LINE, GLUT, PERMW, decltype(pre), CSTX>(
+            acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, pre, cst, wn * 128,
+            wm * 64);
     } else if (full) {
       PipeEpi<EPI_OUT>::template run<false, LINE, GLUT, PERMW, NoPre, CSTL>(
           acc, n0 + wn * 128, m0 + wm * 64, lane, M, N, bias, R, ldr, Y, ldy, lf, escr, gtab, NoPre{}, cst, wn * 128,
@@ -2537,8 +2727,11 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
 #undef SR_PP_CASE
   } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
     // (the FFN1 epilogues stage their constants during K-step 1 of a persistent tile: nk >= 4)
+    // (SR_GEMM_RES_HALF: the persistent LNR epilogues stage consecutive row statistics, stat_ld 1)
     const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK &&
-                         ((epi != EPI_LNF_GELU_F16 && epi != EPI_LNF_GELU_F8) || K >= 4 * GBK);
+                         ((epi != EPI_LNF_GELU_F16 && epi != EPI_LNF_GELU_F8) || K >= 4 * GBK) &&
+                         !(SR_GEMM_RES_HALF && (epi == EPI_LNR16_STATS || epi == EPI_LNR16_STATS_Y8) &&
+                           lfv.stat_ld != 1);
     // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)
     const int64_t g = persist ? 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8)) : big_tiles;
     SR_CHECK(!persist || (g % 8 == 0 && g >= 8), "gemm: persistent grid must be a multiple of 8");

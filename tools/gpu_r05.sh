@@ -42,7 +42,8 @@ for P in ${PARTS//,/ }; do
           done; done ;;
     var) L=$PWD/super-rag_amd/super_rag_amd/lib_ab; V=${VAR:?VAR}
          SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so timeout -k 10 400 \
-           python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_ffn1_epilogue.py tests/test_gpu_encoder.py -x -q \
+           python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_ffn1_epilogue.py tests/test_gpu_encoder.py \
+           tests/test_gpu_rerank_fidelity.py tests/test_gpu_rerank_fidelity_v2m3.py tests/test_gpu_configs.py -x -q \
            --timeout 240 --timeout-method thread > gpurun_out/$TAG/var_tests_$V.log 2>&1 || exit 1
          for r in 1 2; do for D in $PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so $L/libsrmi_diag_$V.so; do
            echo "== $(basename $D) r$r" >> gpurun_out/$TAG/var_ffn1_$V.log
