@@ -57,7 +57,8 @@ int sr_diag_gemm_stats(const void* X, int64_t lda, const void* W, const float* b
                        int device, void* stream);
 
 /* Diagnostic: the fp16 FFN1 of sr_diag_ffn1 with in-kernel s_memtime phase stamps (diag 9: the
- * product epilogue, 10: its math without the global stores).  stamps: device uint64 [grid x 8
+ * product epilogue, 10: its math without the global stores, 11: the product epilogue without the
+ * next tile's staging in its shadow -- timing only, wrong results).  stamps: device uint64 [grid x 8
  * waves x 8] = per wave [tile transitions, cycles of: K-step 0 (tile start -> its barrier),
  * K-step 1, the rest of the K-loop, the epilogue, the transition wait + barrier, K-steps per
  * tile, 0] (grid = 8 x min(32, tiles / 8) persistent workgroups). */

@@ -1508,7 +1508,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // the stores): per-wave s_memtime phase sums of every tile -- K-step 0, K-step 1, the rest of
   // the K-loop, the epilogue, the tile transition -- stored once at the end (lf.y8 as uint64 [8]
   // per wave); the stamps themselves cost a lgkmcnt(0) right behind a barrier
-  constexpr bool STAMP = DIAG == 9 || DIAG == 10;
+  constexpr bool STAMP = DIAG == 9 || DIAG == 10 || DIAG == 11;  // (11: 9 without the next tile's staging)
   // global store instructions per wave the epilogue leaves in flight (the diagnostics without
   // stores leave none: their waits must not let the next tile's staging loads through)
   constexpr int NST = (DIAG == 5 || DIAG == 10) ? 0 : PipeEpi<EPI>::NSTORE;
@@ -1536,16 +1536,17 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr bool RESEPI = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS || EPI == EPI_RES16_STATS_Y8 ||
                           EPI == EPI_LNR16_STATS_Y8;
   constexpr bool RLNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
-  // (the LNR epilogues on fp16 operands only: the RES16 and fp8-operand instantiations spilled
-  // 12-36 B in this form and RES16 measured 907 -> 860 TF/s, profiles/r05_res_half/)
-  constexpr bool RHALF = SR_GEMM_RES_HALF && RLNR && !F8IN && LINE && PERSIST && SR_GEMM_WIDE_BUFST &&
-                         SR_GEMM_PERMW && SR_GEMM_STATS_MODE == 2;
+  // (EPI_LNR16_STATS on fp16 operands only: the RES16 and fp8-operand instantiations spilled
+  // 12-36 B in this form, RES16 measured 907 -> 860 TF/s and the e4m3-copy LNR (fp8 mode 3's
+  // O-projection) 777 -> 761, profiles/r05_res_half/, r05_wexp_lds/)
+  constexpr bool RHALF = SR_GEMM_RES_HALF && EPI == EPI_LNR16_STATS && !F8IN && LINE && PERSIST &&
+                         SR_GEMM_WIDE_BUFST && SR_GEMM_PERMW && SR_GEMM_STATS_MODE == 2;
   constexpr bool CSTX = CSTL || RHALF;              // an epilogue constants table in LDS
   constexpr int NCST = CSTL ? 4 : RHALF ? (RLNR ? 4 : 1) : 0;  // its 1 KiB pieces (one per wave)
   constexpr int LSCR = LINE ? (RHALF ? 8 * 1024 : 8 * 2048) : 0;
-  __shared__ __attribute__((aligned(16))) half_t lds[2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0) +
-                                                     (CSTX ? 2048 : 0) + (SCAN ? 512 : 0) +
-                                                     (GLUT ? 4 * GTAB : 0)];
+  constexpr int LDS_BASE = 2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0) + (CSTX ? 2048 : 0) + (SCAN ? 512 : 0) +
+                           (GLUT ? 4 * GTAB : 0);
+  __shared__ __attribute__((aligned(16))) half_t lds[LDS_BASE];
   float* const cst = reinterpret_cast<float*>(lds + 2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0));
   (void)cst;
   float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0) +
@@ -1776,7 +1777,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     // (interleaving the 16 pieces one per p3 MFMA instead measured -2.3 % on the main loop and
     // -3.5 % end to end: profiles/r05_stage_ilv/)
     if (SN == 1 && DIAG != 1 && grp == (kt & 1)) stage(kt + 2, cur, m0, n0);
-    if (SN == 2 && !LATE) {
+    if (SN == 2 && !LATE && DIAG != 11) {
       if (more_) {
         if (grp == 0)
           stage(0, lds, mn, nn);
@@ -1881,6 +1882,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       for (int i = 0; i < 8; ++i) {
         const int n = PERMW ? n0 + wn * 128 + 32 * (i >> 1) + 4 * (i & 1) + perm32(lane & 15)
                             : n0 + arow + 16 * i;
+        // (from an LDS copy staged with the tile's first K-step instead: fp8 FFN1 1,572 -> 1,540
+        // TF/s, spills 8 -> 20 B, profiles/r05_wexp_lds/)
         sa[i] = wexp[n < N ? n : N - 1];
       }
     }
@@ -2447,12 +2450,12 @@ void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8,
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
                       int M, int N, int K, hipStream_t stream, uint64_t* stamps) {
-  SR_CHECK(diag == 0 || diag == 2 || (diag >= 5 && diag <= 7) || diag == 9 || diag == 10,
-           "ffn1_diag: diag must be 0, 2, 5, 6, 7, 9 or 10");
+  SR_CHECK(diag == 0 || diag == 2 || (diag >= 5 && diag <= 7) || (diag >= 9 && diag <= 11),
+           "ffn1_diag: diag must be 0, 2, 5, 6, 7, 9, 10 or 11");
   SR_CHECK(N % 256 == 0 && M > 0, "ffn1_diag: N % 256 == 0, M > 0");
   // diag 7 stores every tile unchecked onto rows 0..255 of Y
   SR_CHECK(diag != 7 || (M >= 256 && ldy >= N), "ffn1_diag: diag 7 needs M >= 256, ldy >= N");
-  SR_CHECK((diag != 9 && diag != 10) || (stamps && !f8), "ffn1_diag: diag 9 / 10 need a stamp buffer (fp16)");
+  SR_CHECK(diag < 9 || (stamps && !f8), "ffn1_diag: diag 9 / 10 / 11 need a stamp buffer (fp16)");
   LnFold lf;
   lf.mr = mr;
   lf.colsum = colsum;
@@ -2508,6 +2511,8 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
       SR_FD(9)
     } else if (diag == 10) {
       SR_FD(10)
+    } else if (diag == 11) {
+      SR_FD(11)
     } else {
       SR_FD(7)
     }
@@ -2730,8 +2735,7 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
     // (SR_GEMM_RES_HALF: the persistent LNR epilogues stage consecutive row statistics, stat_ld 1)
     const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK &&
                          ((epi != EPI_LNF_GELU_F16 && epi != EPI_LNF_GELU_F8) || K >= 4 * GBK) &&
-                         !(SR_GEMM_RES_HALF && (epi == EPI_LNR16_STATS || epi == EPI_LNR16_STATS_Y8) &&
-                           lfv.stat_ld != 1);
+                         !(SR_GEMM_RES_HALF && epi == EPI_LNR16_STATS && lfv.stat_ld != 1);
     // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)
     const int64_t g = persist ? 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8)) : big_tiles;
     SR_CHECK(!persist || (g % 8 == 0 && g >= 8), "gemm: persistent grid must be a multiple of 8");

@@ -1,6 +1,7 @@
 """In-kernel phase stamps of the persistent fp16 FFN1 GEMM (diagnostic library, sr_diag_ffn1_stamps):
 where a tile's cycles go -- K-step 0, K-step 1, the rest of the K-loop, the epilogue, the tile
-transition -- with the product epilogue (diag 9) and with its math but no global stores (diag 10).
+transition -- with the product epilogue (diag 9), with its math but no global stores (diag 10), and
+with the product epilogue but no staging of the next tile in its shadow (diag 11, timing only).
 
     python tools/ffn1_stamps.py [--M 524288] [--reps 5]
 
@@ -40,7 +41,8 @@ def main():
     st = torch.zeros(grid * 8 * 8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     names = ["K-step 0", "K-step 1", "rest of K-loop", "epilogue", "transition"]
-    for diag, what in ((9, "product epilogue"), (10, "math, no global stores")):
+    for diag, what in ((9, "product epilogue"), (10, "math, no global stores"),
+                       (11, "product epilogue, next tile not staged (wrong results)")):
         acc = None
         for r in range(a.reps + 1):
             st.zero_()

@@ -47,7 +47,7 @@ for P in ${PARTS//,/ }; do
            --timeout 240 --timeout-method thread > gpurun_out/$TAG/var_tests_$V.log 2>&1 || exit 1
          for r in 1 2; do for D in $PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so $L/libsrmi_diag_$V.so; do
            echo "== $(basename $D) r$r" >> gpurun_out/$TAG/var_ffn1_$V.log
-           SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 300 python -u tools/ffn1_bench.py --diags 0,2 --rounds 2 \
+           SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 300 python -u tools/ffn1_bench.py --diags 0,2 --rounds 2 $VAR_FFN1_ARGS \
              >> gpurun_out/$TAG/var_ffn1_$V.log 2>&1 || exit 1
          done; done ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
