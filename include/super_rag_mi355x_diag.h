@@ -56,6 +56,14 @@ int sr_diag_gemm_stats(const void* X, int64_t lda, const void* W, const float* b
                        int64_t ldr, void* Y, int64_t ldy, int M, int N, int K, float* stat_out,
                        int device, void* stream);
 
+/* Diagnostic: the FFN2 / O-projection GEMM of the LN-folded encoders, EPI_LNR16_STATS:
+ * Y = X W^T + bias + ((R - mu) rstd) gamma per row (R un-normalised, mr = (mu, rstd) per row,
+ * consecutive), fp16 Y, and the (sum, M2) partials of every 128-column span of Y as
+ * sr_diag_gemm_stats. */
+int sr_diag_gemm_lnr_stats(const void* X, int64_t lda, const void* W, const float* bias, const void* R,
+                           int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
+                           int N, int K, float* stat_out, int device, void* stream);
+
 /* Diagnostic: the fp16 FFN1 of sr_diag_ffn1 with in-kernel s_memtime phase stamps (diag 9: the
  * product epilogue, 10: its math without the global stores, 11: the product epilogue without the
  * next tile's staging in its shadow -- timing only, wrong results).  stamps: device uint64 [grid x 8

@@ -838,6 +838,30 @@ int sr_diag_gemm_stats(const void* X, int64_t lda, const void* W, const float* b
   SR_API_END
 }
 
+int sr_diag_gemm_lnr_stats(const void* X, int64_t lda, const void* W, const float* bias, const void* R,
+                           int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
+                           int N, int K, float* stat_out, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(R);
+  SR_NONNULL(mr);
+  SR_NONNULL(gamma);
+  SR_NONNULL(Y);
+  SR_NONNULL(stat_out);
+  SR_CHECK(N % 256 == 0, "diag_gemm_lnr_stats: N % 256 == 0");
+  sr::DeviceGuard g(device);
+  sr::LnFold lf;
+  lf.mr = mr;
+  lf.gamma = gamma;
+  lf.stat_out = stat_out;
+  sr::launch_gemm(sr::EPI_LNR16_STATS, reinterpret_cast<const sr::half_t*>(X), lda,
+                  reinterpret_cast<const sr::half_t*>(W), bias, R, ldr, Y, ldy, M, N, K,
+                  reinterpret_cast<hipStream_t>(stream), &lf);
+  SR_API_END
+}
+
 int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                  const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
                  int N, int K, int device, void* stream) {

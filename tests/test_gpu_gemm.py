@@ -147,3 +147,45 @@ def test_stats_epilogue_large_offset_rows(offset, M):
     ratio = np.abs(mean) / np.sqrt(m2 / 128)
     print(f"offset {offset}: max |mean|/std {ratio.max():.0f}, max rel M2 err {rel.max():.2e}")
     assert rel.max() <= 2e-3, rel.max()
+
+
+@pytest.mark.parametrize("M,K", [(256 * 200 + 77, 768), (256 * 176, 3072), (1000, 768)])
+def test_lnr_stats_epilogue_persistent_ragged(M, K):
+    """The FFN2 / O-projection GEMM of the LN-folded encoders (EPI_LNR16_STATS: Y = X W^T + b +
+    LN(R) with R un-normalised, and the 128-column (sum, M2) partials of the fp16 Y) on the
+    persistent kernel's half-tile epilogue (>= 512 tiles: constants and row statistics staged in
+    LDS, 2 KiB line scratch, residual prefetch, next tile staged in the epilogue) and on the
+    one-tile-per-workgroup kernel (M = 1000): every output row against fp64, the partials against a
+    two-pass fp64 computation on the same fp16 outputs, rows past M untouched (guard band)."""
+    import numpy as np
+    import torch
+    from super_rag_amd import _native as NT
+    dev = torch.device("cuda", 0)
+    N, GUARD = 768, 40
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    X = (torch.randn(M, K, device=dev, generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device=dev, generator=g) * 0.02).half()
+    b = torch.randn(N, device=dev, generator=g) * 0.1
+    gamma = 1.0 + torch.randn(N, device=dev, generator=g) * 0.2
+    R = (torch.randn(M, N, device=dev, generator=g) * 0.8 + 0.3).half()
+    Rf = R.float()
+    mu = Rf.mean(1)
+    rstd = torch.rsqrt(Rf.var(1, unbiased=False) + 1e-5)
+    mr = torch.stack([mu, rstd], 1).contiguous()
+    Yall = torch.full((M + GUARD, N), 777.0, device=dev, dtype=torch.float16)
+    st = torch.full((M, N // 128, 2), float("nan"), device=dev)
+    NT.call_diag("sr_diag_gemm_lnr_stats", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(), N,
+                 mr.data_ptr(), gamma.data_ptr(), Yall.data_ptr(), N, M, N, K, st.data_ptr(), 0,
+                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = (X.double() @ W.double().T + b.double()
+           + ((Rf.double() - mu.double()[:, None]) * rstd.double()[:, None]) * gamma.double())
+    Y = Yall[:M]
+    err = (Y.double() - ref).abs().max().item()
+    assert err <= 2 ** -10 * max(1.0, ref.abs().max().item()) + 1e-4, err
+    assert bool((Yall[M:] == 777.0).all()), "rows past M were written"
+    y = Y.double().cpu().numpy().reshape(M, N // 128, 128)
+    s = st.double().cpu().numpy()
+    m2 = ((y - y.mean(-1, keepdims=True)) ** 2).sum(-1)
+    np.testing.assert_allclose(s[..., 0], y.sum(-1), rtol=1e-6, atol=1e-3)
+    assert (np.abs(s[..., 1] - m2) <= 2e-3 * m2 + 1e-4).all()
