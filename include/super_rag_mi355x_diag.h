@@ -64,6 +64,15 @@ int sr_diag_gemm_lnr_stats(const void* X, int64_t lda, const void* W, const floa
                            int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
                            int N, int K, float* stat_out, int device, void* stream);
 
+/* Diagnostic: K5c (fused QKV projection + attention, LN-folded: X un-normalised rows, W the folded
+ * [Q; K; V] weight (3d x d), bias the folded bias, colsum its row sums, mr (mu, rstd) per row; S ==
+ * 128, head dim 64) with in-kernel s_memtime phase stamps.  stamps: device uint64 [grid x 8 waves
+ * x 8] = per wave [tiles, cycles of: the K-loop, the epilogue into the LDS images, the attention,
+ * the tile transition, 0, 0, 0]; grid = 8 x min(32, ceil(B S / 256 x heads / 8)). */
+int sr_diag_qkv_attention_stamps(const void* X, int64_t lda, const void* W, const float* bias,
+                                 const float* colsum, const float* mr, const int32_t* mask, void* ctx, int B,
+                                 int S, int d, int heads, uint64_t* stamps, int device, void* stream);
+
 /* Diagnostic: the fp16 FFN1 of sr_diag_ffn1 with in-kernel s_memtime phase stamps (diag 9: the
  * product epilogue, 10: its math without the global stores, 11: the product epilogue without the
  * next tile's staging in its shadow -- timing only, wrong results).  stamps: device uint64 [grid x 8

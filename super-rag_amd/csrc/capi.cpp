@@ -906,6 +906,29 @@ int sr_diag_copy(const void* src, void* dst, int64_t bytes, int device, void* st
   SR_API_END
 }
 
+int sr_diag_qkv_attention_stamps(const void* X, int64_t lda, const void* W, const float* bias,
+                                 const float* colsum, const float* mr, const int32_t* mask, void* ctx, int B,
+                                 int S, int d, int heads, uint64_t* stamps, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(colsum);
+  SR_NONNULL(mr);
+  SR_NONNULL(mask);
+  SR_NONNULL(ctx);
+  SR_NONNULL(stamps);
+  sr::DeviceGuard g(device);
+  sr::LnFold lf;
+  lf.mr = mr;
+  lf.colsum = colsum;
+  sr::launch_qkv_attention(sr::EPI_LNF_F16, reinterpret_cast<const sr::half_t*>(X), lda,
+                           reinterpret_cast<const sr::half_t*>(W), bias, &lf, mask,
+                           reinterpret_cast<sr::half_t*>(ctx), B, S, d, heads,
+                           reinterpret_cast<hipStream_t>(stream), nullptr, stamps);
+  SR_API_END
+}
+
 int sr_diag_attention(int variant, const void* qkv, const int32_t* mask, void* ctx, int B, int S,
                       int Sq, int d, int heads, int device, void* stream) {
   SR_API_BEGIN

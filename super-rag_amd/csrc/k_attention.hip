@@ -813,8 +813,21 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const float* __restrict__ colsum, const float* __restrict__ mr,
     const int32_t* __restrict__ mask, half_t* __restrict__ ctx, int M, int d, int heads,
-    float scale_log2, int hg) {
+    float scale_log2, int hg, uint64_t* __restrict__ stamps) {
   constexpr int DH = 64;
+  // DIAG 3 (diagnostic library): per-wave s_memtime phase sums of every tile -- the K-loop, the
+  // epilogue into the LDS images, the attention, the tile transition -- stored once at the end
+  // (stamps: uint64 [grid x 8 waves x 8] = [tiles, K-loop, epilogue, attention, transition, 0..])
+  constexpr bool STAMP = DIAG == 3;
+  uint32_t st_t0 = 0, st_sum[5] = {0, 0, 0, 0, 0};
+  auto stamp = [&](int phase) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memtime();
+      st_sum[phase] = __builtin_amdgcn_readfirstlane(st_sum[phase] + (t1 - st_t0));
+      st_t0 = t1;
+    }
+  };
+  (void)stamps;
   constexpr int IMG = 3 * QA_BM * DH;  // Q, K, V images (96 KiB)
   // LDS: the images, then one K-step buffer (PB) past them; odd K-steps use PA = the first 56 KiB
   // of the image area (dead during the K-loop).  So the next tile's K-step 0 (PB) is staged while
@@ -891,6 +904,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     stage(1, PA, m0, h);
   }
   __builtin_amdgcn_s_barrier();
+  if constexpr (STAMP) st_t0 = (uint32_t)__builtin_amdgcn_s_memtime();
 
   for (;;) {
 #pragma unroll
@@ -958,6 +972,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
 
+    stamp(1);  // the K-loop
     // ---- epilogue -> LDS images (PA / PB are dead: every wave passed the last barrier after its
     // final LDS reads, and no staging is in flight) ----
     half_t* Qi = lds;
@@ -1008,6 +1023,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     }
     if (tid < QA_BM) kbias[tid] = (m_mk < M && mkv != 0) ? 0.f : -INFINITY;
     __syncthreads();
+    stamp(2);  // the epilogue
     const int t_next = t + t_step;
     const bool more = t_next < t_end;
     const int h_n = tile_h(t_next), m0_n = tile_m(t_next);
@@ -1131,6 +1147,8 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         }
       }
     }  // attend
+    stamp(3);  // the attention
+    if constexpr (STAMP) st_sum[0] = __builtin_amdgcn_readfirstlane(st_sum[0] + 1);
     if (!more) break;
     // every wave is done with the images: the next tile's K-step 1 goes into PA; K-step 0 (group 0,
     // older than this wave's 4 ctx stores) must have landed before the barrier
@@ -1143,9 +1161,17 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         SR_WAITCNT(0, 15);
     }
     __builtin_amdgcn_s_barrier();
+    stamp(4);  // the transition
     t = t_next;
     h = h_n;
     m0 = m0_n;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && stamps) {
+      uint64_t* o = stamps + ((int64_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] = st_sum[i];
+    }
   }
 }
 }  // namespace
@@ -1211,7 +1237,7 @@ bool qkv_attention_supported(int S, int d, int heads) {
 
 void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                           const LnFold* lf, const int32_t* mask, half_t* ctx, int B, int S, int d,
-                          int heads, hipStream_t stream, uint8_t* ctx8) {
+                          int heads, hipStream_t stream, uint8_t* ctx8, uint64_t* stamps) {
   SR_CHECK(qkv_attention_supported(S, d, heads), "qkv_attention: needs S == 128 and d_h == 64");
   SR_CHECK(epi == EPI_BIAS_F16 || (epi == EPI_LNF_F16 && lf && lf->mr && lf->colsum && lf->stat_ld == 1),
            "qkv_attention: epilogue EPI_BIAS_F16 or EPI_LNF_F16 (row statistics + column sums)");
@@ -1246,12 +1272,16 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
     const char* e = diag_getenv("SR_QA_DIAG");
     return e ? std::atoi(e) : 0;
   }();
-  if (epi == EPI_LNF_F16 && diag == 1)
+  SR_CHECK(!stamps || epi == EPI_LNF_F16, "qkv_attention: stamps with the LN-folded epilogue");
+  if (stamps)
+    hipLaunchKernelGGL((qkv_attn_kernel<true, 3>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg, stamps);
+  else if (epi == EPI_LNF_F16 && diag == 1)
     hipLaunchKernelGGL((qkv_attn_kernel<true, 1>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
-                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg, stamps);
   else if (epi == EPI_LNF_F16 && diag == 2)
     hipLaunchKernelGGL((qkv_attn_kernel<true, 2>), grid, block, 0, stream, X, lda, W, bias, lf->colsum,
-                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg, stamps);
   else
 #endif
 #if SR_WITH_DIAG
@@ -1259,20 +1289,21 @@ void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W
     half_t* c8 = reinterpret_cast<half_t*>(ctx8);
     if (epi == EPI_LNF_F16)
       hipLaunchKernelGGL((qkv_attn_kernel<true, 0, true>), grid, block, 0, stream, X, lda, W, bias,
-                         lf->colsum, lf->mr, mask, c8, (int)M, d, heads, scale_log2, hg);
+                         lf->colsum, lf->mr, mask, c8, (int)M, d, heads, scale_log2, hg, stamps);
     else
       hipLaunchKernelGGL((qkv_attn_kernel<false, 0, true>), grid, block, 0, stream, X, lda, W, bias,
-                         nullptr, nullptr, mask, c8, (int)M, d, heads, scale_log2, hg);
+                         nullptr, nullptr, mask, c8, (int)M, d, heads, scale_log2, hg, stamps);
   } else
 #else
-  SR_CHECK(!ctx8, "qkv_attention: the e4m3 ctx output (fp8 mode 5) is in the diagnostic library only");
+  SR_CHECK(!ctx8 && !stamps, "qkv_attention: the e4m3 ctx output (fp8 mode 5) and the stamps are in the "
+                             "diagnostic library only");
 #endif
   if (epi == EPI_LNF_F16)
     hipLaunchKernelGGL(qkv_attn_kernel<true>, grid, block, 0, stream, X, lda, W, bias, lf->colsum,
-                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg);
+                       lf->mr, mask, ctx, (int)M, d, heads, scale_log2, hg, stamps);
   else
     hipLaunchKernelGGL(qkv_attn_kernel<false>, grid, block, 0, stream, X, lda, W, bias, nullptr,
-                       nullptr, mask, ctx, (int)M, d, heads, scale_log2, hg);
+                       nullptr, mask, ctx, (int)M, d, heads, scale_log2, hg, stamps);
   SR_LAUNCH_CHECK();
 }
 

@@ -111,7 +111,8 @@ void launch_cosine_scan_gemm(const half_t* corpus, int64_t ldc, const uint8_t* l
 bool qkv_attention_supported(int S, int d, int heads);
 void launch_qkv_attention(int epi, const half_t* X, int64_t lda, const half_t* W, const float* bias,
                           const LnFold* lf, const int32_t* mask, half_t* ctx, int B, int S, int d,
-                          int heads, hipStream_t stream, uint8_t* ctx8 = nullptr);
+                          int heads, hipStream_t stream, uint8_t* ctx8 = nullptr,
+                          uint64_t* stamps = nullptr);
 void launch_attention(const half_t* qkv, const int32_t* mask, half_t* ctx, int B, int S, int Sq,
                       int d, int heads, hipStream_t stream);
 void attention_force_variant(int v);  // test hook: -1 auto, 0 = 64-key-tile kernel, 1 = K5b, 2 = K5b with 8 waves

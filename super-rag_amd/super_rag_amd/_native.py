@@ -159,6 +159,9 @@ DIAG_SIGNATURES = {
     "sr_diag_gemm_stats": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                    c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int,
                                    c_void_p]),
+    "sr_diag_qkv_attention_stamps": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                             c_int, c_void_p]),
     "sr_diag_gemm_lnr_stats": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                        c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
                                        c_void_p, c_int, c_void_p]),

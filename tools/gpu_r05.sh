@@ -29,6 +29,7 @@ for P in ${PARTS//,/ }; do
     ffn1) timeout -k 10 300 python -u tools/ffn1_bench.py --diags ${FFN1_DIAGS:-0,2} --rounds 3 > gpurun_out/$TAG/ffn1.log 2>&1 || exit 1
           timeout -k 10 300 python -u tools/ffn1_bench.py --M 1638400 --diags ${FFN1_DIAGS:-0,2} --rounds 3 > gpurun_out/$TAG/ffn1_1638k.log 2>&1 || exit 1 ;;
     stamps) timeout -k 10 300 python -u tools/ffn1_stamps.py > gpurun_out/$TAG/ffn1_stamps.log 2>&1 || exit 1 ;;
+    k5cst) timeout -k 10 300 python -u tools/k5c_stamps.py > gpurun_out/$TAG/k5c_stamps.log 2>&1 || exit 1 ;;
     v5) SUPER_RAG_AMD_LIB=$PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so timeout -k 10 400 python -u bench.py --workload config5 --fp8 5 --steps 10 --warmup 3 --no-extras > gpurun_out/$TAG/bench_c5_fp8m5_diaglib.log 2>&1 || exit 1 ;;
     ab) L=super-rag_amd/super_rag_amd/lib_ab
         timeout -k 10 900 bash tools/ab_bench.sh $TAG ${AB_LIBS:-$L/libsrmi_base.so $L/libsrmi_cstl.so $L/libsrmi_rpf.so} > gpurun_out/$TAG/ab.log 2>&1 || exit 1 ;;
