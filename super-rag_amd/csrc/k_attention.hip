@@ -784,6 +784,10 @@ void attention512_kernel(const half_t* __restrict__ qkv, const int32_t* __restri
 // 32 queries each).  The QKV activation never touches HBM: per token 4.6 KB of writes and reads
 // disappear.  Numerics equal the unfused pair bit for bit (same MFMA order per accumulator, same
 // epilogue FMAs, same fp16 rounding, same attention code order).
+#ifndef SR_QA_K1_EARLY
+#define SR_QA_K1_EARLY 0  // K5c: the next tile's K-step 1 staged mid-attention (once every wave holds
+                          // its Q / K fragments, into the dead Q / K images) instead of after it
+#endif
 constexpr int QA_BM = 256;              // tokens per panel
 constexpr int QA_BN = 192;              // Q_h, K_h, V_h rows of W
 constexpr int QA_STAGE = (QA_BM + QA_BN) * 64;  // halfs per K-step buffer (56 KiB)
@@ -1033,12 +1037,12 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     const int sq = wave >> 2, qw = (wave & 3) * 32;
     // (a panel may hold one sequence; DIAG 2 skips the attention)
     const bool attend = DIAG != 2 && m0 + QA_BM / 2 * (sq + 1) <= M;
+    // the scores S^T = K Q^T of the wave's two 16-query tiles (Q, K fragments from the images)
+    float4v sc[2][8];
     if (attend) {
       const half_t* Qs = Qi + sq * 128 * DH;
       const half_t* Ks = Ki + sq * 128 * DH;
-      const half_t* Vs = Vi + sq * 128 * DH;
-      const float* kb = kbias + sq * 128;
-      half8 qf[2][2];
+      half8 qf[2][2], kf[8][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = qw + 16 * u + (lane & 15);
@@ -1046,6 +1050,33 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         for (int s2 = 0; s2 < 2; ++s2)
           qf[u][s2] = *reinterpret_cast<const half8*>(Qs + r * DH + a2_kswz(r, g + 4 * s2) * 8);
       }
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        const int kr = 16 * kt + (lane & 15);
+        kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
+        kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt) {
+          float4v a = {0.f, 0.f, 0.f, 0.f};
+          a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
+          sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
+        }
+    }
+    if constexpr (SR_QA_K1_EARLY) {
+      // every wave has read its Q / K fragments: the Q / K images (PA = their first 56 KiB; V lies
+      // past them) take the next tile's K-step 1 while the softmax and P.V run
+      SR_WAITCNT(63, 0);  // lgkmcnt(0): the fragment reads have returned
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      if (more && grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (attend) {
+      const half_t* Vs = Vi + sq * 128 * DH;
+      const float* kb = kbias + sq * 128;
       float4v o[2][4], lsum[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -1054,25 +1085,9 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
         for (int tt = 0; tt < 4; ++tt) o[u][tt] = float4v{0.f, 0.f, 0.f, 0.f};
       }
       {
-        // software-pipelined per 16-query tile u: the MFMAs of tile 1's scores run while tile 0's
-        // softmax VALU issues, tile 0's P.V while tile 1's softmax issues (two waves per SIMD in the
-        // same phase have no partner work to overlap otherwise).  Per-value operation order is K5b's.
-        half8 kf[8][2];
-#pragma unroll
-        for (int kt = 0; kt < 8; ++kt) {
-          const int kr = 16 * kt + (lane & 15);
-          kf[kt][0] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g) * 8);
-          kf[kt][1] = *reinterpret_cast<const half8*>(Ks + kr * DH + a2_kswz(kr, g + 4) * 8);
-        }
-        float4v sc[2][8];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int kt = 0; kt < 8; ++kt) {
-            float4v a = {0.f, 0.f, 0.f, 0.f};
-            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
-            sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
-          }
+        // software-pipelined per 16-query tile u: tile 0's P.V while tile 1's softmax issues (two
+        // waves per SIMD in the same phase have no partner work to overlap otherwise).  Per-value
+        // operation order is K5b's.
         // V^T fragments of the four 32-key chunks (key order 32c + 4g + j, then 32c + 16 + 4g + j)
         const int q4 = (lane >> 2) & 3, pp = lane & 3;
         half8 va[4][4];
@@ -1152,8 +1167,10 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     if (!more) break;
     // every wave is done with the images: the next tile's K-step 1 goes into PA; K-step 0 (group 0,
     // older than this wave's 4 ctx stores) must have landed before the barrier
-    __syncthreads();
-    if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
+    if constexpr (!SR_QA_K1_EARLY) {
+      __syncthreads();
+      if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
+    }
     if (grp == 0) {
       if (attend)
         SR_WAITCNT(4, 15);
