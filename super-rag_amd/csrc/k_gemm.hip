@@ -397,6 +397,27 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
 // from mr (launch_ln_stats_finalize of the producer's partials).  The *_STATS epilogues write the
 // Chan partials of their own fp16-rounded outputs: per 128-column wave span the sum over the 4
 // lane groups (xor-shuffles 16 / 32), then M2 around that span's mean.
+// The pivot of a row's 128-value span (stats mode 2): sq = sum (x - c)^2 is taken with x - c
+// rounded to fp16, exact when x is within a factor 2 of c (Sterbenz) and, for c = 0, always.  So
+// c = the span's first value when the row sits far from zero -- its values 2, 4, 6 (lane m & 15's
+// column group 0) all within |c| / 2 of it, which every row with mean > ~16 std passes -- and c = 0
+// otherwise, where sq - sum^2 / 128 loses only (mean / std)^2 x 2^-24 of M2 to cancellation.  (c =
+// the first value always: up to ~3e-3 of M2 lost on centred rows; c = 0 always: every digit on rows
+// with mean >> std)  v: the lane's column group 0 (8 consecutive values of its row).
+// TEST = false: c = the first value always (the e4m3-copy LNR epilogue, fp8 mode 3's
+// O-projection: the test's registers spilled it 8 -> 32 B).
+template <bool TEST = true>
+__device__ __forceinline__ _Float16 span_pivot(const half8& v, int lane) {
+  bool far = true;
+  if constexpr (TEST) {
+    const float c = (float)v[0], tol = 0.5f * fabsf(c);
+#pragma unroll
+    for (int k = 2; k < 8; k += 2) far = far && fabsf((float)v[k] - c) <= tol;
+  }
+  const unsigned short cl = far ? __builtin_bit_cast(unsigned short, v[0]) : (unsigned short)0;
+  return __builtin_bit_cast(_Float16, (unsigned short)__shfl(cl, lane & 15, 64));
+}
+
 // pre(): called once the epilogue's constant loads (bias, column sums / LayerNorm weight, row
 // statistics) are issued: the persistent kernel stages the next tile's first K-steps there, so
 // those loads are older than the staging pieces and their wait (vmcnt counts in order) does not
@@ -761,19 +782,16 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         // one pass: sum and sum of squares of the fp16 values (1: fp32 add + fma per value, 2:
         // v_dot2c_f32_f16 per value pair -- the products of fp16 values are exact in fp32), then
         // M2 = sq - sum^2 / 128 per 128-column span.
-        // Mode 2 takes the squares around a PIVOT c, the row's first value in the span (lane
-        // m & 15's hv[0][0], shared by a shuffle): sq = sum (x - c)^2 with x - c in fp16 (exact by
-        // Sterbenz whenever x is within a factor 2 of c, i.e. exactly in the large-offset rows
-        // where sq - sum^2 / 128 would cancel; else rounded to 2^-11 of |x - c|), the sum stays
-        // the exact sum of x, and M2 = sq - (sum - 128 c)^2 / 128 (rows with mean >>
-        // std lost every digit of M2 to the cancellation; tests/test_gpu_gemm.py
-        // test_stats_epilogue_large_offset_rows)
+        // Mode 2 also takes the squares around a PIVOT c, the row's first value in the span (lane
+        // m & 15's hv[0][0], shared by a shuffle), and span_m2 picks the plain or the pivoted M2
+        // by the span's mean / std (rows with mean >> std lost every digit of M2 to
+        // the cancellation; tests/test_gpu_gemm.py test_stats_epilogue_large_offset_rows and
+        // test_lnr_stats_epilogue_persistent_ragged)
         float sq = 0.f;
         typedef _Float16 h2v __attribute__((ext_vector_type(2)));
         h2v c2 = {(_Float16)0.f, (_Float16)0.f};
         if constexpr (SR_GEMM_STATS_MODE == 2) {
-          const _Float16 c = __builtin_bit_cast(
-              _Float16, (unsigned short)__shfl(__builtin_bit_cast(unsigned short, hv[0][0]), lane & 15, 64));
+          const _Float16 c = span_pivot<!(Y8 && LNR)>(hv[0], lane);
           c2 = h2v{c, c};
         }
 #pragma unroll
@@ -1232,12 +1250,11 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
       for (int r = 0; r < 8; ++r) hv[pp][r] = (half_t)v[r];
       *reinterpret_cast<half8*>(sb + (wofs ^ (uint32_t)(pp << 6))) = hv[pp];
     }
-    // statistics: pivot = the row's first value in the wave's 128-column span (column group 0,
-    // lane m & 15), sums over the column groups in order 0..3 (store_tile_wide's order)
+    // statistics: the span's pivot (span_pivot of column group 0's first values), sums over the
+    // column groups in order 0..3 (store_tile_wide's order)
     typedef _Float16 h2v __attribute__((ext_vector_type(2)));
     if (h == 0) {
-      piv[j] = __builtin_bit_cast(_Float16, (unsigned short)__shfl(__builtin_bit_cast(unsigned short, hv[0][0]),
-                                                                    lane & 15, 64));
+      piv[j] = span_pivot(hv[0], lane);
       ssum[j] = 0.f;
       ssq[j] = 0.f;
     }

@@ -146,7 +146,7 @@ def test_stats_epilogue_large_offset_rows(offset, M):
     rel = np.abs(s[..., 1] - m2) / m2
     ratio = np.abs(mean) / np.sqrt(m2 / 128)
     print(f"offset {offset}: max |mean|/std {ratio.max():.0f}, max rel M2 err {rel.max():.2e}")
-    assert rel.max() <= 2e-3, rel.max()
+    assert rel.max() <= (2e-4 if offset == 0.0 else 2e-3), rel.max()
 
 
 @pytest.mark.parametrize("M,K", [(256 * 200 + 77, 768), (256 * 176, 3072), (1000, 768)])
@@ -188,4 +188,6 @@ def test_lnr_stats_epilogue_persistent_ragged(M, K):
     s = st.double().cpu().numpy()
     m2 = ((y - y.mean(-1, keepdims=True)) ** 2).sum(-1)
     np.testing.assert_allclose(s[..., 0], y.sum(-1), rtol=1e-6, atol=1e-3)
-    assert (np.abs(s[..., 1] - m2) <= 2e-3 * m2 + 1e-4).all()
+    rel = np.abs(s[..., 1] - m2) / m2
+    print(f"M = {M}, K = {K}: max |dY| {err:.2e}, max rel M2 err {rel.max():.2e}")
+    assert rel.max() <= 2e-4, rel.max()
