@@ -784,6 +784,10 @@ void attention512_kernel(const half_t* __restrict__ qkv, const int32_t* __restri
 // 32 queries each).  The QKV activation never touches HBM: per token 4.6 KB of writes and reads
 // disappear.  Numerics equal the unfused pair bit for bit (same MFMA order per accumulator, same
 // epilogue FMAs, same fp16 rounding, same attention code order).
+#ifndef SR_QA_CSTL
+#define SR_QA_CSTL 0  // K5c: the next tile's epilogue constants (bias / column sums of its head, row
+                      // statistics and key mask of its panel) staged into LDS with its K-step 0
+#endif
 #ifndef SR_QA_K1_EARLY
 #define SR_QA_K1_EARLY 0  // K5c: the next tile's K-step 1 staged mid-attention (once every wave holds
                           // its Q / K fragments, into the dead Q / K images) instead of after it
@@ -836,10 +840,15 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
   // LDS: the images, then one K-step buffer (PB) past them; odd K-steps use PA = the first 56 KiB
   // of the image area (dead during the K-loop).  So the next tile's K-step 0 (PB) is staged while
   // this tile's attention reads the images, and its K-step 1 (PA) right after.
-  __shared__ __attribute__((aligned(16))) half_t lds[IMG + QA_STAGE];
+  // CSTL: past PB, the tile's epilogue constants (floats): [3 x 64 bias][3 x 64 column sums]
+  // [256 x (mu, rstd)][256 key mask (int)] = 4.5 KiB
+  constexpr int QA_CSTH = SR_QA_CSTL ? 2304 : 0;
+  __shared__ __attribute__((aligned(16))) half_t lds[IMG + QA_STAGE + QA_CSTH];
   __shared__ float kbias[QA_BM];
   half_t* const PA = lds;
   half_t* const PB = lds + IMG;
+  float* const qcst = reinterpret_cast<float*>(lds + IMG + QA_STAGE);
+  (void)qcst;
   // persistent walkers: tile t = (panel, head), head fastest; every XCD walks a contiguous range
   // of tiles so the 12 heads of a panel share its X rows in that XCD's L2 (W stays L2-resident)
   const int panels = (M + QA_BM - 1) / QA_BM, nwg = panels * heads;
@@ -897,12 +906,45 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 #endif
   };
 
+  // CSTL: group 0's waves stage a tile's constants beside its K-step 0 (older than their ctx
+  // stores, so the transition's wait covers them): wave 0 the bias of the head's Q / K / V rows
+  // (3 x 256 B), wave 1 their column sums, wave 2 the panel's row statistics (2 x 1 KiB), wave 3 its
+  // key mask (1 KiB); rows past M read as zero (masked keys, never stored)
+  auto stage_cst = [&](int mm, int hh) __attribute__((always_inline)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (SR_QA_CSTL) {
+      const uint32_t l4 = (uint32_t)lane * 4u, l16 = l4 * 4u;
+      const int nrow = __builtin_amdgcn_readfirstlane(max(0, min(QA_BM, M - mm)));
+      if (w4 < 2) {
+        const float* src = w4 == 0 ? bias : colsum;
+        if (w4 == 0 || LNF) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const auto r = panel_rsrc(reinterpret_cast<const half_t*>(src + (int64_t)q * d + hh * DH), 256);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(qcst + 192 * w4 + 64 * q), 4, l4, 0, 0, 0);
+          }
+        }
+      } else if (w4 == 2) {
+        if (LNF) {
+          const auto r = panel_rsrc(reinterpret_cast<const half_t*>(mr + (int64_t)mm * 2), (int64_t)nrow * 8);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(qcst + 384), 16, l16, 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(qcst + 640), 16, l16, 1024, 0, 0);
+        }
+      } else {
+        const auto r = panel_rsrc(reinterpret_cast<const half_t*>(mask + mm), (int64_t)nrow * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SR_LDS(qcst + 896), 16, l16, 0, 0, 0);
+      }
+    }
+#endif
+  };
+
   float4v acc[6][4];
   half8 aX[3], aY[3], bX[4], bY[4];
 
   // first tile: group 0 stages K-step 0 (PB) and waits for it, group 1 K-step 1 (PA)
   if (grp == 0) {
     stage(0, PB, m0, h);
+    stage_cst(m0, h);
     SR_WAITCNT(0, 15);
   } else if (nk > 1) {
     stage(1, PA, m0, h);
@@ -987,7 +1029,8 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     // (every thread loads -- threads past QA_BM repeat a row -- so no branch merges the value
     // and the load stays in flight until its use)
     const int m_mk = m0 + (tid & (QA_BM - 1));
-    const int mkv = mask[m_mk < M ? m_mk : M - 1];
+    const int mkv = SR_QA_CSTL ? reinterpret_cast<const int*>(qcst + 896)[tid & (QA_BM - 1)]
+                               : mask[m_mk < M ? m_mk : M - 1];
     // column-group outer: the bias / column sums of a group are loaded once (not once per row
     // group), and its LDS image address is one per lane -- the swizzles depend on the row only
     // through (row >> 1) & 7, which a row group's 16 j does not change -- with the row groups at
@@ -998,7 +1041,10 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     for (int j = 0; j < 4; ++j) {
       const int ml = wm * 64 + 16 * j + (lane & 15);
       const int mg = m0 + ml < M ? m0 + ml : M - 1;
-      mrj[j] = LNF ? *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2) : make_float2(0.f, 1.f);
+      if constexpr (SR_QA_CSTL)
+        mrj[j] = LNF ? reinterpret_cast<const float2*>(qcst + 384)[ml] : make_float2(0.f, 1.f);
+      else
+        mrj[j] = LNF ? *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2) : make_float2(0.f, 1.f);
     }
     const int ml0 = wm * 64 + (lane & 15);
 #pragma unroll
@@ -1006,9 +1052,12 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
       const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
       const int seg = n >> 6, dim = n & 63;
       const int col = seg * d + h * DH + dim;
-      const float4v b = *reinterpret_cast<const float4v*>(bias + col);
+      const float4v b = SR_QA_CSTL ? *reinterpret_cast<const float4v*>(qcst + seg * 64 + dim)
+                                   : *reinterpret_cast<const float4v*>(bias + col);
       float4v c = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (LNF) c = *reinterpret_cast<const float4v*>(colsum + col);
+      if constexpr (LNF)
+        c = SR_QA_CSTL ? *reinterpret_cast<const float4v*>(qcst + 192 + seg * 64 + dim)
+                       : *reinterpret_cast<const float4v*>(colsum + col);
       half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
       const int chunk = seg == 2 ? a2_vswz(ml0, dim >> 3) : a2_kswz(ml0, dim >> 3);
       half_t* const wp = img + ml0 * DH + chunk * 8 + (dim & 7);
@@ -1031,7 +1080,10 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     const int t_next = t + t_step;
     const bool more = t_next < t_end;
     const int h_n = tile_h(t_next), m0_n = tile_m(t_next);
-    if (more && grp == 0) stage(0, PB, m0_n, h_n);  // the next tile's K-step 0 lands during attention
+    if (more && grp == 0) {  // the next tile's K-step 0 (and constants) land during attention
+      stage(0, PB, m0_n, h_n);
+      stage_cst(m0_n, h_n);
+    }
 
     // ---- attention: waves 4s .. 4s+3 own sequence s of the panel, 32 queries each ----
     const int sq = wave >> 2, qw = (wave & 3) * 32;

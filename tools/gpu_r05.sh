@@ -44,13 +44,14 @@ for P in ${PARTS//,/ }; do
     var) L=$PWD/super-rag_amd/super_rag_amd/lib_ab; V=${VAR:?VAR}
          SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so timeout -k 10 400 \
            python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_ffn1_epilogue.py tests/test_gpu_encoder.py \
-           tests/test_gpu_rerank_fidelity.py tests/test_gpu_rerank_fidelity_v2m3.py tests/test_gpu_configs.py -x -q \
+           tests/test_gpu_rerank_fidelity.py tests/test_gpu_rerank_fidelity_v2m3.py tests/test_gpu_configs.py \
+           tests/test_gpu_fused_attention.py -x -q \
            --timeout 240 --timeout-method thread > gpurun_out/$TAG/var_tests_$V.log 2>&1 || exit 1
-         for r in 1 2; do for D in $PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so $L/libsrmi_diag_$V.so; do
+         [ "${VAR_FFN1:-1}" = 1 ] && for r in 1 2; do for D in $PWD/super-rag_amd/super_rag_amd/lib/libsrmi_diag.so $L/libsrmi_diag_$V.so; do
            echo "== $(basename $D) r$r" >> gpurun_out/$TAG/var_ffn1_$V.log
            SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 300 python -u tools/ffn1_bench.py --diags 0,2 --rounds 2 $VAR_FFN1_ARGS \
              >> gpurun_out/$TAG/var_ffn1_$V.log 2>&1 || exit 1
-         done; done ;;
+         done; done; true ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
