@@ -785,11 +785,13 @@ void attention512_kernel(const half_t* __restrict__ qkv, const int32_t* __restri
 // disappear.  Numerics equal the unfused pair bit for bit (same MFMA order per accumulator, same
 // epilogue FMAs, same fp16 rounding, same attention code order).
 #ifndef SR_QA_CSTL
-#define SR_QA_CSTL 0  // K5c: the next tile's epilogue constants (bias / column sums of its head, row
+#define SR_QA_CSTL 1  // K5c: the next tile's epilogue constants (bias / column sums of its head, row
                       // statistics and key mask of its panel) staged into LDS with its K-step 0
+                      // (K5c 1,021-1,025 -> 1,028 TF/s; 138 parity tests on it, profiles/r05_k5c_cstl/)
 #endif
 #ifndef SR_QA_K1_EARLY
-#define SR_QA_K1_EARLY 0  // K5c: the next tile's K-step 1 staged mid-attention (once every wave holds
+#define SR_QA_K1_EARLY 0  // K5c: the next tile's K-step 1 staged mid-attention (+0.3 % K5c alone,
+                          // 24 B of spills beside CSTL: off; profiles/r05_k5c_cstl/) (once every wave holds
                           // its Q / K fragments, into the dead Q / K images) instead of after it
 #endif
 constexpr int QA_BM = 256;              // tokens per panel
