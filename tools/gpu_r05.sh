@@ -52,6 +52,8 @@ for P in ${PARTS//,/ }; do
            SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 300 python -u tools/ffn1_bench.py --diags 0,2 --rounds 2 $VAR_FFN1_ARGS \
              >> gpurun_out/$TAG/var_ffn1_$V.log 2>&1 || exit 1
          done; done; true ;;
+    gloo2) timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 2 --no-extras \
+             --no-cpu-baseline > gpurun_out/$TAG/bench_2rank_gloo.log 2>&1 || exit 1 ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
