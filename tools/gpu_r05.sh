@@ -54,6 +54,10 @@ for P in ${PARTS//,/ }; do
          done; done; true ;;
     gloo2) timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 2 --no-extras \
              --no-cpu-baseline > gpurun_out/$TAG/bench_2rank_gloo.log 2>&1 || exit 1 ;;
+    dprof) timeout -k 10 400 python -u tools/bench_dropin.py --profile --profile-concurrency 64 --seconds 10 \
+             > gpurun_out/$TAG/dropin_profile_c64.txt 2>&1 || exit 1
+           timeout -k 10 400 python -u tools/bench_dropin.py --profile --profile-concurrency 1 --seconds 10 \
+             > gpurun_out/$TAG/dropin_profile_c1.txt 2>&1 || exit 1 ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
