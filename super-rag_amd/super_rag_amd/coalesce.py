@@ -8,23 +8,54 @@ that arrive while a batch is running queue up and the next batch takes all of th
 ``max_batch``).  Leadership is handed to the first queued caller when a batch ends, so no caller
 keeps serving other callers' requests after its own result is ready.  Results are per item and
 identical to running the items one by one (the batched kernels are row-independent).
+
+``acall`` is the same queue for coroutines: a waiting coroutine holds no thread (its slot carries
+an asyncio future, completed with one ``call_soon_threadsafe`` per event loop per batch), and a
+coroutine that finds the device idle runs the batches in one worker thread, which keeps leading
+while the next queued slot is a coroutine's.  With one worker thread blocked per waiting request
+(``asyncio.to_thread`` around ``__call__``), every finished batch woke its ~30 callers' threads,
+which then contended for the interpreter lock.
 """
 from __future__ import annotations
 
+import asyncio
+import logging
 import threading
 from typing import Any, Callable, List, Sequence
 
 
-class _Slot:
-    __slots__ = ("item", "result", "error", "done", "lead", "event")
+logger = logging.getLogger(__name__)
 
-    def __init__(self, item):
+
+class _Slot:
+    __slots__ = ("item", "result", "error", "done", "lead", "event", "loop", "fut")
+
+    def __init__(self, item, loop=None):
         self.item = item
         self.result = None
         self.error = None
         self.done = False
         self.lead = False
-        self.event = threading.Event()
+        self.loop = loop                                   # acall: the caller's event loop
+        self.fut = loop.create_future() if loop is not None else None
+        self.event = threading.Event() if loop is None else None
+
+
+def _report(runner) -> None:
+    """A batch's own failure reaches its callers; anything escaping _lead itself is a bug."""
+    if not runner.cancelled() and runner.exception() is not None:
+        logger.error("coalescer leader failed: %r", runner.exception())
+
+
+def _finish(slots) -> None:
+    """(in the slots' event loop) complete the futures of one batch's coroutine slots."""
+    for s in slots:
+        if s.fut.done():  # cancelled by its caller
+            continue
+        if s.error is not None:
+            s.fut.set_exception(s.error)
+        else:
+            s.fut.set_result(s.result)
 
 
 class Coalescer:
@@ -53,7 +84,29 @@ class Coalescer:
             raise slot.error
         return slot.result
 
+    async def acall(self, item):
+        """``__call__`` for a coroutine: same batches, same per-item results, no thread held while
+        the item waits for its batch."""
+        slot = _Slot(item, asyncio.get_running_loop())
+        lead = False
+        with self._lock:
+            self._queue.append(slot)
+            if not self._busy:
+                self._busy = True
+                lead = True
+        if lead:
+            # not awaited: the worker may go on to later coroutines' batches after this one's
+            runner = slot.loop.run_in_executor(None, self._lead)
+            runner.add_done_callback(_report)
+        return await slot.fut
+
     def _lead(self) -> None:
+        """Run batches while the queue's next slot is a coroutine's (it has no thread of its own
+        to lead with); hand over to a queued thread caller, or go idle."""
+        while self._lead_one():
+            pass
+
+    def _lead_one(self) -> bool:
         with self._lock:
             batch = self._queue[: self.max_batch]
             del self._queue[: self.max_batch]
@@ -71,13 +124,28 @@ class Coalescer:
             self.batches += 1
             self.items += len(batch)
             nxt = None
+            keep = False
             if self._queue:
                 nxt = self._queue[0]
-                nxt.lead = True
+                if nxt.fut is None:
+                    nxt.lead = True
+                else:
+                    keep = True  # a coroutine's slot: this thread runs the next batch too
+                    nxt = None
             else:
                 self._busy = False
+        by_loop = {}
         for s in batch:
             s.done = True
-            s.event.set()
+            if s.fut is None:
+                s.event.set()
+            else:
+                by_loop.setdefault(s.loop, []).append(s)
+        for loop, slots in by_loop.items():
+            try:
+                loop.call_soon_threadsafe(_finish, slots)
+            except RuntimeError:  # the caller's loop has closed: nobody awaits these
+                pass
         if nxt is not None:
             nxt.event.set()
+        return keep

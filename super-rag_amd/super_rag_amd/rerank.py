@@ -47,6 +47,9 @@ class RerankService:
         (GIL contention; 210.7 vs 228.1 q/s, profiles/r03_dropin/)."""
         if not self.coalesce:
             return self._score_many(self.encoder, self.tokenizer, self.device_batch, [(query, texts)])[0]
+        return self._pair_coalescer()((query, list(texts)))
+
+    def _pair_coalescer(self):
         coal = getattr(self.encoder, "_pair_coalescer", None)
         if coal is None:
             from .coalesce import Coalescer
@@ -54,7 +57,7 @@ class RerankService:
             coal = Coalescer(lambda items: RerankService._score_many(enc, tok, dev_b, items),
                              max_batch=max(1, dev_b // 100))
             setattr(self.encoder, "_pair_coalescer", coal)
-        return coal((query, list(texts)))
+        return coal
 
     @staticmethod
     def _score_many(encoder, tokenizer, device_batch: int, items) -> List[np.ndarray]:
@@ -127,7 +130,10 @@ class RerankService:
 
     async def _rank_texts(self, query: str, texts: List[str]) -> List[int]:
         try:
-            logits = await asyncio.to_thread(self.score, query, texts)
+            if self.coalesce:  # awaits its shared batch without holding a thread (coalesce.acall)
+                logits = await self._pair_coalescer().acall((query, list(texts)))
+            else:
+                logits = await asyncio.to_thread(self.score, query, texts)
         except Exception as e:  # noqa: BLE001
             raise RerankError(f"Internal rerank operation failed: {e}",
                               {"provider": self.rerank_provider, "model": self.model,

@@ -194,3 +194,55 @@ def test_devices_gate_takes_every_shard_device_in_order():
     after = gate_busy()
     for d in (1, 2, 3):
         assert after[d]["search"][1] == before.get(d, {}).get("search", (0, 0))[1] + 1
+
+
+def test_coalescer_acall_batches_coroutines_without_threads_and_mixes_with_threads():
+    """Coalescer.acall: concurrent coroutines share batches, each gets its own item's result,
+    a failing batch raises in every coroutine of it, and thread callers on the same queue still
+    get theirs (a coroutine's slot is led by the worker thread, a thread caller's by itself)."""
+    import asyncio
+    from super_rag_amd.coalesce import Coalescer
+    sizes = []
+    gate = threading.Event()
+
+    def run(items):
+        sizes.append(len(items))
+        gate.wait(0.02)
+        if any(i == -1 for i in items):
+            raise ValueError("bad item")
+        return [i * i for i in items]
+
+    c = Coalescer(run, max_batch=16)
+
+    async def many(n):
+        return await asyncio.gather(*[c.acall(i) for i in range(n)])
+
+    got = asyncio.run(many(200))
+    assert got == [i * i for i in range(200)]
+    assert max(sizes) > 1 and sum(sizes) == 200 and c.items == 200
+
+    async def failing():
+        return await asyncio.gather(c.acall(3), c.acall(-1), return_exceptions=True)
+
+    res = asyncio.run(failing())
+    assert any(isinstance(r, ValueError) for r in res)
+
+    # threads and coroutines on one queue
+    out_threads = {}
+
+    def thread_caller(i):
+        out_threads[i] = c(i)
+
+    async def mixed():
+        ts = [threading.Thread(target=thread_caller, args=(1000 + i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        vals = await asyncio.gather(*[c.acall(i) for i in range(64)])
+        for t in ts:
+            t.join(timeout=30)
+            assert not t.is_alive()
+        return vals
+
+    vals = asyncio.run(mixed())
+    assert vals == [i * i for i in range(64)]
+    assert out_threads == {1000 + i: (1000 + i) ** 2 for i in range(8)}

@@ -58,6 +58,8 @@ for P in ${PARTS//,/ }; do
              > gpurun_out/$TAG/dropin_profile_c64.txt 2>&1 || exit 1
            timeout -k 10 400 python -u tools/bench_dropin.py --profile --profile-concurrency 1 --seconds 10 \
              > gpurun_out/$TAG/dropin_profile_c1.txt 2>&1 || exit 1 ;;
+    d1) timeout -k 10 400 python -u tools/bench_dropin.py --concurrency 64 256 --seconds 10 \
+          > gpurun_out/$TAG/dropin_1proc.json 2> gpurun_out/$TAG/dropin_1proc.err || exit 1 ;;
     ffn1t) timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn1_epilogue.py -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/ffn1_tests.log 2>&1 || exit 1 ;;
     *) echo "unknown part $P"; exit 2 ;;
   esac
