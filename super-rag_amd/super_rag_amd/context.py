@@ -17,11 +17,26 @@ class ContextManager:
     def query(self, query, score_threshold=0.5, topk=3, vector=None, index_types=None, chat_id=None):
         if vector is None:
             vector = self.embedding_model.embed_query(query)
+        query_embedding, kw = self._search_args(query, score_threshold, topk, vector, index_types, chat_id)
+        return self.adaptor.connector.search(query_embedding, **kw).results
+
+    async def aquery(self, query, score_threshold=0.5, topk=3, vector=None, index_types=None,
+                     chat_id=None):
+        """query for a coroutine (the connector's asearch: a coalesced search holds no thread)."""
+        if vector is None:
+            vector = await self.embedding_model.aembed_query(query)
+        query_embedding, kw = self._search_args(query, score_threshold, topk, vector, index_types, chat_id)
+        conn = self.adaptor.connector
+        if hasattr(conn, "asearch"):
+            return (await conn.asearch(query_embedding, **kw)).results
+        import asyncio
+        return (await asyncio.to_thread(conn.search, query_embedding, **kw)).results
+
+    def _search_args(self, query, score_threshold, topk, vector, index_types, chat_id):
         filter_condition = self._create_combined_filter(index_types, chat_id)
         query_embedding = QueryWithEmbedding(query=query, top_k=topk, embedding=vector)
         # Same kwargs as context.py:37-47; the store ignores all but top_k, as SeekDB's did.
-        results = self.adaptor.connector.search(
-            query_embedding,
+        return query_embedding, dict(
             collection_name=self.collection_name,
             query_vector=query_embedding.embedding,
             with_vectors=True,
@@ -31,7 +46,6 @@ class ContextManager:
             score_threshold=score_threshold,
             filter=filter_condition,
         )
-        return results.results
 
     def _create_combined_filter(self, index_types: Optional[List[str]] = None,
                                 chat_id: Optional[str] = None) -> Optional[Any]:

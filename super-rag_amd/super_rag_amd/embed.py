@@ -90,6 +90,15 @@ class EmbeddingService:
             return self.embed_documents([content])[0]
         # concurrent single-query calls (one per search request, embedding_service.py:114) are
         # coalesced into one device batch per encoder (coalesce.py); results are per query
+        try:
+            return self._query_coalescer()(content.replace("\n", " ")).tolist()
+        except BatchProcessingError:
+            raise
+        except Exception as e:  # noqa: BLE001
+            raise EmbeddingError(f"Embedding API error: {e}",
+                                 {"provider": self.embedding_provider, "model": self.model}) from e
+
+    def _query_coalescer(self):
         coal = getattr(self.encoder, "_query_coalescer", None)
         if coal is None:
             from .coalesce import Coalescer
@@ -99,16 +108,22 @@ class EmbeddingService:
                 return list(EmbeddingService._embed_with(enc, tok, dev_b, texts))
             coal = Coalescer(run, max_batch=self.device_batch)
             setattr(self.encoder, "_query_coalescer", coal)
+        return coal
+
+    async def aembed_query(self, content: str) -> List[float]:
+        """embed_query for a coroutine: the coalesced query awaits its batch without holding a
+        worker thread (coalesce.Coalescer.acall); same result and errors."""
+        if not self.coalesce:
+            return await asyncio.to_thread(self.embed_query, content)
+        if not content or not content.strip():
+            raise EmptyTextError(1)
         try:
-            return coal(content.replace("\n", " ")).tolist()
+            return (await self._query_coalescer().acall(content.replace("\n", " "))).tolist()
         except BatchProcessingError:
             raise
         except Exception as e:  # noqa: BLE001
             raise EmbeddingError(f"Embedding API error: {e}",
                                  {"provider": self.embedding_provider, "model": self.model}) from e
-
-    async def aembed_query(self, content: str) -> List[float]:
-        return await asyncio.to_thread(self.embed_query, content)
 
     def is_multimodal(self) -> bool:
         return self.multimodal

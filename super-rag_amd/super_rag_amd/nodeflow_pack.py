@@ -203,14 +203,13 @@ class VectorSearchService:
             ctx["collection"] = name
             cm = ContextManager(name, embedding_model, VECTOR_DB_TYPE, ctx)
 
-            def embed_and_query():
-                vector = embedding_model.embed_query(query)
-                return cm.query(query, score_threshold=similarity_threshold, topk=top_k,
-                                vector=vector, index_types=["vector"], chat_id=chat_id)
             # The reference runs these synchronously on the event loop (vector_search.py:76-86);
-            # a worker thread keeps the loop free and lets concurrent requests coalesce into
-            # device batches (coalesce.py).  Same calls, same results.
-            results = await asyncio.to_thread(embed_and_query)
+            # here the coalesced embed and search await their shared device batches (coalesce.py)
+            # without holding a thread, so the loop stays free and concurrent requests batch.
+            # Same calls, same results.
+            vector = await embedding_model.aembed_query(query)
+            results = await cm.aquery(query, score_threshold=similarity_threshold, topk=top_k,
+                                      vector=vector, index_types=["vector"], chat_id=chat_id)
             for item in results:
                 if item.metadata is None:
                     item.metadata = {}

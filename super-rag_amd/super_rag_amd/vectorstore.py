@@ -22,6 +22,8 @@ re-snapshotted after every add/delete (checkpoint/resume; SeekDB persisted serve
 """
 from __future__ import annotations
 
+import asyncio
+
 import copy
 import json
 from collections import OrderedDict
@@ -407,19 +409,39 @@ class MI355XVectorStoreConnector:
                                results=self._hybrid(c, q, query.query or "", int(query.top_k), flt))
         if self.coalesce:
             # concurrent single-query searches share one device batch (coalesce.py)
-            if c.coalescer is None:
-                with c.lock:
-                    if c.coalescer is None:
-                        from .coalesce import Coalescer
-                        c.coalescer = Coalescer(lambda items, c=c: self._search_batch(c, items),
-                                                max_batch=self.max_batch)
-            results = c.coalescer((q, int(query.top_k), flt))
+            results = self._coalescer(c)((q, int(query.top_k), flt))
         else:
             results = self._search_batch(c, [(q, int(query.top_k), flt)])[0]
-        if thr is not None:
-            # similarity = 1 - distance >= threshold (results are distance-ascending: a prefix)
-            results = [d for d in results if 1.0 - d.score >= float(thr)]
-        return QueryResult(query=query.query, results=results)
+        return QueryResult(query=query.query, results=self._threshold(results, thr))
+
+    async def asearch(self, query, **kwargs):
+        """search for a coroutine: a coalesced dense search awaits its device batch without
+        holding a worker thread (coalesce.Coalescer.acall); hybrid / uncoalesced searches run
+        search in a worker thread.  Same results."""
+        c = _get(self.collection_name)
+        if c is None or query.top_k is None or query.top_k <= 0 or self.hybrid or not self.coalesce:
+            return await asyncio.to_thread(self.search, query, **kwargs)
+        q = np.asarray(query.embedding, dtype=np.float32)
+        flt = kwargs.get("filter") if self.honor_filter else None
+        thr = kwargs.get("score_threshold") if self.honor_score_threshold else None
+        results = await self._coalescer(c).acall((q, int(query.top_k), flt))
+        return QueryResult(query=query.query, results=self._threshold(results, thr))
+
+    def _coalescer(self, c):
+        if c.coalescer is None:
+            with c.lock:
+                if c.coalescer is None:
+                    from .coalesce import Coalescer
+                    c.coalescer = Coalescer(lambda items, c=c: self._search_batch(c, items),
+                                            max_batch=self.max_batch)
+        return c.coalescer
+
+    @staticmethod
+    def _threshold(results, thr):
+        if thr is None:
+            return results
+        # similarity = 1 - distance >= threshold (results are distance-ascending: a prefix)
+        return [d for d in results if 1.0 - d.score >= float(thr)]
 
     @staticmethod
     def _allow_mask(c: _Collection, flt):

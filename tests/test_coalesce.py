@@ -246,3 +246,57 @@ def test_coalescer_acall_batches_coroutines_without_threads_and_mixes_with_threa
     vals = asyncio.run(mixed())
     assert vals == [i * i for i in range(64)]
     assert out_threads == {1000 + i: (1000 + i) ** 2 for i in range(8)}
+
+
+def test_async_paths_equal_the_sync_ones():
+    """The coroutine paths the flow uses -- EmbeddingService.aembed_query, ContextManager.aquery
+    (connector.asearch) and RerankService.async_rerank -- await Coalescer.acall and return what
+    the sync calls return, concurrently, with the empty-query error kept."""
+    import asyncio
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.context import ContextManager
+    from super_rag_amd.embed import EmbeddingService
+    from super_rag_amd.models import TextNode
+    from doubles import RelevanceEncoder
+    from super_rag_amd.rerank import RerankService
+    V.set_store_backend(lambda dim, dev: NumpyStore(dim, dev), NumpyStore.load)
+    V._collections.clear()
+    try:
+        tok = TextTokenizer()
+        enc = HashEncoder(tok, 16)
+        emb = EmbeddingService("openai", "BAAI/bge-m3", "", "", 10, encoder=enc, tokenizer=tok)
+        conn = V.MI355XVectorStoreConnector({"collection": "acoal", "coalesce": True, "max_batch": 16})
+        rng = np.random.default_rng(1)
+        conn.store.add([TextNode(text=f"passage {i} " * int(rng.integers(1, 4)), metadata={"i": i},
+                                 embedding=rng.standard_normal(16).tolist()) for i in range(300)])
+        cm = ContextManager("acoal", emb, "mi355x", {"collection": "acoal", "coalesce": True,
+                                                     "max_batch": 16})
+        rer = RerankService("jina_ai", "BAAI/bge-reranker-v2-m3", "", "", encoder=RelevanceEncoder(tok),
+                            tokenizer=tok, device_batch=256)
+        queries = [f"query {i}" for i in range(48)]
+
+        def sync_one(q):
+            docs = cm.query(q, topk=1 + len(q) % 7, index_types=["vector"])
+            return [(d.text, d.score) for d in docs]
+
+        want = [sync_one(q) for q in queries]
+
+        async def async_one(q):
+            v = await emb.aembed_query(q)
+            docs = await cm.aquery(q, topk=1 + len(q) % 7, vector=v, index_types=["vector"])
+            ranked = await rer.async_rerank(q, docs)
+            return [(d.text, d.score) for d in docs], [d.text for d in ranked]
+
+        async def run_all():
+            return await asyncio.gather(*[async_one(q) for q in queries])
+
+        got = asyncio.run(run_all())
+        assert [g[0] for g in got] == want
+        for q, (docs, ranked) in zip(queries, got):
+            assert sorted(ranked) == sorted(t for t, _ in docs)
+        assert enc._query_coalescer.items == 2 * len(queries)  # sync + async
+        with pytest.raises(Exception):
+            asyncio.run(emb.aembed_query("   "))
+    finally:
+        V._collections.clear()
+        V.set_store_backend(V._native_store, V._native_load)
