@@ -128,10 +128,25 @@ class RerankService:
             raise RerankError(f"Rerank API error: {e}",
                               {"provider": self.rerank_provider, "model": self.model}) from e
 
+    def _encoded_coalescer(self):
+        """Coalescer of already tokenised pairs (the coroutine path): each request tokenises its
+        own pairs on the event loop while the device runs the previous batch, and the batch
+        leader only packs and scores.  (Tokenised by the leader, ~30 requests' pairs took ~55 ms
+        per ~66 ms device batch with the device idle meanwhile, profiles/r05_dropin/.)"""
+        coal = getattr(self.encoder, "_encoded_pair_coalescer", None)
+        if coal is None:
+            from .coalesce import Coalescer
+            enc, dev_b = self.encoder, self.device_batch
+            coal = Coalescer(lambda items: RerankService._score_encoded(enc, dev_b, items),
+                             max_batch=max(1, dev_b // 100))
+            setattr(self.encoder, "_encoded_pair_coalescer", coal)
+        return coal
+
     async def _rank_texts(self, query: str, texts: List[str]) -> List[int]:
         try:
             if self.coalesce:  # awaits its shared batch without holding a thread (coalesce.acall)
-                logits = await self._pair_coalescer().acall((query, list(texts)))
+                encoded = self.tokenizer.encode_pairs(query, list(texts))
+                logits = await self._encoded_coalescer().acall(encoded)
             else:
                 logits = await asyncio.to_thread(self.score, query, texts)
         except Exception as e:  # noqa: BLE001

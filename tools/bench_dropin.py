@@ -73,7 +73,7 @@ def _coalescers():
         c = getattr(enc, "_query_coalescer", None)
         if c is not None:
             out["embed"] = c
-        c = getattr(enc, "_pair_coalescer", None)
+        c = getattr(enc, "_encoded_pair_coalescer", None) or getattr(enc, "_pair_coalescer", None)
         if c is not None:
             out["rerank"] = c
     for col in list(V._collections.values()):
