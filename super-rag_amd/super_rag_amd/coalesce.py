@@ -79,7 +79,7 @@ class Coalescer:
             slot.event.wait()
             slot.event.clear()
         if not slot.done:
-            self._lead()
+            self._lead(caller=True)
         if slot.error is not None:
             raise slot.error
         return slot.result
@@ -95,18 +95,24 @@ class Coalescer:
                 self._busy = True
                 lead = True
         if lead:
-            # not awaited: the worker may go on to later coroutines' batches after this one's
-            runner = slot.loop.run_in_executor(None, self._lead)
-            runner.add_done_callback(_report)
+            self._spawn_leader(slot.loop)
         return await slot.fut
 
-    def _lead(self) -> None:
+    def _spawn_leader(self, loop) -> None:
+        """(in loop's thread) a worker of loop's executor leads; not awaited, so it may go on to
+        later coroutines' batches after the first one."""
+        runner = loop.run_in_executor(None, self._lead)
+        runner.add_done_callback(_report)
+
+    def _lead(self, caller: bool = False) -> None:
         """Run batches while the queue's next slot is a coroutine's (it has no thread of its own
-        to lead with); hand over to a queued thread caller, or go idle."""
-        while self._lead_one():
+        to lead with); hand over to a queued thread caller, or go idle.  A thread CALLER that led
+        (caller=True) does not serve coroutines after its own batch: a worker of the next
+        coroutine's event loop takes over, so the caller returns."""
+        while self._lead_one(caller):
             pass
 
-    def _lead_one(self) -> bool:
+    def _lead_one(self, caller: bool = False) -> bool:
         with self._lock:
             batch = self._queue[: self.max_batch]
             del self._queue[: self.max_batch]
@@ -125,12 +131,16 @@ class Coalescer:
             self.items += len(batch)
             nxt = None
             keep = False
+            hand_to = None
             if self._queue:
                 nxt = self._queue[0]
                 if nxt.fut is None:
                     nxt.lead = True
+                elif caller:
+                    hand_to = nxt.loop  # a worker of that loop leads the coroutines' batches
+                    nxt = None
                 else:
-                    keep = True  # a coroutine's slot: this thread runs the next batch too
+                    keep = True  # a coroutine's slot: this worker runs the next batch too
                     nxt = None
             else:
                 self._busy = False
@@ -148,4 +158,9 @@ class Coalescer:
                 pass
         if nxt is not None:
             nxt.event.set()
+        if hand_to is not None:
+            try:
+                hand_to.call_soon_threadsafe(self._spawn_leader, hand_to)
+            except RuntimeError:  # that loop has closed: lead its queued batches here
+                keep = True
         return keep

@@ -300,3 +300,40 @@ def test_async_paths_equal_the_sync_ones():
     finally:
         V._collections.clear()
         V.set_store_backend(V._native_store, V._native_load)
+
+
+def test_thread_caller_does_not_serve_coroutines_after_its_own_batch():
+    """A thread caller that leads a batch hands the coroutines queued behind it to a worker of
+    their event loop: it returns after its own batch instead of running theirs."""
+    import asyncio
+    from super_rag_amd.coalesce import Coalescer
+    ran_in = []
+    started = threading.Event()
+
+    def run(items):
+        ran_in.append((threading.current_thread().name, list(items)))
+        if items == ["sync"]:
+            started.set()
+            time.sleep(0.2)  # the coroutines queue up behind this batch
+        return [f"r-{i}" for i in items]
+
+    c = Coalescer(run, max_batch=4)
+    out = {}
+
+    def sync_caller():
+        out["sync"] = c("sync")
+        out["sync_done_batches"] = c.batches
+
+    t = threading.Thread(target=sync_caller, name="sync-caller")
+    t.start()
+    started.wait(5)
+
+    async def coros():
+        return await asyncio.gather(*[c.acall(i) for i in range(10)])
+
+    vals = asyncio.run(coros())
+    t.join(10)
+    assert not t.is_alive()
+    assert out["sync"] == "r-sync" and vals == [f"r-{i}" for i in range(10)]
+    # the sync caller ran exactly its own batch
+    assert [n for n, items in ran_in if n == "sync-caller"] == ["sync-caller"]
