@@ -10,11 +10,14 @@ keeps serving other callers' requests after its own result is ready.  Results ar
 identical to running the items one by one (the batched kernels are row-independent).
 
 ``acall`` is the same queue for coroutines: a waiting coroutine holds no thread (its slot carries
-an asyncio future, completed with one ``call_soon_threadsafe`` per event loop per batch), and a
-coroutine that finds the device idle runs the batches in one worker thread, which keeps leading
+an asyncio future, completed with one ``call_soon_threadsafe`` per event loop per batch).  The
+batches of coroutine slots are led by ONE daemon thread the coalescer owns, which keeps leading
 while the next queued slot is a coroutine's.  With one worker thread blocked per waiting request
 (``asyncio.to_thread`` around ``__call__``), every finished batch woke its ~30 callers' threads,
-which then contended for the interpreter lock.
+which then contended for the interpreter lock.  The leader is not a worker of the caller's event
+loop: that loop's executor may be full of sync callers blocked on this same coalescer, or the loop
+thread itself may be blocked in a sync ``__call__`` (the reference calls ``embed_query`` on the
+loop: nodeflow/runners/vector_search.py:76), and either would leave the queue led by nobody.
 """
 from __future__ import annotations
 
@@ -41,12 +44,6 @@ class _Slot:
         self.event = threading.Event() if loop is None else None
 
 
-def _report(runner) -> None:
-    """A batch's own failure reaches its callers; anything escaping _lead itself is a bug."""
-    if not runner.cancelled() and runner.exception() is not None:
-        logger.error("coalescer leader failed: %r", runner.exception())
-
-
 def _finish(slots) -> None:
     """(in the slots' event loop) complete the futures of one batch's coroutine slots."""
     for s in slots:
@@ -67,6 +64,10 @@ class Coalescer:
         self._busy = False
         self.batches = 0        # number of device batches run (diagnostics)
         self.items = 0          # number of items served
+        # the owned leader of coroutine batches: started on first use, woken by _wake_leader
+        self._cv = threading.Condition(threading.Lock())
+        self._wake = False
+        self._leader = None
 
     def __call__(self, item):
         slot = _Slot(item)
@@ -95,20 +96,40 @@ class Coalescer:
                 self._busy = True
                 lead = True
         if lead:
-            self._spawn_leader(slot.loop)
+            self._wake_leader()
         return await slot.fut
 
-    def _spawn_leader(self, loop) -> None:
-        """(in loop's thread) a worker of loop's executor leads; not awaited, so it may go on to
-        later coroutines' batches after the first one."""
-        runner = loop.run_in_executor(None, self._lead)
-        runner.add_done_callback(_report)
+    def _wake_leader(self) -> None:
+        """Hand the lead (this caller holds it: _busy is set) to the owned leader thread.  If that
+        thread cannot be started (interpreter shutdown), lead here instead: _busy must never stay
+        set with nobody leading."""
+        try:
+            with self._cv:
+                if self._leader is None or not self._leader.is_alive():
+                    t = threading.Thread(target=self._leader_loop, name="coalescer-leader", daemon=True)
+                    t.start()
+                    self._leader = t
+                self._wake = True
+                self._cv.notify()
+        except BaseException:  # noqa: BLE001 - no leader thread: serve the queue inline
+            self._lead()
+
+    def _leader_loop(self) -> None:
+        while True:
+            with self._cv:
+                while not self._wake:
+                    self._cv.wait()
+                self._wake = False
+            try:
+                self._lead()
+            except BaseException as e:  # noqa: BLE001 - _lead_one reports batch failures itself
+                logger.error("coalescer leader failed: %r", e)
 
     def _lead(self, caller: bool = False) -> None:
         """Run batches while the queue's next slot is a coroutine's (it has no thread of its own
         to lead with); hand over to a queued thread caller, or go idle.  A thread CALLER that led
-        (caller=True) does not serve coroutines after its own batch: a worker of the next
-        coroutine's event loop takes over, so the caller returns."""
+        (caller=True) does not serve coroutines after its own batch: the owned leader thread takes
+        over, so the caller returns."""
         while self._lead_one(caller):
             pass
 
@@ -131,13 +152,13 @@ class Coalescer:
             self.items += len(batch)
             nxt = None
             keep = False
-            hand_to = None
+            hand_off = False
             if self._queue:
                 nxt = self._queue[0]
                 if nxt.fut is None:
                     nxt.lead = True
                 elif caller:
-                    hand_to = nxt.loop  # a worker of that loop leads the coroutines' batches
+                    hand_off = True  # the owned leader thread leads the coroutines' batches
                     nxt = None
                 else:
                     keep = True  # a coroutine's slot: this worker runs the next batch too
@@ -158,9 +179,6 @@ class Coalescer:
                 pass
         if nxt is not None:
             nxt.event.set()
-        if hand_to is not None:
-            try:
-                hand_to.call_soon_threadsafe(self._spawn_leader, hand_to)
-            except RuntimeError:  # that loop has closed: lead its queued batches here
-                keep = True
+        if hand_off:
+            self._wake_leader()
         return keep

@@ -120,6 +120,11 @@ class Tokenizer:
                 out.append(a)
             return out
 
+    def cache_misses(self, texts: Sequence[str]) -> int:
+        """How many of texts are not in the content-id cache (the LRU order is not touched)."""
+        with self._cache_lock:
+            return sum(1 for t in texts if t not in self._cache)
+
     def content_ids(self, text: str) -> List[int]:
         return self._content_arrays_many([text])[0].tolist()
 

@@ -303,8 +303,8 @@ def test_async_paths_equal_the_sync_ones():
 
 
 def test_thread_caller_does_not_serve_coroutines_after_its_own_batch():
-    """A thread caller that leads a batch hands the coroutines queued behind it to a worker of
-    their event loop: it returns after its own batch instead of running theirs."""
+    """A thread caller that leads a batch hands the coroutines queued behind it to the coalescer's
+    own leader thread: it returns after its own batch instead of running theirs."""
     import asyncio
     from super_rag_amd.coalesce import Coalescer
     ran_in = []
@@ -337,3 +337,51 @@ def test_thread_caller_does_not_serve_coroutines_after_its_own_batch():
     assert out["sync"] == "r-sync" and vals == [f"r-{i}" for i in range(10)]
     # the sync caller ran exactly its own batch
     assert [n for n, items in ran_in if n == "sync-caller"] == ["sync-caller"]
+
+
+@pytest.mark.timeout(60)
+def test_coroutines_are_served_when_the_loop_executor_is_full_or_the_loop_thread_blocks():
+    """the coroutines' leader must not need a worker of the caller's event loop.
+    (a) the loop's default executor has ONE worker, held by a sync caller blocked on the same
+    coalescer (asyncio.to_thread(c, ...)) while coroutines queue; (b) a sync __call__ made on the
+    loop thread itself while coroutines of that loop are queued.  Both finish, results per item."""
+    import asyncio
+    import concurrent.futures as cf
+    from super_rag_amd.coalesce import Coalescer
+    started = threading.Event()
+
+    def run(items):
+        if "slow" in items:
+            started.set()
+            time.sleep(0.15)
+        return [f"r-{i}" for i in items]
+
+    c = Coalescer(run, max_batch=4)
+
+    async def case_a():
+        loop = asyncio.get_running_loop()
+        loop.set_default_executor(cf.ThreadPoolExecutor(max_workers=1))
+        blocked = asyncio.create_task(asyncio.to_thread(c, "slow"))
+        while not started.is_set():
+            await asyncio.sleep(0.005)
+        more_sync = [asyncio.create_task(asyncio.to_thread(c, f"s{i}")) for i in range(3)]
+        vals = await asyncio.wait_for(asyncio.gather(*[c.acall(i) for i in range(12)]), 10)
+        rest = await asyncio.wait_for(asyncio.gather(blocked, *more_sync), 10)
+        return vals, rest
+
+    vals, rest = asyncio.run(case_a())
+    assert vals == [f"r-{i}" for i in range(12)]
+    assert rest == ["r-slow"] + [f"r-s{i}" for i in range(3)]
+
+    started.clear()
+
+    async def case_b():
+        queued = [asyncio.ensure_future(c.acall(i)) for i in range(6)]
+        await asyncio.sleep(0)  # the coroutines enqueue; the loop thread then blocks in __call__
+        own = c("slow")
+        vals = await asyncio.wait_for(asyncio.gather(*queued), 10)
+        return own, vals
+
+    own, vals = asyncio.run(case_b())
+    assert own == "r-slow" and vals == [f"r-{i}" for i in range(6)]
+    assert not c._busy

@@ -88,3 +88,36 @@ def test_content_cache_is_thread_safe_under_constant_eviction():
     assert not errors, errors[:3]
     held = sum(4 * int(v.size) + len(k) + 64 for k, v in tok._cache.items())
     assert tok._cache_bytes == held <= tok._cache_cap_bytes
+
+
+def test_cold_rerank_requests_tokenise_off_the_event_loop():
+    """a coroutine rerank request whose passages mostly miss the token cache tokenises
+    in a worker thread (the HF encode would stall the loop); a warm one stays on the loop."""
+    import asyncio
+    import threading
+    from super_rag_amd import rerank as RR
+    from doubles import RelevanceEncoder, TextTokenizer
+
+    real_tok = Tokenizer(MODELS["bge-reranker-base"], synthetic=True)
+    texts = [f"passage number {i} about topic {i % 7}" for i in range(40)]
+    assert real_tok.cache_misses(texts) == 40
+    real_tok.encode_pairs("q", texts)
+    assert real_tok.cache_misses(texts) == 0 and real_tok.cache_misses(texts + ["new"]) == 1
+
+    tok = TextTokenizer()  # the double, with a cache that remembers what it encoded
+    cached, where = set(), []
+    tok.cache_misses = lambda ts: sum(t not in cached for t in ts)
+    real = tok.encode_pairs
+
+    def spy(q, ps):
+        where.append(threading.current_thread() is threading.main_thread())
+        cached.update(ps)
+        return real(q, ps)
+
+    tok.encode_pairs = spy
+    rer = RR.RerankService("jina_ai", "r", "", "", encoder=RelevanceEncoder(tok), tokenizer=tok,
+                           device_batch=256)
+    cold = asyncio.run(rer._rank_texts("topic 3", texts))
+    warm = asyncio.run(rer._rank_texts("topic 3", texts))
+    assert cold == warm and sorted(cold) == list(range(40))
+    assert where == [False, True]  # cold: a worker thread; warm: the loop (main) thread
