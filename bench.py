@@ -362,7 +362,7 @@ def run_bench(a, mp=None):
 
     # ---- roofline of the dominant kernel -------------------------------------------------------
     wl = "config5" if a.workload == "config5" and a.fp8 == 3 else None
-    roof = dominant_roofline(prof, wl)
+    roof = add_held_peak(dominant_roofline(prof, wl), peaks)
     step_ms = dt / a.steps * 1e3
     kern = kernel_table(prof, a.steps, top=12)
     search_roof = scan_roofline(prof, wl)
@@ -381,6 +381,8 @@ def run_bench(a, mp=None):
         free_workload(W)
         config5 = config5_field(a, world, rank, local, dev, dist,
                                 (fidelity or {}).get("fp8_mode3"))
+        if config5:
+            add_held_peak(config5.get("roofline"), peaks)
 
     # ---- the reference's seeded reranker (bge-reranker-v2-m3) on the rerank stage alone ---------
     v2m3 = None
@@ -460,6 +462,7 @@ def summary(line):
         "ms_per_step": line["ms_per_step"], "recall_at_10": line.get("recall_at_10"),
         "stage_ms": {k: v for k, v in (line.get("stage_ms") or {}).items() if k != "note"},
         "dominant_kernel": roof.get("kernel"), "roofline_frac": roof.get("frac"),
+        "roofline_frac_of_held_peak": roof.get("frac_of_held_peak"),
         "rerank_fidelity": fid(line.get("rerank_fidelity")),
         "drop_in": drop(line.get("drop_in")),
         "config5": {"value": c5["value"], "ms_per_step": c5["ms_per_step"],
@@ -796,10 +799,13 @@ def timed_steps(W, a, world, dev, dist):
         dt = float(t.item())
         # per-stage ms per step: the max over ranks of each stage (the exchange waits for the
         # slowest rank, so its max is the critical one)
-        st = torch.tensor([W.stage_ms[k] for k in StageClock.STAGES], dtype=torch.float64,
+        # (the stages, then the exchange's per-collective keys exchange_c1 / _c2 /
+        # _bm25_allreduce / _c3)
+        keys = list(W.stage_ms)
+        st = torch.tensor([W.stage_ms[k] for k in keys], dtype=torch.float64,
                           device=dev if a.dist_backend != "gloo" else "cpu")
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
-        W.stage_ms = {k: round(float(v), 4) for k, v in zip(StageClock.STAGES, st.tolist())}
+        W.stage_ms = {k: round(float(v), 4) for k, v in zip(keys, st.tolist())}
     return dt, prof
 
 
@@ -955,9 +961,64 @@ def measured_peaks(dev):
     e1.record()
     torch.cuda.synchronize()
     out["mfma_f16_gemm_mainloop_TFs"] = round(2.0 * M * Nn * K * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e12, 1)
+    del X, W, Y
+    out.update(mfma_rate_peaks(dev))
     out["note"] = ("measured on this box after the timed region; roofline.peak stays the spec value "
-                   "(HBM 8 TB/s, f16 2.5 PF at 2.4 GHz; the chip holds ~1.8-1.9 GHz under these GEMMs)")
+                   "(HBM 8 TB/s, f16 2.5 PF / fp8 5 PF at 2.4 GHz); mfma_*_peak_TFs_held: the MFMA "
+                   "issue-rate microbenchmark (sr_diag_mfma_rate: every CU, 8 waves x 8 independent "
+                   "chains, random operands, >= 2 s of launches first) at the clock the chip held "
+                   "under it (s_memtime / s_memrealtime)")
     return out
+
+
+def mfma_rate_peaks(dev, warm_s=2.0, timed=4):
+    """The MFMA issue-rate peak on this box: sr_diag_mfma_rate in the
+    product's f16 and block-scaled fp8 shapes, back-to-back launches for warm_s seconds (DVFS
+    settles), then `timed` launches between HIP events; the clock from the kernel's own
+    s_memtime / s_memrealtime stamps (median over workgroups) of the timed launches."""
+    import time as _t
+    import torch
+    from super_rag_amd import _native as N
+    out = {}
+    blocks = 1024
+    sink = torch.empty(blocks * 512, device=dev)
+    stamps = torch.zeros(blocks * 2, device=dev, dtype=torch.int64)
+    st = torch.cuda.current_stream().cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for f8, K, iters, name in ((0, 32, 500, "f16"), (1, 128, 250, "f8")):
+        flop = blocks * 8.0 * iters * 8 * 16 * 16 * K * 2
+
+        def launch():
+            N.call_diag("sr_diag_mfma_rate", f8, blocks, iters, sink.data_ptr(), stamps.data_ptr(), 0, st)
+        t0 = _t.perf_counter()
+        while _t.perf_counter() - t0 < warm_s:
+            launch()
+            torch.cuda.synchronize()
+        e0.record()
+        for _ in range(timed):
+            launch()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / timed
+        s = stamps.view(blocks, 2).double().cpu()
+        clk = (s[:, 0] / s[:, 1].clamp(min=1) * 0.1).median().item()   # GHz (realtime: 100 MHz)
+        out[f"mfma_{name}_peak_TFs_held"] = round(flop / (ms * 1e-3) / 1e12, 1)
+        out[f"mfma_{name}_clock_ghz"] = round(clk, 3)
+        out[f"mfma_{name}_frac_of_spec"] = round(flop / (ms * 1e-3) / 1e12 /
+                                                 (PEAK_F8_TFLOPS if f8 else PEAK_F16_TFLOPS), 4)
+    return out
+
+
+def add_held_peak(roof, peaks):
+    """roofline.frac_of_held_peak: achieved / the MFMA peak measured on this box (the f16 or fp8
+    figure by the kernel's operands); roofline.frac stays against the spec peak."""
+    if not roof or not peaks or roof.get("bound") != "mfma":
+        return roof
+    key = "mfma_f8_peak_TFs_held" if str(roof.get("kernel", "")).startswith("gemm_f8") else "mfma_f16_peak_TFs_held"
+    if peaks.get(key):
+        roof["held_peak"] = peaks[key]
+        roof["frac_of_held_peak"] = round(roof["achieved"] / peaks[key], 4)
+    return roof
 
 
 def source_fingerprint(root=ROOT):

@@ -64,6 +64,21 @@ int sr_diag_gemm_lnr_stats(const void* X, int64_t lda, const void* W, const floa
                            int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
                            int N, int K, float* stat_out, int device, void* stream);
 
+/* Diagnostic: the e4m3-copy statistics epilogues (fp8 mode 3's O-projection: EPI_LNR16_STATS_Y8
+ * when lnr != 0, as sr_diag_gemm_lnr_stats; EPI_RES16_STATS_Y8 otherwise, as sr_diag_gemm_stats,
+ * mr / gamma unused): fp16 Y, its e4m3 copy y8 (bytes, row stride ldy) and the (sum, M2) partials. */
+int sr_diag_gemm_stats_y8(int lnr, const void* X, int64_t lda, const void* W, const float* bias,
+                          const void* R, int64_t ldr, const float* mr, const float* gamma, void* Y,
+                          int64_t ldy, uint8_t* y8, int M, int N, int K, float* stat_out, int device,
+                          void* stream);
+
+/* Diagnostic: the MFMA issue-rate peak on this box (k_diag.hip).  blocks workgroups of 8 waves,
+ * each wave 8 independent accumulator chains x iters of the product's MFMA (f8 = 0: f16
+ * 16x16x32; f8 = 1: block-scaled fp8 16x16x128) on random operands; FLOP = blocks x 8 x iters x 8 x
+ * 16 x 16 x K x 2 (K = 32 / 128).  sink: device float [blocks x 512]; stamps: device uint64
+ * [blocks x 2] = (d s_memtime, d s_memrealtime) of each block's loop (clock = ratio x 100 MHz). */
+int sr_diag_mfma_rate(int f8, int blocks, int iters, float* sink, uint64_t* stamps, int device, void* stream);
+
 /* Diagnostic: K5c (fused QKV projection + attention, LN-folded: X un-normalised rows, W the folded
  * [Q; K; V] weight (3d x d), bias the folded bias, colsum its row sums, mr (mu, rstd) per row; S ==
  * 128, head dim 64) with in-kernel s_memtime phase stamps.  stamps: device uint64 [grid x 8 waves

@@ -862,6 +862,41 @@ int sr_diag_gemm_lnr_stats(const void* X, int64_t lda, const void* W, const floa
   SR_API_END
 }
 
+int sr_diag_gemm_stats_y8(int lnr, const void* X, int64_t lda, const void* W, const float* bias,
+                          const void* R, int64_t ldr, const float* mr, const float* gamma, void* Y,
+                          int64_t ldy, uint8_t* y8, int M, int N, int K, float* stat_out, int device,
+                          void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(R);
+  SR_NONNULL(Y);
+  SR_NONNULL(y8);
+  SR_NONNULL(stat_out);
+  SR_CHECK(N % 256 == 0, "diag_gemm_stats_y8: N % 256 == 0");
+  SR_CHECK(!lnr || (mr && gamma), "diag_gemm_stats_y8: the LNR form needs mr and gamma");
+  sr::DeviceGuard g(device);
+  sr::LnFold lf;
+  lf.mr = lnr ? mr : nullptr;
+  lf.gamma = lnr ? gamma : nullptr;
+  lf.stat_out = stat_out;
+  lf.y8 = y8;
+  sr::launch_gemm(lnr ? sr::EPI_LNR16_STATS_Y8 : sr::EPI_RES16_STATS_Y8, reinterpret_cast<const sr::half_t*>(X),
+                  lda, reinterpret_cast<const sr::half_t*>(W), bias, R, ldr, Y, ldy, M, N, K,
+                  reinterpret_cast<hipStream_t>(stream), &lf);
+  SR_API_END
+}
+
+int sr_diag_mfma_rate(int f8, int blocks, int iters, float* sink, uint64_t* stamps, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(sink);
+  SR_NONNULL(stamps);
+  sr::DeviceGuard g(device);
+  sr::launch_mfma_rate(f8, blocks, iters, sink, stamps, reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
 int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                  const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
                  int N, int K, int device, void* stream) {

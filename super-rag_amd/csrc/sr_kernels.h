@@ -80,6 +80,10 @@ void gemm_force_tile(int t);  // test hook: -1 auto, else a GemmVariant
 void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                       const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy,
                       int M, int N, int K, hipStream_t stream, uint64_t* stamps = nullptr);
+// MFMA issue-rate peak (k_diag.hip): blocks x 8 waves x iters x 8 independent MFMAs of the
+// product's f16 (f8 = 0) or block-scaled fp8 (f8 = 1) shape on random operands; stamps[2 b] /
+// [2 b + 1] = d(s_memtime) / d(s_memrealtime) of block b's wave 0 around its loop.
+void launch_mfma_rate(int f8, int blocks, int iters, float* sink, uint64_t* stamps, hipStream_t st);
 #endif
 void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8, const float* bias,
                      const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,

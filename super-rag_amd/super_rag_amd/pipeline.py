@@ -47,9 +47,14 @@ class StageClock:
     select).  On device tensors a mark is a HIP event recorded on the current stream (the stream
     every library kernel of the pipeline is launched on; an RCCL collective is ordered into it by
     torch, so the event after a collective marks its completion); on host tensors (the gloo CPU
-    path) a perf_counter stamp.  Events are read back once, in read()."""
+    path) a perf_counter stamp.  Events are read back once, in read().
+    The exchange marks name their collective ("exchange.c1" ...): read() also returns each one's
+    share as exchange_c1 (query all_gather), exchange_c2 (all_to_all of the per-shard lists),
+    exchange_bm25_allreduce (hybrid: the corpus statistics) and exchange_c3 (passage fetch), whose
+    sum is exchange."""
 
     STAGES = ("embed", "search", "exchange", "rerank")
+    EXCHANGES = ("c1", "c2", "bm25_allreduce", "c3")
 
     def __init__(self):
         self.marks = []          # (stage, event or float) in issue order; None stage = start
@@ -71,6 +76,7 @@ class StageClock:
     def read(self) -> dict:
         """{stage: ms per step} over the marks so far (synchronises recorded events)."""
         tot = {s: 0.0 for s in self.STAGES}
+        tot.update({"exchange_" + x: 0.0 for x in self.EXCHANGES})
         prev = None
         for stage, m in self.marks:
             if stage is not None and prev is not None:
@@ -81,7 +87,10 @@ class StageClock:
                     dt = prev.elapsed_time(m)
                 else:  # (a host stamp next to an event: not comparable, not charged)
                     dt = 0.0
-                tot[stage] += dt
+                main, _, sub = stage.partition(".")
+                tot[main] += dt
+                if sub:
+                    tot["exchange_" + sub] += dt
             prev = m
         n = max(1, self.steps)
         return {s: round(v / n, 4) for s, v in tot.items()}
@@ -138,7 +147,7 @@ class SearchPipeline:
         allq = torch.empty((self.world * B, q_emb.shape[1]), dtype=q_emb.dtype, device=qx.device)
         dist.all_gather_into_tensor(allq, qx, group=self.group)
         allq = allq.to(dev) if host else allq
-        self._mark("exchange", allq)                                        # C1
+        self._mark("exchange.c1", allq)
         sims, rows = self.store.search_dev(allq, self.K, row_offset=self.offset)
         self._mark("search", sims)
         return self._exchange(sims, rows, B, self.K, host, dev)
@@ -153,7 +162,7 @@ class SearchPipeline:
         dist.all_to_all_single(rr, rows, group=self.group)
         if host:
             rs, rr = rs.to(dev), rr.to(dev)
-        self._mark("exchange", rs)                                          # C2
+        self._mark("exchange.c2", rs)
         out = self.merge_fn(rs.view(self.world, B, k), rr.view(self.world, B, k), k,
                             device=dev.index or 0)
         self._mark("search", out[0])
@@ -184,7 +193,7 @@ class SearchPipeline:
                 dist.all_gather_into_tensor(out, x, group=self.group)
                 return out.to(dev) if host else out
             allq, toks, lens = gather(q_emb), gather(toks), gather(lens)
-            self._mark("exchange", allq)                                    # C1
+            self._mark("exchange.c1", allq)
             gst = self.lexical.query_stats_dev(toks, lens)
             self._mark("search", gst)
             if host:
@@ -193,7 +202,7 @@ class SearchPipeline:
                 gst = g.to(dev)
             else:
                 dist.all_reduce(gst, group=self.group)
-            self._mark("exchange", gst)                                     # BM25 statistics
+            self._mark("exchange.bm25_allreduce", gst)
         sims, rows = self.store.search_dev(allq, ke, row_offset=self.offset)
         lsc, lrows = self.lexical.search_tok_dev(toks, lens, ke, gstats=gst, row_offset=self.offset)
         self._mark("search", lsc)
@@ -238,7 +247,7 @@ class SearchPipeline:
         lq = rl.view(self.world, B * K).sum(0, dtype=self.p_len.dtype).to(dev)
         idx = torch.arange(B * K, device=dev, dtype=cand_rows.dtype).view(B, K)
         idx = torch.where(cand_rows >= 0, idx, torch.full_like(idx, -1))
-        self._mark("exchange", idx)                                         # C3
+        self._mark("exchange.c3", idx)
         return tq, lq, idx
 
     def rerank(self, q_tok: torch.Tensor, q_len: torch.Tensor, cand_rows: torch.Tensor):

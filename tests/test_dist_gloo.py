@@ -289,5 +289,11 @@ def test_stage_clock_times_the_exchange_world_2():
     for r in range(world):
         st, n = res[r]
         assert n == 3
-        assert set(st) == {"embed", "search", "exchange", "rerank"}
+        assert set(st) == {"embed", "search", "exchange", "rerank", "exchange_c1", "exchange_c2",
+                           "exchange_bm25_allreduce", "exchange_c3"}
         assert st["exchange"] > 0 and st["search"] > 0, st
+        # each collective on its own key; the dense path has no BM25 reduce
+        assert st["exchange_c1"] > 0 and st["exchange_c2"] > 0 and st["exchange_c3"] > 0, st
+        assert st["exchange_bm25_allreduce"] == 0.0, st
+        parts = st["exchange_c1"] + st["exchange_c2"] + st["exchange_c3"]
+        assert abs(parts - st["exchange"]) <= 1e-3 + 1e-6 * st["exchange"], st
