@@ -784,16 +784,10 @@ void attention512_kernel(const half_t* __restrict__ qkv, const int32_t* __restri
 // 32 queries each).  The QKV activation never touches HBM: per token 4.6 KB of writes and reads
 // disappear.  Numerics equal the unfused pair bit for bit (same MFMA order per accumulator, same
 // epilogue FMAs, same fp16 rounding, same attention code order).
-#ifndef SR_QA_CSTL
-#define SR_QA_CSTL 1  // K5c: the next tile's epilogue constants (bias / column sums of its head, row
-                      // statistics and key mask of its panel) staged into LDS with its K-step 0
-                      // (K5c 1,021-1,025 -> 1,028 TF/s; 138 parity tests on it, profiles/r05_k5c_cstl/)
-#endif
-#ifndef SR_QA_K1_EARLY
-#define SR_QA_K1_EARLY 0  // K5c: the next tile's K-step 1 staged mid-attention (+0.3 % K5c alone,
-                          // 24 B of spills beside CSTL: off; profiles/r05_k5c_cstl/) (once every wave holds
-                          // its Q / K fragments, into the dead Q / K images) instead of after it
-#endif
+// The next tile's epilogue constants (bias / column sums of its head, row statistics and key mask
+// of its panel) are staged into LDS with its K-step 0 (K5c 1,021-1,025 -> 1,028 TF/s;
+// profiles/r05_k5c_cstl/).  (Staging the next tile's K-step 1 mid-attention into the dead Q / K
+// images instead of after it: +0.3 % K5c alone, but 24 B of spills beside the constants; not kept.)
 constexpr int QA_BM = 256;              // tokens per panel
 constexpr int QA_BN = 192;              // Q_h, K_h, V_h rows of W
 constexpr int QA_STAGE = (QA_BM + QA_BN) * 64;  // halfs per K-step buffer (56 KiB)
@@ -844,7 +838,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
   // this tile's attention reads the images, and its K-step 1 (PA) right after.
   // CSTL: past PB, the tile's epilogue constants (floats): [3 x 64 bias][3 x 64 column sums]
   // [256 x (mu, rstd)][256 key mask (int)] = 4.5 KiB
-  constexpr int QA_CSTH = SR_QA_CSTL ? 2304 : 0;
+  constexpr int QA_CSTH = 2304;
   __shared__ __attribute__((aligned(16))) half_t lds[IMG + QA_STAGE + QA_CSTH];
   __shared__ float kbias[QA_BM];
   half_t* const PA = lds;
@@ -914,7 +908,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
   // key mask (1 KiB); rows past M read as zero (masked keys, never stored)
   auto stage_cst = [&](int mm, int hh) __attribute__((always_inline)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (SR_QA_CSTL) {
+    {
       const uint32_t l4 = (uint32_t)lane * 4u, l16 = l4 * 4u;
       const int nrow = __builtin_amdgcn_readfirstlane(max(0, min(QA_BM, M - mm)));
       if (w4 < 2) {
@@ -1031,8 +1025,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     // (every thread loads -- threads past QA_BM repeat a row -- so no branch merges the value
     // and the load stays in flight until its use)
     const int m_mk = m0 + (tid & (QA_BM - 1));
-    const int mkv = SR_QA_CSTL ? reinterpret_cast<const int*>(qcst + 896)[tid & (QA_BM - 1)]
-                               : mask[m_mk < M ? m_mk : M - 1];
+    const int mkv = reinterpret_cast<const int*>(qcst + 896)[tid & (QA_BM - 1)];
     // column-group outer: the bias / column sums of a group are loaded once (not once per row
     // group), and its LDS image address is one per lane -- the swizzles depend on the row only
     // through (row >> 1) & 7, which a row group's 16 j does not change -- with the row groups at
@@ -1042,24 +1035,17 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ml = wm * 64 + 16 * j + (lane & 15);
-      const int mg = m0 + ml < M ? m0 + ml : M - 1;
-      if constexpr (SR_QA_CSTL)
-        mrj[j] = LNF ? reinterpret_cast<const float2*>(qcst + 384)[ml] : make_float2(0.f, 1.f);
-      else
-        mrj[j] = LNF ? *reinterpret_cast<const float2*>(mr + (int64_t)mg * 2) : make_float2(0.f, 1.f);
+      mrj[j] = LNF ? reinterpret_cast<const float2*>(qcst + 384)[ml] : make_float2(0.f, 1.f);
     }
     const int ml0 = wm * 64 + (lane & 15);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int n = wn * 96 + 16 * i + 4 * g;   // tile row: segment n >> 6, head dim n & 63
       const int seg = n >> 6, dim = n & 63;
-      const int col = seg * d + h * DH + dim;
-      const float4v b = SR_QA_CSTL ? *reinterpret_cast<const float4v*>(qcst + seg * 64 + dim)
-                                   : *reinterpret_cast<const float4v*>(bias + col);
+      const float4v b = *reinterpret_cast<const float4v*>(qcst + seg * 64 + dim);
       float4v c = {0.f, 0.f, 0.f, 0.f};
       if constexpr (LNF)
-        c = SR_QA_CSTL ? *reinterpret_cast<const float4v*>(qcst + 192 + seg * 64 + dim)
-                       : *reinterpret_cast<const float4v*>(colsum + col);
+        c = *reinterpret_cast<const float4v*>(qcst + 192 + seg * 64 + dim);
       half_t* img = seg == 0 ? Qi : seg == 1 ? Ki : Vi;
       const int chunk = seg == 2 ? a2_vswz(ml0, dim >> 3) : a2_kswz(ml0, dim >> 3);
       half_t* const wp = img + ml0 * DH + chunk * 8 + (dim & 7);
@@ -1118,15 +1104,6 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
           a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][0], qf[u][0], a, 0, 0, 0);
           sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][1], qf[u][1], a, 0, 0, 0);
         }
-    }
-    if constexpr (SR_QA_K1_EARLY) {
-      // every wave has read its Q / K fragments: the Q / K images (PA = their first 56 KiB; V lies
-      // past them) take the next tile's K-step 1 while the softmax and P.V run
-      SR_WAITCNT(63, 0);  // lgkmcnt(0): the fragment reads have returned
-      __syncthreads();
-      __builtin_amdgcn_sched_barrier(0);
-      if (more && grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
-      __builtin_amdgcn_sched_barrier(0);
     }
     if (attend) {
       const half_t* Vs = Vi + sq * 128 * DH;
@@ -1221,10 +1198,8 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(
     if (!more) break;
     // every wave is done with the images: the next tile's K-step 1 goes into PA; K-step 0 (group 0,
     // older than this wave's 4 ctx stores) must have landed before the barrier
-    if constexpr (!SR_QA_K1_EARLY) {
-      __syncthreads();
-      if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
-    }
+    __syncthreads();
+    if (grp == 1 && nk > 1) stage(1, PA, m0_n, h_n);
     if (grp == 0) {
       if (attend)
         SR_WAITCNT(4, 15);

@@ -27,66 +27,10 @@
 #include "sr_common.h"
 #include "sr_kernels.h"
 
-#ifndef SR_GEMM_LINE_GELU
-#define SR_GEMM_LINE_GELU 0  // whole-line stores for the GELU epilogues too (A/B builds)
-#endif
-#ifndef SR_GEMM_GELU_LUT
-#define SR_GEMM_GELU_LUT 1  // FFN1 epilogues: erf from an LDS table (0: A&S 7.1.26, A/B builds)
-#endif
-#ifndef SR_GEMM_LATE_STAGE
-#define SR_GEMM_LATE_STAGE 0  // 1: persistent wide epilogues stage the next tile after the epilogue's
-                              // constant loads (A/B build; measured -0.3 % end to end,
-                              // profiles/r03_gemm_epilogue_ab/)
-#endif
-#ifndef SR_GEMM_PERMW
-#define SR_GEMM_PERMW 1  // wide epilogues: W rows staged in the perm32 order, no permlane16_swap
-#endif
-#ifndef SR_GEMM_GELU_V2
-#define SR_GEMM_GELU_V2 1  // FFN1 epilogues: 2 GELU(x) = x * T(x), T = erfc(-x / sqrt 2) from a
-                           // 1025-entry LDS table over [-4 sqrt 2, 4 sqrt 2] (0: gelu2_lut)
-#endif
-#ifndef SR_GEMM_GELU_LINE
-#define SR_GEMM_GELU_LINE 1  // fp16 FFN1 epilogue: whole 128-B line stores through a 2 KiB scratch
-#endif
-#ifndef SR_GEMM_GELU_BUFST
-#define SR_GEMM_GELU_BUFST 1  // fp16 FFN1 line stores: lane-constant addresses + buffer stores
-#endif
-#ifndef SR_GEMM_WIDE_BUFST
-#define SR_GEMM_WIDE_BUFST 1  // wide LINE epilogues: lane-constant addresses + buffer loads / stores
-#endif
-#ifndef SR_GEMM_WIDE_BUFLD
-#define SR_GEMM_WIDE_BUFLD 1  // ... and the residual rows through buffer loads
-#endif
-#ifndef SR_GEMM_GELU_BUFST8
-#define SR_GEMM_GELU_BUFST8 1  // fp8 FFN1 stores: range-checked buffer stores at lane offsets
-#endif
-#ifndef SR_GEMM_ST_AUX
-#define SR_GEMM_ST_AUX 2  // cache-policy bits of the FFN1 line stores: nt (streaming; A/B: 0, sc0, sc0 sc1)
-#endif
-#ifndef SR_GEMM_WST_AUX
-#define SR_GEMM_WST_AUX 0  // cache-policy bits of the wide epilogues' line stores (A/B builds)
-#endif
-#ifndef SR_GEMM_STATS_MODE
-#define SR_GEMM_STATS_MODE 2  // *_STATS epilogues' row partials: 0 two-pass M2, 1 one-pass fp32,
-                              // 2 one-pass v_dot2c_f32_f16 (A/B builds)
-#endif
-#ifndef SR_GEMM_GELU_LINE8
-#define SR_GEMM_GELU_LINE8 0  // fp8 FFN1 epilogue: 16-B row stores through 1 KiB of scratch (A/B:
-                              // 8 stores per wave instead of 16, but the scratch exchange costs
-                              // more: 1,551 -> 1,447 TF/s, profiles/r04_ffn1_epilogue/)
-#endif
-#ifndef SR_GEMM_GELU_CSTL
-#define SR_GEMM_GELU_CSTL 1  // FFN1 epilogues: bias / colsum / row statistics from LDS (staged by
-                             // LDS-DMA during the K-loop), no global load inside the epilogue
-#endif
-#ifndef SR_GEMM_LINE_STORE
-#define SR_GEMM_LINE_STORE 1  // whole-line epilogue stores through LDS (0: direct, A/B builds)
-#endif
-#ifndef SR_GEMM_RES_HALF
-#define SR_GEMM_RES_HALF 1  // persistent residual + statistics epilogues in half-tile order: their
-                            // constants from an LDS table, a 2 KiB line scratch, row group j + 1's
-                            // residual loaded before row group j's stores (store_tile_res)
-#endif
+// Store cache policy of the FFN1 line stores: nt (streaming; the output is read once, by the next
+// GEMM).  Measured against 0 / sc0 / sc0 sc1 / sc1 in rounds 4-5 (profiles/r05_store_policy/):
+// within +-0.5 %.  The wide epilogues' line stores use the default policy (0).
+constexpr int kFfn1StoreAux = 2;
 
 namespace sr {
 
@@ -199,32 +143,6 @@ __device__ __forceinline__ f2v gelu2_erf2(f2v x) {
   const f2v e = x * (x * splat2(-0.72134752044448170f));
   const f2v w = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
   return pk_fma(ax, pk_fma(-p, w, splat2(1.0f)), x);
-}
-
-// 2 * GELU(x) = x + |x| erf(|x| / sqrt 2) with erf from a 1024-entry LDS table over [0, 4) (step
-// 1/256, entries (erf(z_i), erf(z_i+1) - erf(z_i)), linear interpolation; z >= 4 takes the last
-// entry: erf(4) = 1 - 1.5e-8): one LDS read and 5 VALU per element instead of a v_rcp, a v_exp and
-// 9 VALU.  |error| <= 2.5e-6 (rms 1.0e-6 on N(0, 2) inputs) against fp16 output rounding of rms
-// 5.8e-4 (A&S 7.1.26: 4.2e-7).  Used by the FFN1 epilogues of the pipelined kernels
-// (EPI_LNF_GELU_F16 / _F8), whose GELU math was ~36 % of the kernel (profiles/r02_pmc_gemm_study).
-constexpr int GELU_TAB = 1024;
-__device__ __forceinline__ float gelu2_lut(float x, const float2* __restrict__ tab) {
-  const float ax = fabsf(x);
-  const float az = ax * (256.0f * 0.70710678118654752f);
-  const uint32_t i = min((uint32_t)az, (uint32_t)(GELU_TAB - 1));
-  const float2 t = tab[i];
-  return fmaf(ax, fmaf(__builtin_amdgcn_fractf(az), t.y, t.x), x);
-}
-__device__ __forceinline__ f2v gelu2_lut2(f2v x, const float2* __restrict__ tab) {
-  return f2v{gelu2_lut(x.x, tab), gelu2_lut(x.y, tab)};
-}
-// the table, written by a workgroup's threads before its first barrier
-__device__ __forceinline__ void gelu_tab_init(float2* __restrict__ tab, int tid, int nthreads) {
-  for (int i = tid; i < GELU_TAB; i += nthreads) {
-    const float z0 = (float)i * (1.0f / 256.0f);
-    const float e0 = erff(z0), e1 = erff(z0 + (1.0f / 256.0f));
-    tab[i] = make_float2(e0, e1 - e0);
-  }
 }
 
 // 2 GELU(x) = x * T(x), T(x) = 1 + erf(x / sqrt 2) = erfc(-x / sqrt 2), linearly interpolated
@@ -397,25 +315,80 @@ __device__ __forceinline__ void store_tile_fast(float4v (&acc)[FN][FM], int nw0,
 // from mr (launch_ln_stats_finalize of the producer's partials).  The *_STATS epilogues write the
 // Chan partials of their own fp16-rounded outputs: per 128-column wave span the sum over the 4
 // lane groups (xor-shuffles 16 / 32), then M2 around that span's mean.
-// The pivot of a row's 128-value span (stats mode 2): sq = sum (x - c)^2 is taken with x - c
-// rounded to fp16, exact when x is within a factor 2 of c (Sterbenz) and, for c = 0, always.  So
-// c = the span's first value when the row sits far from zero -- its values 2, 4, 6 (lane m & 15's
-// column group 0) all within |c| / 2 of it, which every row with mean > ~16 std passes -- and c = 0
-// otherwise, where sq - sum^2 / 128 loses only (mean / std)^2 x 2^-24 of M2 to cancellation.  (c =
-// the first value always: up to ~3e-3 of M2 lost on centred rows; c = 0 always: every digit on rows
-// with mean >> std)  v: the lane's column group 0 (8 consecutive values of its row).
-// TEST = false: c = the first value always (the e4m3-copy LNR epilogue, fp8 mode 3's
-// O-projection: the test's registers spilled it 8 -> 32 B).
-template <bool TEST = true>
-__device__ __forceinline__ _Float16 span_pivot(const half8& v, int lane) {
-  bool far = true;
-  if constexpr (TEST) {
-    const float c = (float)v[0], tol = 0.5f * fabsf(c);
+// The *_STATS epilogues' (sum, M2) partials of a row's 128-value span, exact without any
+// data-dependent form: M2 = sq - (sum - 128 c)^2 / 128 with sq = sum (x - c)^2 taken in fp32 around
+// the pivot c = fp16(the mean of the span's first 64 values, column groups 0 and 1):
+//   * x - c is EXACT in fp32 (x and c are fp16 values: their difference needs at most 24 bits for
+//     any exponent gap under 13), so no bit of the deviation is lost, centred row or not;
+//   * the squares and sums round once each in fp32 (2^-24 relative);
+//   * cancellation: sum (x - c)^2 = M2 + 128 (mean - c)^2, and since c is the mean of one half,
+//     128 (mean - c)^2 = 32 (mean_1 - mean_2)^2 <= M2 (the between-halves part of M2): at most a
+//     factor 2, for every row.
+// Each half span (16 values per lane) is summed per lane and reduced over the row's 4 lane groups
+// on its own (half_span_stats), the halves then added (span_stats): the persistent residual
+// epilogue (store_tile_res) parks the first half's three results in one lane group per row group
+// instead of holding four of each per lane.  The sums of x stay on v_dot2c_f32_f16 (exact
+// products); the deviations are one v_dot2_f32_f16 each (f16x2_minus) and the squares v_fmac_f32:
+// one VALU per value more than an fp16 difference.  Against two-pass fp64 M2 of the same fp16
+// outputs: tests/test_gpu_gemm.py (gate 2e-4).  (Rounds 4-5: x - c rounded to fp16 with c = the
+// span's first value when three samples looked far from zero, else 0: up to 5.3e-4 on centred
+// rows, ~3e-3 in the e4m3-copy epilogue that skipped the test; round 6's first try, the fp16
+// difference around the half-span pivot: 3.9e-4 on centred rows, profiles/r06a/.)
+// d = x - c in fp32 for the two fp16 values of a packed pair (nc = -c), each as ONE v_dot2_f32_f16
+// of the pair with (1, 0) / (0, 1) and nc as the accumulator: exact (x * 1 and x * 0 are exact, the
+// sum rounds once and fits 24 bits), reading the pair from the register it already sits in (a
+// separate v_cvt_f32_f16 per value needed a temporary each, and at 256 VGPRs the residual epilogue
+// spilled; the spill's reload waited vmcnt(0) inside the K-loop)
+__device__ __forceinline__ void f16x2_minus(_Float16 x0, _Float16 x1, float nc, float& lo, float& hi) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  lo = __builtin_amdgcn_fdot2(h2{x0, x1}, h2{(_Float16)1.f, (_Float16)0.f}, nc, false);
+  hi = __builtin_amdgcn_fdot2(h2{x0, x1}, h2{(_Float16)0.f, (_Float16)1.f}, nc, false);
+}
+
+// The 4 lane groups (lane >> 4) of a row hold its 4 column groups: the row's total in every lane.
+__device__ __forceinline__ float row_reduce4(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// One half span (column groups 2h, 2h + 1: 16 values per lane) of the statistics: the lane's sum
+// (v_dot2c) and, around the pivot nc = -c, the lane's sum of squared deviations (f16x2_minus +
+// v_fmac), each reduced over the row's 4 lane groups (row_reduce4).  h = 0 derives the pivot from
+// its own sum first (c = fp16(half sum / 64)).
+template <bool FIRST>
+__device__ __forceinline__ void half_span_stats(const half8& x0, const half8& x1, float& nc, float& sum, float& sq) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const h2 one2 = {(_Float16)1.f, (_Float16)1.f};
+  float s = 0.f;
 #pragma unroll
-    for (int k = 2; k < 8; k += 2) far = far && fabsf((float)v[k] - c) <= tol;
+  for (int r = 0; r < 8; r += 2) s = __builtin_amdgcn_fdot2(h2{x0[r], x0[r + 1]}, one2, s, false);
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) s = __builtin_amdgcn_fdot2(h2{x1[r], x1[r + 1]}, one2, s, false);
+  sum = row_reduce4(s);
+  if constexpr (FIRST) nc = -(float)(_Float16)(sum * (1.f / 64.f));
+  float q = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    float d0, d1;
+    f16x2_minus(x0[r], x0[r + 1], nc, d0, d1);
+    q = fmaf(d0, d0, q);
+    q = fmaf(d1, d1, q);
   }
-  const unsigned short cl = far ? __builtin_bit_cast(unsigned short, v[0]) : (unsigned short)0;
-  return __builtin_bit_cast(_Float16, (unsigned short)__shfl(cl, lane & 15, 64));
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    float d0, d1;
+    f16x2_minus(x1[r], x1[r + 1], nc, d0, d1);
+    q = fmaf(d0, d0, q);
+    q = fmaf(d1, d1, q);
+  }
+  sq = row_reduce4(q);
+}
+
+// The span's (sum, M2) from its two halves' reduced sums (pivot -nc): M2 = sq - (sum - 128 c)^2 / 128.
+__device__ __forceinline__ float2 span_stats(float nc, float s0, float q0, float s1, float q1) {
+  const float sum = s0 + s1, sq = q0 + q1;
+  const float sp = fmaf(128.f, nc, sum);
+  return float2{sum, fmaxf(fmaf(-sp * (1.f / 128.f), sp, sq), 0.f)};
 }
 
 // pre(): called once the epilogue's constant loads (bias, column sums / LayerNorm weight, row
@@ -448,7 +421,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   // (not for the GELU epilogues: there the exchange measured slower, FFN1 932 -> 881 TF/s, while
   // QKV gained 1005 -> 1044 and the residual + statistics GEMMs 1072 -> 1078, ab_line3)
   // (Y8: the e4m3 copy leaves from the line read-back too, as whole 128-B row segments)
-  constexpr bool LINE = LINE_ST && !OUT8 && (SR_GEMM_LINE_GELU || (!GELU && !GELU2));
+  constexpr bool LINE = LINE_ST && !OUT8 && !GELU && !GELU2;
   static_assert(EPI == EPI_BIAS_F16 || GELU || GELU2 || RESN || LNF || LNR, "wide epilogue: fp16 outputs");
   const int g = lane >> 4, odd = g & 1;
   const int nlane = nw0 + 16 * odd + 4 * (g & 2);  // + 32 p
@@ -490,7 +463,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
   // at row M (checked tiles: rows past M read zeros and are not stored)
   // (recomputed per row group from a fresh lane id: hoisted over the whole epilogue, the four
   // offsets spilled the residual epilogues at 256 VGPRs)
-  constexpr bool BUFST = LINE && SR_GEMM_WIDE_BUFST;
+  constexpr bool BUFST = LINE;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     uint32_t bo_res = 0, bo_wr = 0, bo_rd = 0, bo_st = 0;
@@ -508,7 +481,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
     if (!LINE && CHECK && m_row >= M) continue;
     const int m = (LINE && CHECK && m_row >= M) ? M - 1 : m_row;
     half8 r16[(RESN || LNR) ? 4 : 1];
-    if constexpr ((RESN || LNR) && BUFST && SR_GEMM_WIDE_BUFLD) {
+    if constexpr ((RESN || LNR) && BUFST) {
       const int row0 = mw0 + j * 16;
       const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldr * 2 : (int64_t)16 * ldr * 2;
       const auto rr = panel_rsrc(reinterpret_cast<const half_t*>(R) + (int64_t)row0 * ldr + nw0, nb);
@@ -519,15 +492,6 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 #else
         (void)rr;
 #endif
-      }
-    } else if constexpr ((RESN || LNR) && LINE) {
-      // residual row segments at offsets re-derived from the lane id where used (no hoisted
-      // per-lane 64-bit addresses: they spill at 256 VGPRs); m is clamped to row M - 1
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int ln = lane_id_here(), gl = ln >> 4;
-        r16[p] = *reinterpret_cast<const half8*>(reinterpret_cast<const half_t*>(R) + (int64_t)m * ldr +
-                                                 nw0 + 16 * (gl & 1) + 4 * (gl & 2) + 32 * p);
       }
     } else if constexpr (RESN || LNR) {
 #pragma unroll
@@ -590,10 +554,8 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       if constexpr (GELU2) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if constexpr (GLUT && SR_GEMM_GELU_V2)
+          if constexpr (GLUT)
             x[q] = f2v{gelu2_t(x[q].x, gtab), gelu2_t(x[q].y, gtab)};
-          else if constexpr (GLUT)
-            x[q] = gelu2_lut2(x[q], gtab);
           else
             x[q] = gelu2_erf2(x[q]);
         }
@@ -609,13 +571,8 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
           hv[p][2 * q] = (half_t)x[q].x;
           hv[p][2 * q + 1] = (half_t)x[q].y;
         }
-        if constexpr (BUFST) {
+        if constexpr (BUFST)
           *reinterpret_cast<half8*>(reinterpret_cast<char*>(scr) + (bo_wr ^ (uint32_t)(p << 6))) = hv[p];
-        } else if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
-          const int ln = lane_id_here(), gl = ln >> 4;
-          *reinterpret_cast<half8*>(scr + (ln & 15) * 128 +
-                                    (((4 * p + 2 * (gl & 1) + ((gl >> 1) & 1)) ^ (ln & 15)) << 3)) = hv[p];
-        }
         else
           *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
         if constexpr (Y8 && !LINE) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
@@ -677,10 +634,8 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       if constexpr (GELU2) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          if constexpr (GLUT && SR_GEMM_GELU_V2)
+          if constexpr (GLUT)
             v[r] = gelu2_t(v[r], gtab);
-          else if constexpr (GLUT)
-            v[r] = gelu2_lut(v[r], gtab);
           else
             v[r] = gelu2_erf(v[r]);
         }
@@ -693,13 +648,8 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) hv[p][r] = (half_t)v[r];
-        if constexpr (BUFST) {
+        if constexpr (BUFST)
           *reinterpret_cast<half8*>(reinterpret_cast<char*>(scr) + (bo_wr ^ (uint32_t)(p << 6))) = hv[p];
-        } else if constexpr (LINE) {  // -> scratch row (lane & 15), 16-B chunk XOR-swizzled by the row
-          const int ln = lane_id_here(), gl = ln >> 4;
-          *reinterpret_cast<half8*>(scr + (ln & 15) * 128 +
-                                    (((4 * p + 2 * (gl & 1) + ((gl >> 1) & 1)) ^ (ln & 15)) << 3)) = hv[p];
-        }
         else
           *reinterpret_cast<half8*>(reinterpret_cast<half_t*>(Y) + (int64_t)m * ldy + nlane + 32 * p) = hv[p];
         if constexpr (Y8 && !LINE) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
@@ -726,7 +676,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
                                                         (bo_rd ^ (uint32_t)(q << 6)) + q * 1024);
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef int v4i __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, bo_st + q * (uint32_t)(8 * ldy), 0, SR_GEMM_WST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, bo_st + q * (uint32_t)(8 * ldy), 0, 0);
         if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
           typedef int v2i __attribute__((ext_vector_type(2)));
           const v2i q8 = {(int)e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]),
@@ -738,88 +688,15 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         (void)ry;
 #endif
       }
-    } else if constexpr (LINE) {
-      // the row group's 16 x 128 columns were written to the scratch (chunk c of row r at
-      // c ^ r: conflict-free b128 writes and reads); read back as rows 4q + (lane >> 4), chunk
-      // lane & 15, so each store instruction writes 4 whole 256-B row segments
-      half_t* const yw = reinterpret_cast<half_t*>(Y) + (int64_t)(mw0 + j * 16) * ldy + nw0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ln = lane_id_here(), c = ln & 15, rr = 4 * q + (ln >> 4);
-        const half8 o = *reinterpret_cast<const half8*>(scr + rr * 128 + ((c ^ rr) << 3));
-        if (!CHECK || mw0 + j * 16 + rr < M) {
-          *reinterpret_cast<half8*>(yw + (int64_t)rr * ldy + c * 8) = o;
-          if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
-            uint2 q8;
-            q8.x = e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
-            q8.y = e4m3x4((float)o[4], (float)o[5], (float)o[6], (float)o[7]);
-            *reinterpret_cast<uint2*>(lf.y8 + (int64_t)(mw0 + j * 16 + rr) * ldy + nw0 + c * 8) = q8;
-          }
-        }
-      }
     }
     if constexpr (STATS) {
-      // partner lanes (xor 16 / 32) share the row m, so they are active together
-      float sum = 0.f, m2 = 0.f;
-      if constexpr (SR_GEMM_STATS_MODE == 0) {  // two passes: M2 around the span's mean
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-          for (int r = 0; r < 8; ++r) sum += (float)hv[p][r];
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        const float mw = sum * (1.f / 128.f);
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const float dx = (float)hv[p][r] - mw;
-            m2 = fmaf(dx, dx, m2);
-          }
-        m2 += __shfl_xor(m2, 16, 64);
-        m2 += __shfl_xor(m2, 32, 64);
-      } else {
-        // one pass: sum and sum of squares of the fp16 values (1: fp32 add + fma per value, 2:
-        // v_dot2c_f32_f16 per value pair -- the products of fp16 values are exact in fp32), then
-        // M2 = sq - sum^2 / 128 per 128-column span.
-        // Mode 2 also takes the squares around a PIVOT c, the row's first value in the span (lane
-        // m & 15's hv[0][0], shared by a shuffle), and span_m2 picks the plain or the pivoted M2
-        // by the span's mean / std (rows with mean >> std lost every digit of M2 to
-        // the cancellation; tests/test_gpu_gemm.py test_stats_epilogue_large_offset_rows and
-        // test_lnr_stats_epilogue_persistent_ragged)
-        float sq = 0.f;
-        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-        h2v c2 = {(_Float16)0.f, (_Float16)0.f};
-        if constexpr (SR_GEMM_STATS_MODE == 2) {
-          const _Float16 c = span_pivot<!(Y8 && LNR)>(hv[0], lane);
-          c2 = h2v{c, c};
-        }
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          if constexpr (SR_GEMM_STATS_MODE == 2) {
-#pragma unroll
-            for (int r = 0; r < 8; r += 2) {
-              const h2v x2 = {hv[p][r], hv[p][r + 1]};
-              const h2v d2 = x2 - c2;
-              sum = __builtin_amdgcn_fdot2(x2, h2v{(_Float16)1.f, (_Float16)1.f}, sum, false);
-              sq = __builtin_amdgcn_fdot2(d2, d2, sq, false);
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-              const float x = (float)hv[p][r];
-              sum += x;
-              sq = fmaf(x, x, sq);
-            }
-          }
-        }
-        sum += __shfl_xor(sum, 16, 64);
-        sq += __shfl_xor(sq, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        sq += __shfl_xor(sq, 32, 64);
-        const float sp = SR_GEMM_STATS_MODE == 2 ? fmaf(-128.f, (float)c2[0], sum) : sum;
-        m2 = fmaxf(fmaf(-sp * (1.f / 128.f), sp, sq), 0.f);
-      }
+      // partner lanes (xor 16 / 32) share the row m, so they are active together; the two half
+      // spans in store_tile_res's order and arithmetic (the same partials bit for bit)
+      float nc, s0, q0, s1, q1;
+      half_span_stats<true>(hv[0], hv[1], nc, s0, q0);
+      half_span_stats<false>(hv[2], hv[3], nc, s1, q1);
+      const float2 sm = span_stats(nc, s0, q0, s1, q1);
+      const float sum = sm.x, m2 = sm.y;
       if (g == 0 && (!CHECK || m_row < M)) {
         float2 st;
         st.x = sum;
@@ -833,7 +710,7 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 // The LayerNorm-folded FFN1 epilogues (EPI_LNF_GELU_F16 / _F8): 2 GELU(x) = x T(x) from the LDS
 // table (gelu2_t), x = rstd (acc - mu c) + b.  Per 8 outputs of one row (column group p, row
 // group j): 16 fma of the LayerNorm fold, 7 VALU + one ds_read_b64 each of the GELU.
-//   fp16 (scr != nullptr, SR_GEMM_GELU_LINE): half-tile outer -- the bias / column sums of column
+//   fp16 (scr != nullptr): half-tile outer -- the bias / column sums of column
 //     groups 2h, 2h + 1 live at a time (32 VGPRs) -- and per row group the 16 rows x 64 columns
 //     pass through the wave's 2 KiB LDS scratch and leave as WHOLE 128-byte lines (8 rows x 128 B
 //     per dwordx4 store instead of 16 rows x 64 B): the per-CU store path moves whole lines ~3.7x
@@ -929,7 +806,7 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
       asm("" : "+v"(v[r]));
     }
   };
-  if constexpr (!OUT8 && SR_GEMM_GELU_LINE && SR_GEMM_GELU_BUFST) {
+  if constexpr (!OUT8) {
     // ---- fp16, whole-line stores through the 2 KiB scratch (16 rows x 128 B, chunk k of row r
     // at k ^ (r & 7): conflict-free b128 writes and reads) --------------------------------------
     // Every address is a lane constant computed once: the scratch write of pp = 0 (pp = 1 writes
@@ -982,103 +859,13 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
           } else {
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef int v4i __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, SR_GEMM_ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, kFfn1StoreAux);
 #else
             (void)ry;
             (void)gofs;
             (void)g8;
 #endif
           }
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
-    }
-  } else if constexpr (!OUT8 && SR_GEMM_GELU_LINE) {
-    // ---- fp16, whole-line stores through the 2 KiB scratch (16 rows x 128 B, chunk k of row r
-    // at k ^ (r & 7): conflict-free b128 writes and reads) --------------------------------------
-    float4v bc[2][4];  // bias / colsum of column groups 2h, 2h + 1
-    load_consts(bc[0], 0);
-    load_consts(bc[1], 1);
-    if constexpr (!std::is_same<Pre, NoPre>::value) {
-      __builtin_amdgcn_sched_barrier(0);
-      pre();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1) {
-        load_consts(bc[0], 2);
-        load_consts(bc[1], 3);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          float v[8];
-          gelu8(v, 2 * h + pp, j, bc[pp]);
-          half8 hv;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) hv[r] = (half_t)v[r];
-          const int ln = lane_id_here(), gl = ln >> 4, row = ln & 15;
-          const int k = 4 * pp + 2 * (gl & 1) + (gl >> 1);       // 16-B chunk of the 128-B row
-          *reinterpret_cast<half8*>(scr + row * 64 + ((k ^ (row & 7)) << 3)) = hv;
-        }
-        // read back as 8 rows x 8 chunks per instruction: row 8q + (lane >> 3), chunk lane & 7
-        half_t* const yw = reinterpret_cast<half_t*>(Y) + (int64_t)(mw0 + j * 16) * ldy + nw0 + 64 * h;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int ln = lane_id_here(), c = ln & 7, rr = 8 * q + (ln >> 3);
-          const half8 o = *reinterpret_cast<const half8*>(scr + rr * 64 + ((c ^ (rr & 7)) << 3));
-          if constexpr (DMODE == 5) {
-            if ((float)o[0] == 12345.f) reinterpret_cast<half_t*>(Y)[ln] = o[1];
-          } else if (!CHECK || mw0 + j * 16 + rr < M) {
-            *reinterpret_cast<half8*>(yw + (int64_t)rr * ldy + c * 8) = o;
-          }
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
-    }
-  } else if constexpr (OUT8 && SR_GEMM_GELU_LINE8) {
-    // ---- fp8 (e4m3 bytes): per (half, row group) the 16 rows x 64 B pass through 1 KiB of the
-    // scratch (16-B chunk c of row r at c ^ (r & 3)) and leave as ONE dwordx4 store: 8 stores
-    // per wave instead of 16 x dwordx2 (the store cost here is per instruction, not per byte)
-    uint8_t* const sb = reinterpret_cast<uint8_t*>(scr);
-    float4v bc[2][4];
-    load_consts(bc[0], 0);
-    load_consts(bc[1], 1);
-    if constexpr (!std::is_same<Pre, NoPre>::value) {
-      __builtin_amdgcn_sched_barrier(0);
-      pre();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1) {
-        load_consts(bc[0], 2);
-        load_consts(bc[1], 3);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          float v[8];
-          gelu8(v, 2 * h + pp, j, bc[pp]);
-          uint2 q8;
-          q8.x = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
-              v[2], v[3], __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false), true);
-          q8.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(
-              v[6], v[7], __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false), true);
-          const int ln = lane_id_here(), gl = ln >> 4, row = ln & 15;
-          const int k8 = 4 * pp + 2 * (gl & 1) + (gl >> 1);      // 8-B chunk of the 64-B row
-          *reinterpret_cast<uint2*>(sb + row * 64 + ((((k8 >> 1) ^ (row & 3)) << 4) | ((k8 & 1) << 3))) = q8;
-        }
-        const int ln = lane_id_here(), c = ln & 3, rr = ln >> 2;
-        const uint4 o = *reinterpret_cast<const uint4*>(sb + rr * 64 + ((c ^ (rr & 3)) << 4));
-        if constexpr (DMODE == 5) {
-          if (o.x == 0x12345678u) reinterpret_cast<uint32_t*>(Y)[ln] = o.y;
-        } else if (!CHECK || mw0 + j * 16 + rr < M) {
-          *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(Y) + (int64_t)(mw0 + j * 16 + rr) * ldy +
-                                    nw0 + 64 * h + 16 * c) = o;
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
@@ -1094,7 +881,7 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
     }
     // fp8 (BUFST8): the e4m3 rows leave through a range-checked buffer resource per row group
     // (rows past M dropped by the bounds check, no exec mask) at one lane offset per column group
-    constexpr bool B8 = OUT8 && SR_GEMM_GELU_BUFST8 && DMODE == 0;
+    constexpr bool B8 = OUT8 && DMODE == 0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       if (p < 3) load_consts(bc[(p + 1) & 1], p + 1);
@@ -1169,7 +956,6 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
   constexpr bool LNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
   static_assert(LNR || EPI == EPI_RES16_STATS || EPI == EPI_RES16_STATS_Y8, "store_tile_res: residual epilogues");
   static_assert(PERM, "store_tile_res: the W tile staged in perm32 order (8 consecutive columns per lane)");
-  static_assert(SR_GEMM_STATS_MODE == 2, "store_tile_res: pivoted one-pass statistics");
   const int g = lane >> 4, odd = g & 1;
   const int clane = ln0 + 16 * odd + 4 * (g & 2);  // the lane's column in the tile's table (+ 32 p)
   // lane-constant byte offsets: the residual segment of row (lane & 15) (+ 64 B per column group),
@@ -1200,8 +986,9 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
     __builtin_amdgcn_sched_barrier(0);
   }
   float4v bc[2][2], gc[2][2];  // bias / gamma of column groups 2h, 2h + 1
-  float ssum[4], ssq[4];
-  _Float16 piv[4];
+  // the first half's reduced row sums, squared deviations and pivots, parked one row group per lane
+  // group: lane group g keeps row group g's (3 VGPRs; four of each per lane spilled at 256 VGPRs)
+  float park_s = 0.f, park_q = 0.f, park_nc = 0.f;
 #pragma unroll
   for (int st = 0; st < 8; ++st) {
     const int h = st >> 2, j = st & 3;
@@ -1250,24 +1037,19 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
       for (int r = 0; r < 8; ++r) hv[pp][r] = (half_t)v[r];
       *reinterpret_cast<half8*>(sb + (wofs ^ (uint32_t)(pp << 6))) = hv[pp];
     }
-    // statistics: the span's pivot (span_pivot of column group 0's first values), sums over the
-    // column groups in order 0..3 (store_tile_wide's order)
-    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    // statistics of this half span (store_tile_wide's arithmetic: the same partials bit for bit);
+    // the first half parks its results in lane group j, the second fetches them back
+    float nc, hs, hq;
     if (h == 0) {
-      piv[j] = span_pivot(hv[0], lane);
-      ssum[j] = 0.f;
-      ssq[j] = 0.f;
+      half_span_stats<true>(hv[0], hv[1], nc, hs, hq);
+      const bool mine = g == j;
+      park_s = mine ? hs : park_s;
+      park_q = mine ? hq : park_q;
+      park_nc = mine ? nc : park_nc;
+    } else {
+      nc = __shfl(park_nc, (lane & 15) + 16 * j, 64);
+      half_span_stats<false>(hv[0], hv[1], nc, hs, hq);
     }
-    const h2v c2 = {piv[j], piv[j]};
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp)
-#pragma unroll
-      for (int r = 0; r < 8; r += 2) {
-        const h2v x2 = {hv[pp][r], hv[pp][r + 1]};
-        const h2v d2 = x2 - c2;
-        ssum[j] = __builtin_amdgcn_fdot2(x2, h2v{(_Float16)1.f, (_Float16)1.f}, ssum[j], false);
-        ssq[j] = __builtin_amdgcn_fdot2(d2, d2, ssq[j], false);
-      }
     // read back as 8 rows x 128 B per instruction and store (rows past M dropped by the range)
     const int row0 = mw0 + j * 16;
     const int64_t nr = CHECK ? (int64_t)max(0, min(16, M - row0)) : 16;
@@ -1280,7 +1062,7 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
       const half8 o = *reinterpret_cast<const half8*>(sb + rofs + q * 1024);
 #if defined(__HIP_DEVICE_COMPILE__)
       typedef int v4i __attribute__((ext_vector_type(4)));
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, SR_GEMM_WST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, gofs + q * g8, 0, 0);
       if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
         typedef int v2i __attribute__((ext_vector_type(2)));
         const v2i q8 = {(int)e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]),
@@ -1293,13 +1075,9 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
 #endif
     }
     if (h == 1) {
-      float sum = ssum[j], sq = ssq[j];
-      sum += __shfl_xor(sum, 16, 64);
-      sq += __shfl_xor(sq, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      sq += __shfl_xor(sq, 32, 64);
-      const float sp = fmaf(-128.f, (float)piv[j], sum);
-      const float m2 = fmaxf(fmaf(-sp * (1.f / 128.f), sp, sq), 0.f);
+      const float2 sm = span_stats(nc, __shfl(park_s, (lane & 15) + 16 * j, 64), __shfl(park_q, (lane & 15) + 16 * j, 64),
+                                   hs, hq);
+      const float sum = sm.x, m2 = sm.y;
       const int m_row = row0 + (lane & 15);
       if (g == 0 && (!CHECK || m_row < M)) {
         float2 stv;
@@ -1319,8 +1097,7 @@ template <int EPI>
 struct PipeEpi {
   static constexpr bool WIDE = !(EPI == EPI_BIAS_RES_F32 || EPI == EPI_BIAS_TANH_F32);
   // (the fp8-output FFN1 epilogue through its scratch: 8 x 16-B stores, 16 rows x 64 B each)
-  static constexpr int NSTORE = (EPI == EPI_LNF_GELU_F8 && SR_GEMM_GELU_V2 && SR_GEMM_GELU_LINE8 && SR_GEMM_GELU_LUT)
-                                    ? 8 : WIDE ? 16 : 32;
+  static constexpr int NSTORE = WIDE ? 16 : 32;
   template <bool CHECK, bool LINE = false, bool GLUT = false, bool PERM = false, class Pre = NoPre,
             bool CST = false>
   __device__ __forceinline__ static void run(float4v (&acc)[8][4], int nw0, int mw0, int lane, int M,
@@ -1331,7 +1108,7 @@ struct PipeEpi {
                                              const float2* __restrict__ gtab = nullptr,
                                              const Pre& pre = Pre{}, const float* __restrict__ cst = nullptr,
                                              int ln0 = 0, int lm0 = 0) {
-    if constexpr (WIDE && GLUT && SR_GEMM_GELU_V2 && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
+    if constexpr (WIDE && GLUT && (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8))
       store_tile_gelu<EPI, CHECK, PERM, Pre, 0, CST>(acc, nw0, mw0, lane, M, bias, Y, ldy, lf, gtab, scr, pre,
                                                      cst, ln0, lm0);
     else if constexpr (WIDE && CST && (EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS ||
@@ -1516,11 +1293,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // whole-line epilogue stores: a 4 KiB LDS scratch per wave after the two 64 KiB stages (one
   // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
   // (the e4m3-output epilogues never take the line path: no scratch for them)
-  constexpr bool LINE = SR_GEMM_LINE_STORE && PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 &&
-                        EPI != EPI_LNF_GELU_F8 &&
-                        (SR_GEMM_LINE_GELU || (EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16));
+  constexpr bool LINE = PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 && EPI != EPI_LNF_GELU_F8 &&
+                        EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16;
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
-  // GLUT: the FFN1 epilogues' 8 KiB erf table (gelu2_lut) past the stages / line scratch
+  // GLUT: the FFN1 epilogues' 8 KiB erfc table (gelu2_t) past the stages / line scratch
   // STAMP (diagnostic library: sr_diag_ffn1 diag 9 = the product epilogue, 10 = its math without
   // the stores): per-wave s_memtime phase sums of every tile -- K-step 0, K-step 1, the rest of
   // the K-loop, the epilogue, the tile transition -- stored once at the end (lf.y8 as uint64 [8]
@@ -1529,16 +1305,14 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // global store instructions per wave the epilogue leaves in flight (the diagnostics without
   // stores leave none: their waits must not let the next tile's staging loads through)
   constexpr int NST = (DIAG == 5 || DIAG == 10) ? 0 : PipeEpi<EPI>::NSTORE;
-  constexpr bool GLUT = SR_GEMM_GELU_LUT && (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
+  constexpr bool GLUT = (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
-  constexpr int GTAB = SR_GEMM_GELU_V2 ? GELU_NT + 1 : GELU_TAB;  // float2 entries
+  constexpr int GTAB = GELU_NT + 1;  // float2 entries
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
   // and the 32-bit-output epilogues index the rows as staged)
-  constexpr bool PERMW = SR_GEMM_PERMW && PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
+  constexpr bool PERMW = PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
   // GLINE: the fp16 FFN1 epilogue's 2 KiB per-wave line scratch (store_tile_gelu)
-  constexpr bool GLINE = GLUT && SR_GEMM_GELU_V2 &&
-                         ((SR_GEMM_GELU_LINE && EPI == EPI_LNF_GELU_F16) ||
-                          (SR_GEMM_GELU_LINE8 && EPI == EPI_LNF_GELU_F8));
+  constexpr bool GLINE = GLUT && EPI == EPI_LNF_GELU_F16;
   // CSTL: the FFN1 epilogue's per-tile constants -- bias and column sums of the tile's 256 columns,
   // (mu, rstd) of its 256 rows: 4 KiB -- reach LDS by LDS-DMA during the tile's K-loop (group 1,
   // with its K-step 3 burst) instead of as global loads inside the epilogue: vmcnt is in order, so
@@ -1546,7 +1320,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // and the second half's for the first half's 8 line STORES (write completion, the whole chip
   // storing at once) -- measured in-kernel as an epilogue of 11.2k cycles with stores vs 4.4k
   // without (profiles/r05c/ffn1_stamps.log)
-  constexpr bool CSTL = GLUT && SR_GEMM_GELU_V2 && SR_GEMM_GELU_CSTL;
+  constexpr bool CSTL = GLUT;
   // RHALF: the persistent residual + statistics epilogues in half-tile order (store_tile_res): a
   // 2 KiB line scratch per wave and the same 4 KiB constants table ([256 bias][256 gamma][256 x
   // (mu, rstd)]; RES16: the bias only), the next tile's staging issued from inside the epilogue
@@ -1556,8 +1330,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // (EPI_LNR16_STATS on fp16 operands only: the RES16 and fp8-operand instantiations spilled
   // 12-36 B in this form, RES16 measured 907 -> 860 TF/s and the e4m3-copy LNR (fp8 mode 3's
   // O-projection) 777 -> 761, profiles/r05_res_half/, r05_wexp_lds/)
-  constexpr bool RHALF = SR_GEMM_RES_HALF && EPI == EPI_LNR16_STATS && !F8IN && LINE && PERSIST &&
-                         SR_GEMM_WIDE_BUFST && SR_GEMM_PERMW && SR_GEMM_STATS_MODE == 2;
+  constexpr bool RHALF = EPI == EPI_LNR16_STATS && !F8IN && LINE && PERSIST;
   constexpr bool CSTX = CSTL || RHALF;              // an epilogue constants table in LDS
   constexpr int NCST = CSTL ? 4 : RHALF ? (RLNR ? 4 : 1) : 0;  // its 1 KiB pieces (one per wave)
   constexpr int LSCR = LINE ? (RHALF ? 8 * 1024 : 8 * 2048) : 0;
@@ -1569,8 +1342,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   float2* const gtab = reinterpret_cast<float2*>(lds + 2 * STAGE + LSCR + (GLINE ? 8 * 1024 : 0) +
                                                  (CSTX ? 2048 : 0));
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
-  // constant loads (store_tile_wide's pre hook) instead of at the last K-step's barrier
-  constexpr bool LATE = (SR_GEMM_LATE_STAGE || RHALF) && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
+  // first residual load (store_tile_res's pre hook) instead of at the last K-step's barrier (for
+  // the other epilogues measured -0.3 % end to end, profiles/r03_gemm_epilogue_ab/)
+  constexpr bool LATE = RHALF && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -1711,10 +1485,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     for (int q = tid; q < 256; q += blockDim.x) tau_lds[q] = q < M ? bias[q] : INFINITY;
   }
   if constexpr (GLUT) {  // published by the prologue's barrier
-    if constexpr (SR_GEMM_GELU_V2)
-      gelu_t_tab_init(gtab, tid, blockDim.x);
-    else
-      gelu_tab_init(gtab, tid, blockDim.x);
+    gelu_t_tab_init(gtab, tid, blockDim.x);
   }
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
@@ -1942,7 +1713,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       store_tile_gelu<EPI, false, PERMW, NoPre, 0, CSTL>(acc, wn * 128, wm * 64, lane, M, bias, Y, ldy, lf, gtab, gscr,
                                                         NoPre{}, cst, wn * 128, wm * 64);
     } else if constexpr (DIAG == 5 || DIAG == 6 || DIAG == 10) {  // FFN1 epilogue without its stores / its math
-      static_assert(GLUT && SR_GEMM_GELU_V2, "DIAG 5 / 6: the FFN1 epilogue");
+      static_assert(GLUT, "DIAG 5 / 6: the FFN1 epilogue");
       constexpr int DM = DIAG == 10 ? 5 : DIAG;
       if (full)
         store_tile_gelu<EPI, false, PERMW, NoPre, DM, CSTL>(acc, n0 + wn * 128, m0 + wm * 64, lane, M, bias, Y, ldy, lf,
@@ -2519,7 +2290,6 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
   if (diag == 2) {
     SR_FD(2)
   } else {
-#if SR_GEMM_GELU_V2
     if (diag == 5) {
       SR_FD(5)
     } else if (diag == 6) {
@@ -2533,9 +2303,6 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
     } else {
       SR_FD(7)
     }
-#else
-    SR_CHECK(false, "ffn1_diag: diag 5 / 6 need the SR_GEMM_GELU_V2 epilogue");
-#endif
   }
 #undef SR_FD
   SR_LAUNCH_CHECK();
@@ -2749,10 +2516,10 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
 #undef SR_PP_CASE
   } else if (v == GEMM_PIPE || v == GEMM_PIPE_PERSIST) {
     // (the FFN1 epilogues stage their constants during K-step 1 of a persistent tile: nk >= 4)
-    // (SR_GEMM_RES_HALF: the persistent LNR epilogues stage consecutive row statistics, stat_ld 1)
+    // (the persistent LNR epilogues stage consecutive row statistics: stat_ld 1)
     const bool persist = v == GEMM_PIPE_PERSIST && K >= 2 * GBK &&
                          ((epi != EPI_LNF_GELU_F16 && epi != EPI_LNF_GELU_F8) || K >= 4 * GBK) &&
-                         !(SR_GEMM_RES_HALF && epi == EPI_LNR16_STATS && lfv.stat_ld != 1);
+                         !(epi == EPI_LNR16_STATS && lfv.stat_ld != 1);
     // persistent: 8 XCD groups x G walkers (one 8-wave workgroup per CU, 128 KiB LDS)
     const int64_t g = persist ? 8 * std::min<int64_t>(32, ceil_div(big_tiles, 8)) : big_tiles;
     SR_CHECK(!persist || (g % 8 == 0 && g >= 8), "gemm: persistent grid must be a multiple of 8");

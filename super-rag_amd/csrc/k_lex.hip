@@ -45,10 +45,7 @@
 
 namespace sr {
 
-#ifndef SR_LEX_RB
-#define SR_LEX_RB 8192
-#endif
-constexpr int LEX_RB = SR_LEX_RB;      // rows per accumulation block (32 KiB of LDS; 16384: -20 %)
+constexpr int LEX_RB = 8192;           // rows per accumulation block (32 KiB of LDS; 16384: -20 %)
 constexpr int LEX_THREADS = 512;
 constexpr float LEX_SCALE = 65536.f;   // fixed-point unit of the accumulated score
 constexpr int64_t LEX_KEY_BUDGET = (int64_t)1 << 28;  // candidate keys per query block (2 GiB)

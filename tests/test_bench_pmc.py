@@ -215,3 +215,56 @@ def test_logical_names_of_the_fp8_gemm_kernels():
     assert logical(k.format(8, 0)) == "gemm_f16_lnres16_stats"
     assert logical(k.format(6, 0)) == "gemm_f16_lnfold_gelu"
     assert logical("_ZN2sr12_GLOBAL__N_115qkv_attn_kernelILb1ELi0ELb0EEEvPKDF16_") == "qkv_attention"
+
+
+def test_bulk_dropin_collection_adopts_a_store_and_pools_texts():
+    """the drop-in path measured on the headline corpus.  build_collection_bulk
+    adopts an existing store (bench.py hands over its 10M-row corpus), serves pooled texts /
+    metadata through the connector's own search, and release_collection leaves the adopted store
+    open for its owner."""
+    import sys
+    sys.path.insert(0, os.path.join(bench.ROOT, "tests"))
+    import numpy as np
+    from doubles import NumpyStore
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.models import QueryWithEmbedding
+    from tools import bench_dropin as D
+    V.set_store_backend(lambda dim, dev: NumpyStore(dim, dev), NumpyStore.load)
+    V._collections.clear()
+    try:
+        rng = np.random.default_rng(3)
+        st = NumpyStore(16)
+        st.add(rng.standard_normal((5000, 16)).astype(np.float32))
+        old_pool = D.TEXT_POOL
+        D.TEXT_POOL = 700
+        try:
+            con = D.build_collection_bulk("bulk-t", 0, dim=16, store=st)
+        finally:
+            D.TEXT_POOL = old_pool
+        c = V._collections[con.collection_name]
+        assert c.store is st and len(c.texts) == 5000 and len(c.ids) == 5000
+        assert c.texts[4321] == c.texts[4321 % 700] and c.texts[-1] == c.texts[4999]
+        assert c.metadatas[1403] == {"source": "d3.md"} and c.ids[12] == "bulk-12"
+        with pytest.raises(IndexError):
+            c.texts[5000]
+        q = st.get(np.asarray([4321]))[0]
+        res = con.search(QueryWithEmbedding(query="x", top_k=3, embedding=list(map(float, q))))
+        assert res.results[0].text == c.texts[4321] and res.results[0].score < 1e-4
+        D.release_collection("bulk-t")
+        assert con.collection_name not in V._collections and st.count()[0] == 5000
+    finally:
+        V._collections.clear()
+        V.set_store_backend(V._native_store, V._native_load)
+
+
+def test_held_peak_fraction():
+    """roofline.frac_of_held_peak = achieved / the MFMA peak measured on the
+    box (f16 or fp8 by the kernel); frac stays against the spec peak."""
+    peaks = {"mfma_f16_peak_TFs_held": 2000.0, "mfma_f8_peak_TFs_held": 4000.0}
+    r = bench.add_held_peak({"bound": "mfma", "achieved": 1000.0, "frac": 0.4,
+                             "kernel": "gemm_f16_lnres16_stats"}, peaks)
+    assert r["frac_of_held_peak"] == 0.5 and r["held_peak"] == 2000.0 and r["frac"] == 0.4
+    r = bench.add_held_peak({"bound": "mfma", "achieved": 1000.0, "kernel": "gemm_f8_x"}, peaks)
+    assert r["frac_of_held_peak"] == 0.25
+    r = bench.add_held_peak({"bound": "hbm", "achieved": 5000.0, "kernel": "cosine_scan"}, peaks)
+    assert "frac_of_held_peak" not in r

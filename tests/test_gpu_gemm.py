@@ -112,13 +112,31 @@ def test_gemm_split_weights_match_fp32_weights(variant, epi):
         assert err < 0.1 * err_h, (err, err_h)
 
 
+# Relative M2 gate of the *_STATS partials against two-pass fp64 M2 of the same fp16 outputs
+# (the half-span pivot, no data-dependent form; rounds 4-5 needed 1e-3 / 2e-3)
+M2_GATE = 2e-4
+
+
+def _stats_y8(lnr, X, K, W, b, R, N, mr, gamma, Y, M, st):
+    """sr_diag_gemm_stats_y8 (the e4m3-copy forms) -> the e4m3 copy as uint8 [M, N]."""
+    import torch
+    from super_rag_amd import _native as NT
+    y8 = torch.full((M, N), 0x7F, device=Y.device, dtype=torch.uint8)
+    NT.call_diag("sr_diag_gemm_stats_y8", int(lnr), X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(),
+                 N, mr.data_ptr() if mr is not None else None, gamma.data_ptr() if gamma is not None else None,
+                 Y.data_ptr(), N, y8.data_ptr(), M, N, K, st.data_ptr(), 0,
+                 torch.cuda.current_stream().cuda_stream)
+    return y8
+
+
+@pytest.mark.parametrize("y8", [False, True])
 @pytest.mark.parametrize("offset", [0.0, 40.0, -300.0])
 @pytest.mark.parametrize("M", [600, 4096])
-def test_stats_epilogue_large_offset_rows(offset, M):
-    """the *_STATS epilogues' one-pass span partials (sum, M2) feed every folded
-    LayerNorm.  M2 = sq - sum^2 / 128 lost every digit on rows whose mean >> std; with the pivot
-    (the span's first value) the partials must match a two-pass fp64 computation on the SAME fp16
-    outputs for rows with |mean| / std up to ~600, and stay exact-ish for centred rows."""
+def test_stats_epilogue_large_offset_rows(offset, M, y8):
+    """ADVICE r4 / VERDICT r5: the *_STATS epilogues' one-pass span partials (sum, M2) feed every
+    folded LayerNorm.  Around the half-span pivot (the mean of the span's first 64 values) they
+    must match a two-pass fp64 computation on the SAME fp16 outputs within 2e-4 for rows with
+    |mean| / std up to ~600 and for centred rows, in the fp16 form and the e4m3-copy form."""
     import numpy as np
     import torch
     from super_rag_amd import _native as NT
@@ -133,8 +151,11 @@ def test_stats_epilogue_large_offset_rows(offset, M):
          + offset * 2.0 * (torch.arange(M, device=dev) % 3 == 0).float()[:, None]).half()
     Y = torch.empty(M, N, device=dev, dtype=torch.float16)
     st = torch.full((M, N // 128, 2), float("nan"), device=dev)
-    NT.call_diag("sr_diag_gemm_stats", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(), N,
-                 Y.data_ptr(), N, M, N, K, st.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    if y8:
+        _stats_y8(False, X, K, W, b, R, N, None, None, Y, M, st)
+    else:
+        NT.call_diag("sr_diag_gemm_stats", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(), N,
+                     Y.data_ptr(), N, M, N, K, st.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     y = Y.double().cpu().numpy().reshape(M, N // 128, 128)
     s = st.double().cpu().numpy()
@@ -145,20 +166,21 @@ def test_stats_epilogue_large_offset_rows(offset, M):
     np.testing.assert_allclose(s[..., 0], y.sum(-1), rtol=1e-6, atol=1e-3)
     rel = np.abs(s[..., 1] - m2) / m2
     ratio = np.abs(mean) / np.sqrt(m2 / 128)
-    print(f"offset {offset}: max |mean|/std {ratio.max():.0f}, max rel M2 err {rel.max():.2e}")
-    # centred rows: the plain one-pass form (~1e-7) except spans whose samples suggest an offset
-    # (pivoted: <= ~1e-3, measured 5.3e-4 over 24,576 spans); offset rows: the pivoted form
-    assert rel.max() <= (1e-3 if offset == 0.0 else 2e-3), rel.max()
+    print(f"offset {offset} y8 {y8}: max |mean|/std {ratio.max():.0f}, max rel M2 err {rel.max():.2e}")
+    assert rel.max() <= M2_GATE, rel.max()
 
 
+@pytest.mark.parametrize("y8", [False, True])
 @pytest.mark.parametrize("M,K", [(256 * 200 + 77, 768), (256 * 176, 3072), (1000, 768)])
-def test_lnr_stats_epilogue_persistent_ragged(M, K):
+def test_lnr_stats_epilogue_persistent_ragged(M, K, y8):
     """The FFN2 / O-projection GEMM of the LN-folded encoders (EPI_LNR16_STATS: Y = X W^T + b +
     LN(R) with R un-normalised, and the 128-column (sum, M2) partials of the fp16 Y) on the
     persistent kernel's half-tile epilogue (>= 512 tiles: constants and row statistics staged in
     LDS, 2 KiB line scratch, residual prefetch, next tile staged in the epilogue) and on the
     one-tile-per-workgroup kernel (M = 1000): every output row against fp64, the partials against a
-    two-pass fp64 computation on the same fp16 outputs, rows past M untouched (guard band)."""
+    two-pass fp64 computation on the same fp16 outputs (centred rows), rows past M untouched
+    (guard band).  y8: the e4m3-copy form (EPI_LNR16_STATS_Y8, fp8 mode 3's O-projection, on the
+    wide epilogue), whose copy must equal e4m3(the fp16 Y) byte for byte."""
     import numpy as np
     import torch
     from super_rag_amd import _native as NT
@@ -176,9 +198,12 @@ def test_lnr_stats_epilogue_persistent_ragged(M, K):
     mr = torch.stack([mu, rstd], 1).contiguous()
     Yall = torch.full((M + GUARD, N), 777.0, device=dev, dtype=torch.float16)
     st = torch.full((M, N // 128, 2), float("nan"), device=dev)
-    NT.call_diag("sr_diag_gemm_lnr_stats", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(), N,
-                 mr.data_ptr(), gamma.data_ptr(), Yall.data_ptr(), N, M, N, K, st.data_ptr(), 0,
-                 torch.cuda.current_stream().cuda_stream)
+    if y8:
+        q8 = _stats_y8(True, X, K, W, b, R, N, mr, gamma, Yall, M, st)
+    else:
+        NT.call_diag("sr_diag_gemm_lnr_stats", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(), N,
+                     mr.data_ptr(), gamma.data_ptr(), Yall.data_ptr(), N, M, N, K, st.data_ptr(), 0,
+                     torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     ref = (X.double() @ W.double().T + b.double()
            + ((Rf.double() - mu.double()[:, None]) * rstd.double()[:, None]) * gamma.double())
@@ -186,10 +211,13 @@ def test_lnr_stats_epilogue_persistent_ragged(M, K):
     err = (Y.double() - ref).abs().max().item()
     assert err <= 2 ** -10 * max(1.0, ref.abs().max().item()) + 1e-4, err
     assert bool((Yall[M:] == 777.0).all()), "rows past M were written"
+    if y8:
+        want = Y.float().clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q8, want), int((q8 != want).sum().item())
     y = Y.double().cpu().numpy().reshape(M, N // 128, 128)
     s = st.double().cpu().numpy()
     m2 = ((y - y.mean(-1, keepdims=True)) ** 2).sum(-1)
     np.testing.assert_allclose(s[..., 0], y.sum(-1), rtol=1e-6, atol=1e-3)
     rel = np.abs(s[..., 1] - m2) / m2
-    print(f"M = {M}, K = {K}: max |dY| {err:.2e}, max rel M2 err {rel.max():.2e}")
-    assert rel.max() <= 1e-3, rel.max()
+    print(f"M = {M}, K = {K}, y8 {y8}: max |dY| {err:.2e}, max rel M2 err {rel.max():.2e}")
+    assert rel.max() <= M2_GATE, rel.max()

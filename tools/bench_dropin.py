@@ -17,6 +17,10 @@ is the ceiling this path approaches as batches fill; the reference's own host or
 5.1 ms per query (profiles/r02_reference_orchestration.json) before any model work.
 
     python tools/bench_dropin.py [--rows 100000] [--concurrency 64 256] [--seconds 15]
+
+From BULK_ROWS (1M) rows on, the collection is built by the bulk device path (build_collection_bulk:
+rows generated on the GPU, texts pooled), so the drop-in path can be measured on config 4's 10M-row
+corpus; bench.py hands its own headline store over instead of building a second one.
 """
 from __future__ import annotations
 
@@ -62,6 +66,90 @@ def build_collection(col_id: str, rows: int, dim: int = 768, words_per_chunk: in
                           embedding=v[i].tolist()) for i in range(n)]
         con.add(nodes)
     return con
+
+
+TEXT_POOL = 100000      # distinct chunk texts of a bulk-built collection (row r: pool[r % TEXT_POOL])
+BULK_ROWS = 1000000     # from this size on, run() builds the collection by the bulk device path
+
+
+class PooledRows:
+    """Read-only row -> value view for a bulk-built collection: row r holds pool[r % len(pool)]
+    (10M rows with 100k distinct chunk texts / metadata records: a 10M-entry list of 500-byte
+    strings would not fit the setup time)."""
+    __slots__ = ("pool", "n", "fmt")
+
+    def __init__(self, pool, n: int, fmt=None):
+        self.pool, self.n, self.fmt = pool, int(n), fmt
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, r):
+        if isinstance(r, slice):
+            return [self[i] for i in range(*r.indices(self.n))]
+        r = int(r)
+        if r < 0:
+            r += self.n
+        if not 0 <= r < self.n:
+            raise IndexError(r)
+        return self.fmt(r) if self.fmt is not None else self.pool[r % len(self.pool)]
+
+    def __iter__(self):
+        return (self[i] for i in range(self.n))
+
+
+def build_collection_bulk(col_id: str, rows: int, dim: int = 768, words_per_chunk: int = 90,
+                          seed: int = 0, store=None):
+    """build_collection at any size, without the per-node host path: the clustered rows are
+    generated on the GPU in 1M-row chunks and appended with NativeStore.add_dev, or an existing
+    store is adopted (bench.py hands over the headline's 10M-row corpus, built once); texts and
+    metadata are PooledRows over TEXT_POOL chunks.  Search results, the flow and the rerank are the
+    connector's own; only ingest differs (not measured here).  Returns the connector."""
+    import torch
+    from super_rag_amd import nodeflow_pack as P
+    from super_rag_amd import vectorstore as V
+    P.register()
+    P.register_collection(P.LocalCollection(col_id, {"embedding": {"model": EMBED_MODEL}}))
+    con = V.VectorStoreConnectorAdaptor("mi355x", {"collection": P.collection_name_for(col_id)}).connector
+    con.create_collection(vector_size=dim)
+    c = V._collections[con.collection_name]
+    if store is not None:
+        own = c.store
+        c.store = store
+        if hasattr(own, "close"):
+            own.close()
+        rows = int(store.count()[0])
+    else:
+        dev = torch.device("cuda", c.device)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        centers = torch.randn(256, dim, generator=g, device=dev)
+        step = 1 << 20
+        for a in range(0, rows, step):
+            n = min(step, rows - a)
+            v = centers[torch.arange(a, a + n, device=dev) % 256] + \
+                0.5 * torch.randn(n, dim, generator=g, device=dev)
+            c.store.add_dev(v.contiguous())
+            del v
+        torch.cuda.synchronize()
+    rng = np.random.default_rng(seed)
+    npool = min(TEXT_POOL, rows)
+    w = rng.integers(0, len(WORDS), (npool, words_per_chunk))
+    with c.lock:
+        c.texts = PooledRows([" ".join(WORDS[j] for j in w[i]) for i in range(npool)], rows)
+        c.metadatas = PooledRows([{"source": f"d{i}.md"} for i in range(npool)], rows)
+        c.ids = PooledRows(None, rows, fmt=lambda r: f"bulk-{r}")
+        c.row_of = {}
+        c.version += 1
+    return con
+
+
+def release_collection(col_id: str) -> None:
+    """Drop a bulk collection from the registry WITHOUT closing an adopted store (its owner, the
+    bench's headline workload, still holds it)."""
+    from super_rag_amd import nodeflow_pack as P
+    from super_rag_amd import vectorstore as V
+    with V._registry_lock:
+        V._collections.pop(P.collection_name_for(col_id), None)
 
 
 def _coalescers():
@@ -184,10 +272,17 @@ def _windows(concurrency, seconds: float, start_at: float):
 
 
 def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16,
-        start_at: float = 0.0, lat_out: str | None = None) -> dict:
+        start_at: float = 0.0, lat_out: str | None = None, store=None) -> dict:
+    """store: adopt this NativeStore as the collection's rows (bench.py: the headline's corpus)."""
     col_id = "dropin"
     t = time.time()
-    build_collection(col_id, rows)
+    bulk = store is not None or rows >= BULK_ROWS
+    if bulk:
+        build_collection_bulk(col_id, rows, store=store)
+        if store is not None:
+            rows = int(store.count()[0])
+    else:
+        build_collection(col_id, rows)
     setup = time.time() - t
     rng = np.random.default_rng(7)
     queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
@@ -198,10 +293,14 @@ def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup
                     "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
                     "(synthetic weights, hashing tokenizer); vector_topk 100, S_pair <= 128"),
            "rows": rows, "setup_s": round(setup, 1),
+           "collection": ("bulk: rows on the device (NativeStore.add_dev or the headline's store), "
+                          f"texts pooled over {TEXT_POOL} chunks") if bulk else "connector add()",
            "runs": [measure(c, seconds, col_id, queries,
                             lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None))
                     for c in _windows(concurrency, seconds, start_at)],
            "reference_orchestration_ms_per_query": 5.14}
+    if store is not None:
+        release_collection(col_id)
     return out
 
 
@@ -228,7 +327,7 @@ def main():
     if a.profile:
         import cProfile
         import pstats
-        build_collection("dropin", a.rows)
+        (build_collection_bulk if a.rows >= BULK_ROWS else build_collection)("dropin", a.rows)
         rng = np.random.default_rng(7)
         queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
         measure(16, 3.0, "dropin", queries)
