@@ -172,6 +172,21 @@ __device__ __forceinline__ void gelu_t_tab_init(float2* __restrict__ tab, int ti
   }
 }
 
+// The e4m3-output FFN1 epilogue (fp8 modes) reads T at the NEAREST of GELU_NT8 + 1 nodes over the
+// same range (one fp32 entry each, 16 KiB): per element v_fma + v_med3 (index space + 0.5,
+// clamped), v_cvt_u32, one address op, one ds_read_b32, v_mul -- 5 VALU against the interpolated
+// form's 7.  |T error| <= h8 / 2 max|T'| = 1.1e-3 (x > 0: <= 0.11 % of x T; x = -2: 0.33 %), against
+// e4m3's relative half-step of 3.1 %.
+#ifndef SR_F8_GELU_NEAREST
+#define SR_F8_GELU_NEAREST 1  // (A/B of round 6; resolved after the measurement)
+#endif
+constexpr int GELU_NT8 = 4096;
+__device__ __forceinline__ void gelu_t8_tab_init(float* __restrict__ tab, int tid, int nthreads) {
+  constexpr double h = 2.0 * (double)GELU_XMAX / (double)GELU_NT8;
+  for (int i = tid; i <= GELU_NT8; i += nthreads)
+    tab[i] = (float)erfc(-(-(double)GELU_XMAX + (double)i * h) * 0.70710678118654752);
+}
+
 // W-row order of the wide epilogues (PERMW): inside each 32-row block, LDS row k holds W row
 // perm32(k), so that MFMA tile 2p's rows 4g .. 4g+3 (lane group g) and tile 2p+1's rows 4g ..
 // 4g+3 are the 8 CONSECUTIVE output columns 32p + 16(g & 1) + 4(g & 2) + 0..7 -- the layout the
@@ -788,6 +803,22 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
     }
     // the 8 table reads issued together, consumed after a scheduling fence (left to the
     // scheduler, each read was awaited right behind its own issue)
+    if constexpr (OUT8 && SR_F8_GELU_NEAREST) {  // nearest node of the 4,097-entry fp32 table
+      const float* const t8 = reinterpret_cast<const float*>(gtab);
+      float tn[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        tn[r] = t8[(uint32_t)__builtin_amdgcn_fmed3f(
+            fmaf(v[r], (float)GELU_NT8 / (2.0f * GELU_XMAX), 0.5f * (float)GELU_NT8 + 0.5f), 0.0f, (float)GELU_NT8)];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        // e4m3: 2 GELU >= -0.34, so only the upper saturation bound can apply (e4m3x4's clamp)
+        v[r] = fminf(v[r] * tn[r], 448.f);
+        asm("" : "+v"(v[r]));
+      }
+      return;
+    }
     float fr[8];
     float2 tv[8];
 #pragma unroll
@@ -1307,7 +1338,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr int NST = (DIAG == 5 || DIAG == 10) ? 0 : PipeEpi<EPI>::NSTORE;
   constexpr bool GLUT = (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
-  constexpr int GTAB = GELU_NT + 1;  // float2 entries
+  // float2 entries (the fp8 FFN1's nearest-node table: GELU_NT8 + 1 floats)
+  constexpr int GTAB = (EPI == EPI_LNF_GELU_F8 && SR_F8_GELU_NEAREST) ? (GELU_NT8 + 2) / 2 : GELU_NT + 1;
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
   // and the 32-bit-output epilogues index the rows as staged)
   constexpr bool PERMW = PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
@@ -1475,8 +1507,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
 #pragma unroll
   for (int i = 0; i < 8; ++i) sa[i] = 119;  // the scan: 2^-8 on both operands
 
-  if (PERSIST && lf.stagger > 0) {  // de-phase the walkers of an XCD (their store bursts)
-    const int n_sleep = ((blockIdx.x >> 3) & 7) * lf.stagger;
+  if (PERSIST && lf.stagger != 0) {  // de-phase the walkers of an XCD (> 0) or the XCDs (< 0)
+    const int n_sleep = lf.stagger > 0 ? ((blockIdx.x >> 3) & 7) * lf.stagger : (blockIdx.x & 7) * -lf.stagger;
     for (int i = 0; i < n_sleep; ++i) __builtin_amdgcn_s_sleep(8);
   }
   float* const tau_lds = reinterpret_cast<float*>(lds + 2 * STAGE);
@@ -1485,7 +1517,10 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     for (int q = tid; q < 256; q += blockDim.x) tau_lds[q] = q < M ? bias[q] : INFINITY;
   }
   if constexpr (GLUT) {  // published by the prologue's barrier
-    gelu_t_tab_init(gtab, tid, blockDim.x);
+    if constexpr (EPI == EPI_LNF_GELU_F8 && SR_F8_GELU_NEAREST)
+      gelu_t8_tab_init(reinterpret_cast<float*>(gtab), tid, blockDim.x);
+    else
+      gelu_t_tab_init(gtab, tid, blockDim.x);
   }
   // prologue of the first tile: group 0 stages K-step 0 (and waits for it), group 1 K-step 1
   if (grp == 0) {
@@ -2273,7 +2308,7 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
   {  // the product's walker de-phasing (SR_GEMM_STAGGER, launch_gemm)
     const char* e = diag_getenv("SR_GEMM_STAGGER");
     const int st = e ? std::atoi(e) : 0;
-    lf.stagger = st > 0 ? std::max(1, st * K / 768) : 0;
+    lf.stagger = st > 0 ? std::max(1, st * K / 768) : st < 0 ? std::min(-1, st * K / 768) : 0;
   }
   ProfScope prof(f8 ? "ffn1_diag_f8" : "ffn1_diag", stream, 2.0 * M * (double)N * K, 0.0);
   const half_t* x = reinterpret_cast<const half_t*>(X);
@@ -2462,12 +2497,14 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
     if (n_env < 0 || n_env == N) lfv.group_m = g_env;
   lfv.x_k = x_k == K ? 0 : x_k;
   // de-phasing of the persistent walkers: phase step ~1/16 of a tile (K / 96 x 512 cycles);
-  // SR_GEMM_STAGGER = units of 512 cycles per phase (0 = off)
+  // SR_GEMM_STAGGER = units of 512 cycles per phase (0 = off): > 0 de-phases the walkers inside
+  // each XCD (their L2 working set spreads), < 0 the 8 XCDs against each other (diagnostic)
   static const int stagger_env = [] {
     const char* e = diag_getenv("SR_GEMM_STAGGER");
-    return e ? std::atoi(e) : -1;
+    return e ? std::atoi(e) : 0;
   }();
-  lfv.stagger = stagger_env >= 0 ? (stagger_env > 0 ? std::max(1, stagger_env * K / 768) : 0) : 0;
+  lfv.stagger = stagger_env > 0 ? std::max(1, stagger_env * K / 768)
+                : stagger_env < 0 ? std::min(-1, stagger_env * K / 768) : 0;
   if (v == GEMM_BIG) {
     launch_tile<256, 256, 2, 4, false>(epi, dim3((unsigned)big_tiles), stream, X, lda, W, bias, R,
                                        ldr, Y, ldy, M, N, K, x_k / GBK);

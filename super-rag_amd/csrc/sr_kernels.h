@@ -48,9 +48,10 @@ struct LnFold {
                                    //          ldy bytes), the next fp8 GEMM's A operand
   int group_m = 0;                 // pipelined kernels: tile t walks groups of group_m m-panels
                                    // (m fastest inside a group); 0 / 1 = n fastest
-  int stagger = 0;                 // persistent pipelined kernels: walker w of an XCD starts
-                                   // (w & 7) x stagger x 512 cycles late, de-phasing the CUs'
-                                   // epilogue store bursts (HBM write bandwidth)
+  int stagger = 0;                 // persistent pipelined kernels (diagnostic): > 0: walker w of
+                                   // an XCD starts (w & 7) x stagger x 512 cycles late; < 0: the
+                                   // walkers of XCD x start x |stagger| x 512 cycles late
+                                   // (de-phasing the epilogue store bursts)
   int x_k = 0;                     // split weights: X has x_k columns and K = 2 x_k; the K-steps
                                    // past x_k re-read X from k = 0, so W = [W_hi | W_lo] (N x 2 x_k)
                                    // gives X W_hi^T + X W_lo^T in one fp32 accumulation (0 = K)

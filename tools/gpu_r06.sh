@@ -11,6 +11,16 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$T
 for P in ${PARTS//,/ }; do
   case $P in
     stats) timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm.py -k "stats" -v -s --timeout 240 --timeout-method thread > gpurun_out/$TAG/stats.log 2>&1 || exit 1 ;;
+    embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
+    xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
+             echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
+             SR_GEMM_STAGGER=$S timeout -k 10 200 python -u tools/ffn1_bench.py --M 1638400 --diags 0 --rounds 3 >> gpurun_out/$TAG/xstag.log 2>&1 || exit 1
+           done ;;
+    f8ab) L=$PWD/super-rag_amd/super_rag_amd
+          for r in 1 2; do for D in $L/lib/libsrmi_diag.so $L/lib_ab/libsrmi_diag_${F8AB:-interp}.so; do
+            echo "== $(basename $D) r$r" >> gpurun_out/$TAG/f8ab.log
+            SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 200 python -u tools/ffn1_bench.py --f8 --M 1638400 --diags 0 --rounds 2 >> gpurun_out/$TAG/f8ab.log 2>&1 || exit 1
+          done; done ;;
     peaks) timeout -k 10 200 python -u -c "import torch, json, bench; print(json.dumps(bench.mfma_rate_peaks(torch.device('cuda', 0))))" > gpurun_out/$TAG/peaks.log 2>&1 || exit 1 ;;
     c3) timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -k config3 -x -v -s --timeout 240 --timeout-method thread > gpurun_out/$TAG/c3.log 2>&1 || exit 1 ;;
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=15 > gpurun_out/$TAG/gpu_tests.log 2>&1 || exit 1 ;;
