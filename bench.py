@@ -354,8 +354,13 @@ def run_bench(a, mp=None):
     if rank == 0 and world == 1 and not a.no_extras and a.dropin_seconds > 0:
         from tools.bench_dropin import run as dropin_run
         # (the headline's own corpus when the sizes agree: built once, as VERDICT r5 item 4 asks)
-        drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds,
-                             store=W.store if a.dropin_rows == N_total and world == 1 else None)
+        try:
+            drop_in = dropin_run(rows=a.dropin_rows, concurrency=(64, 256), seconds=a.dropin_seconds,
+                                 store=W.store if a.dropin_rows == N_total and world == 1 else None)
+        except Exception as e:  # noqa: BLE001 - the headline line must survive a drop-in failure
+            import traceback
+            traceback.print_exc()
+            drop_in = {"error": f"{type(e).__name__}: {e}"}
         drop_in["pipeline_qps_same_box"] = round(value, 2)
         if mp is not None:
             # N serving processes on this GPU, C callers each (one window per C), measured

@@ -79,6 +79,13 @@ int sr_diag_gemm_stats_y8(int lnr, const void* X, int64_t lda, const void* W, co
  * [blocks x 2] = (d s_memtime, d s_memrealtime) of each block's loop (clock = ratio x 100 MHz). */
 int sr_diag_mfma_rate(int f8, int blocks, int iters, float* sink, uint64_t* stamps, int device, void* stream);
 
+/* Diagnostic: sr_diag_gemm_lnr_stats's persistent kernel with in-kernel s_memtime phase stamps
+ * (stamps: device uint64 [grid x 8 waves x 8], sr_diag_ffn1_stamps' layout; grid = 8 x min(32,
+ * ceil(tiles / 8))). */
+int sr_diag_gemm_lnr_stats_stamps(const void* X, int64_t lda, const void* W, const float* bias, const void* R,
+                                  int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
+                                  int N, int K, float* stat_out, uint64_t* stamps, int device, void* stream);
+
 /* Diagnostic: K5c (fused QKV projection + attention, LN-folded: X un-normalised rows, W the folded
  * [Q; K; V] weight (3d x d), bias the folded bias, colsum its row sums, mr (mu, rstd) per row; S ==
  * 128, head dim 64) with in-kernel s_memtime phase stamps.  stamps: device uint64 [grid x 8 waves

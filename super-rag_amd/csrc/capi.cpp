@@ -897,6 +897,26 @@ int sr_diag_mfma_rate(int f8, int blocks, int iters, float* sink, uint64_t* stam
   SR_API_END
 }
 
+int sr_diag_gemm_lnr_stats_stamps(const void* X, int64_t lda, const void* W, const float* bias, const void* R,
+                                  int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
+                                  int N, int K, float* stat_out, uint64_t* stamps, int device, void* stream) {
+  SR_API_BEGIN
+  SR_NONNULL(X);
+  SR_NONNULL(W);
+  SR_NONNULL(bias);
+  SR_NONNULL(R);
+  SR_NONNULL(mr);
+  SR_NONNULL(gamma);
+  SR_NONNULL(Y);
+  SR_NONNULL(stat_out);
+  SR_NONNULL(stamps);
+  sr::DeviceGuard g(device);
+  sr::launch_lnr_stats_stamps(reinterpret_cast<const sr::half_t*>(X), lda, reinterpret_cast<const sr::half_t*>(W),
+                              bias, R, ldr, mr, gamma, Y, ldy, M, N, K, stat_out, stamps,
+                              reinterpret_cast<hipStream_t>(stream));
+  SR_API_END
+}
+
 int sr_diag_ffn1(int diag, int f8, const void* X, int64_t lda, const void* W, const uint8_t* wexp,
                  const float* bias, const float* colsum, const float* mr, void* Y, int64_t ldy, int M,
                  int N, int K, int device, void* stream) {

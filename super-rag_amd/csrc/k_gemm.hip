@@ -197,6 +197,11 @@ __device__ __forceinline__ int perm32(int k) {
 }
 // the piece-dependent (uniform) part of perm32 for staging piece i (rows 8i + lane / 8 of a band)
 __host__ __device__ constexpr int perm_row_off(int i) { return 32 * (i >> 2) + 8 * (i & 1) + 4 * ((i >> 1) & 1); }
+// The e4m3-output FFN1 (P64): inside each 64-row block LDS row k = 16 t + 4 g + r (tile t of the
+// quad, lane group g, row r) holds W row 16 g + 4 t + r, so lane group g's rows of the quad's 4 tiles
+// are the 16 CONSECUTIVE output columns 16 g .. 16 g + 15: one 16-byte e4m3 store per (quad, row
+// group).  The lane part of the staging offset, 16 (l3 >> 2) + (l3 & 3), is perm32's; the piece part:
+__host__ __device__ constexpr int perm64_row_off(int i) { return 32 * (i & 1) + 4 * (i >> 1); }
 
 __device__ __forceinline__ f2v gelu_erf2(f2v x) {
   const f2v z = __builtin_elementwise_abs(x) * splat2(0.70710678118654752f);
@@ -730,9 +735,12 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
 //     pass through the wave's 2 KiB LDS scratch and leave as WHOLE 128-byte lines (8 rows x 128 B
 //     per dwordx4 store instead of 16 rows x 64 B): the per-CU store path moves whole lines ~3.7x
 //     faster (tools/diag/store_rate.hip) and the FFN1 tile writes 128 KiB.
-//   fp8 / fallback: column-group outer (the bias / column sums of ONE group live, the next one's
-//     loaded while this one is processed), one 8-byte / 16-byte store per (p, j).
-// Same outputs and the same 16 stores per wave either way.
+//   fp8, the W tile staged in perm64 order (PERM, the product): quad outer -- the bias / column
+//     sums of the lane's 16 consecutive columns of quad q live at a time (32 VGPRs) -- and ONE
+//     16-byte store per (quad, row group): 8 stores per wave, 16 rows x 64 B each (the perm32 form
+//     stored 16 x 8 B, 16 rows x 32 B each; whole lines through a 1 KiB scratch measured slower).
+//   fallback (diagnostic variants without PERMW): column-group outer, one 8- / 16-byte store per
+//     (p, j), 16 per wave.
 // DMODE (timing diagnostics, wrong results): 5 = the math (and the scratch exchange) without the
 // global stores, 6 = the stores of the raw accumulators without the math.
 // CST: the tile's bias / column sums / row statistics come from the LDS table the K-loop staged
@@ -756,7 +764,9 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if constexpr (CST) {
-      mrj[j] = *reinterpret_cast<const float2*>(cst + 512 + 2 * (lm0 + j * 16 + (lane & 15)));
+      // (the table address from a fresh lane id: hoisted out of the tile loop, it spilled at 256
+      // VGPRs in the fp8 kernel and its reload waited vmcnt(0) -- the next tile's staging -- here)
+      mrj[j] = *reinterpret_cast<const float2*>(cst + 512 + 2 * (lm0 + j * 16 + (lane_id_here() & 15)));
     } else {
       int m = mw0 + j * 16 + (lane & 15);
       m = (CHECK && m >= M) ? M - 1 : m;
@@ -900,6 +910,71 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // the second half's constant loads stay here
+    }
+  } else if constexpr (OUT8 && PERM) {
+    // ---- fp8, perm64 tile: lane group g owns columns 64 q + 16 g .. + 15 of quad q ----------------
+    auto load16 = [&](float4v (&d)[4], int q, int hh) __attribute__((always_inline)) {
+      const int col = 64 * q + 16 * g + 8 * hh;  // the 8 columns of gelu8's p = 2 q + hh
+      if constexpr (CST) {
+        d[0] = *reinterpret_cast<const float4v*>(cst + ln0 + col);
+        d[1] = *reinterpret_cast<const float4v*>(cst + ln0 + col + 4);
+        d[2] = *reinterpret_cast<const float4v*>(cst + 256 + ln0 + col);
+        d[3] = *reinterpret_cast<const float4v*>(cst + 256 + ln0 + col + 4);
+      } else {
+        d[0] = *reinterpret_cast<const float4v*>(bias + nw0 + col);
+        d[1] = *reinterpret_cast<const float4v*>(bias + nw0 + col + 4);
+        d[2] = *reinterpret_cast<const float4v*>(lf.colsum + nw0 + col);
+        d[3] = *reinterpret_cast<const float4v*>(lf.colsum + nw0 + col + 4);
+      }
+    };
+    float4v bc[2][4];
+    load16(bc[0], 0, 0);
+    load16(bc[1], 0, 1);
+    if constexpr (!std::is_same<Pre, NoPre>::value) {
+      __builtin_amdgcn_sched_barrier(0);
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 1) {
+        load16(bc[0], 1, 0);
+        load16(bc[1], 1, 1);
+      }
+      // (lane-constant byte offset of the lane's 16 bytes in a row group; rows past M are dropped
+      // by the buffer resource's range)
+      const int ln = lane_id_here();
+      const uint32_t bo = (uint32_t)((ln & 15) * (int)ldy + 64 * q + 16 * (ln >> 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v0[8], v1[8];
+        gelu8(v0, 2 * q, j, bc[0]);
+        gelu8(v1, 2 * q + 1, j, bc[1]);
+        if constexpr (DMODE == 5) {
+          float z = 0.f;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) z += v0[r] + v1[r];
+          if (z == 12345.678f) reinterpret_cast<float*>(Y)[lane] = z;
+        } else {
+          typedef int v4i __attribute__((ext_vector_type(4)));
+          const v4i o = {__builtin_amdgcn_cvt_pk_fp8_f32(v0[2], v0[3], __builtin_amdgcn_cvt_pk_fp8_f32(v0[0], v0[1], 0, false), true),
+                         __builtin_amdgcn_cvt_pk_fp8_f32(v0[6], v0[7], __builtin_amdgcn_cvt_pk_fp8_f32(v0[4], v0[5], 0, false), true),
+                         __builtin_amdgcn_cvt_pk_fp8_f32(v1[2], v1[3], __builtin_amdgcn_cvt_pk_fp8_f32(v1[0], v1[1], 0, false), true),
+                         __builtin_amdgcn_cvt_pk_fp8_f32(v1[6], v1[7], __builtin_amdgcn_cvt_pk_fp8_f32(v1[4], v1[5], 0, false), true)};
+          const int row0 = mw0 + j * 16;
+          const int64_t nb = CHECK ? (int64_t)max(0, min(16, M - row0)) * ldy : (int64_t)16 * ldy;
+          const auto ry = panel_rsrc(reinterpret_cast<const half_t*>(reinterpret_cast<const uint8_t*>(Y) +
+                                                                     (int64_t)row0 * ldy + nw0), nb);
+#if defined(__HIP_DEVICE_COMPILE__)
+          __builtin_amdgcn_raw_buffer_store_b128(o, ry, bo, 0, 0);
+#else
+          (void)o;
+          (void)ry;
+          (void)bo;
+#endif
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the second quad's constant loads stay here
     }
   } else {
     // ---- column-group outer, one 8- / 16-byte store per (p, j) -----------------------------------
@@ -1324,7 +1399,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // whole-line epilogue stores: a 4 KiB LDS scratch per wave after the two 64 KiB stages (one
   // array: a second __shared__ object made the compiler wait vmcnt(0) before the K-loop's reads)
   // (the e4m3-output epilogues never take the line path: no scratch for them)
-  constexpr bool LINE = PipeEpi<EPI>::WIDE && !SCAN && DIAG == 0 && EPI != EPI_LNF_GELU_F8 &&
+  // (DIAG 9 = the product epilogue with stamps: the residual epilogues' line path too)
+  constexpr bool LINE = PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG == 9) && EPI != EPI_LNF_GELU_F8 &&
                         EPI != EPI_BIAS_GELU_F16 && EPI != EPI_LNF_GELU_F16;
   // (EPI_SCAN / EPI_SCAN8: a 1 KiB tau table of the <= 256 queries past the stages)
   // GLUT: the FFN1 epilogues' 8 KiB erfc table (gelu2_t) past the stages / line scratch
@@ -1333,9 +1409,6 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // the K-loop, the epilogue, the tile transition -- stored once at the end (lf.y8 as uint64 [8]
   // per wave); the stamps themselves cost a lgkmcnt(0) right behind a barrier
   constexpr bool STAMP = DIAG == 9 || DIAG == 10 || DIAG == 11;  // (11: 9 without the next tile's staging)
-  // global store instructions per wave the epilogue leaves in flight (the diagnostics without
-  // stores leave none: their waits must not let the next tile's staging loads through)
-  constexpr int NST = (DIAG == 5 || DIAG == 10) ? 0 : PipeEpi<EPI>::NSTORE;
   constexpr bool GLUT = (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
   // float2 entries (the fp8 FFN1's nearest-node table: GELU_NT8 + 1 floats)
@@ -1343,6 +1416,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
   // and the 32-bit-output epilogues index the rows as staged)
   constexpr bool PERMW = PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
+  // P64: the e4m3-output FFN1 stages its W rows in perm64 order instead (store_tile_gelu: one
+  // 16-byte store per quad and row group, 8 per wave)
+  constexpr bool P64 = PERMW && EPI == EPI_LNF_GELU_F8;
+  // global store instructions per wave the epilogue leaves in flight (the diagnostics without
+  // stores leave none: their waits must not let the next tile's staging loads through)
+  constexpr int NST = (DIAG == 5 || DIAG == 10) ? 0 : P64 ? 8 : PipeEpi<EPI>::NSTORE;
   // GLINE: the fp16 FFN1 epilogue's 2 KiB per-wave line scratch (store_tile_gelu)
   constexpr bool GLINE = GLUT && EPI == EPI_LNF_GELU_F16;
   // CSTL: the FFN1 epilogue's per-tile constants -- bias and column sums of the tile's 256 columns,
@@ -1376,7 +1455,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // LATE: the next tile's first two K-steps are staged from inside the epilogue, right after its
   // first residual load (store_tile_res's pre hook) instead of at the last K-step's barrier (for
   // the other epilogues measured -0.3 % end to end, profiles/r03_gemm_epilogue_ab/)
-  constexpr bool LATE = RHALF && PERSIST && !SCAN && DIAG == 0 && PipeEpi<EPI>::WIDE;
+  constexpr bool LATE = RHALF && PERSIST && !SCAN && (DIAG == 0 || DIAG == 9) && PipeEpi<EPI>::WIDE;
 
   const int tiles_n = (N + BN - 1) / BN;  // N % 256 == 0 except for EPI_SCAN (corpus chunk rows)
   const int nwg = tiles_n * ((M + BM - 1) / BM);
@@ -1460,7 +1539,8 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, SR_LDS(s + (w4 * 8 + i) * 8 * GBK), 16,
                                                vbw[i & 1], sw, 0, 0);
       // next piece's row offset (bytes = rows x 2K): PERMW rows 0 8 4 12 32 40 36 44
-      if (i < 7) sw += (PERMW ? perm_row_off(i + 1) - perm_row_off(i) : 8) * 2 * K;
+      if (i < 7)
+        sw += (P64 ? perm64_row_off(i + 1) - perm64_row_off(i) : PERMW ? perm_row_off(i + 1) - perm_row_off(i) : 8) * 2 * K;
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1703,8 +1783,9 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
       const uint8_t* wexp = lf.wexp;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int n = PERMW ? n0 + wn * 128 + 32 * (i >> 1) + 4 * (i & 1) + perm32(lane & 15)
-                            : n0 + arow + 16 * i;
+        const int n = P64     ? n0 + wn * 128 + 64 * (i >> 2) + 16 * ((lane & 15) >> 2) + 4 * (i & 3) + (lane & 3)
+                      : PERMW ? n0 + wn * 128 + 32 * (i >> 1) + 4 * (i & 1) + perm32(lane & 15)
+                              : n0 + arow + 16 * i;
         // (from an LDS copy staged with the tile's first K-step instead: fp8 FFN1 1,572 -> 1,540
         // TF/s, spills 8 -> 20 B, profiles/r05_wexp_lds/)
         sa[i] = wexp[n < N ? n : N - 1];
@@ -2340,6 +2421,27 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
     }
   }
 #undef SR_FD
+  SR_LAUNCH_CHECK();
+}
+
+// Stamped product launch of the residual + statistics GEMM (EPI_LNR16_STATS: FFN2 / O-projection,
+// the persistent kernel with its half-tile epilogue) -- sr_diag_gemm_lnr_stats_stamps: per-wave
+// s_memtime phase sums into stamps (the FFN1 stamps' layout, tools/lnr_stamps.py)
+void launch_lnr_stats_stamps(const half_t* X, int64_t lda, const half_t* W, const float* bias, const void* R,
+                             int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
+                             int N, int K, float* stat_out, uint64_t* stamps, hipStream_t stream) {
+  SR_CHECK(N % 256 == 0 && M > 0 && K % GBK == 0 && K >= 2 * GBK, "lnr_stamps: N % 256, K % 64, K >= 128");
+  SR_CHECK(ldy % 8 == 0 && ldr % 8 == 0 && lda % 8 == 0, "lnr_stamps: 16-byte rows");
+  LnFold lf;
+  lf.mr = mr;
+  lf.gamma = gamma;
+  lf.stat_out = stat_out;
+  lf.y8 = reinterpret_cast<uint8_t*>(stamps);  // (the non-Y8 epilogue has no e4m3 copy)
+  lf.group_m = K <= 1024 ? (N >= 2048 ? 8 : 4) : 0;  // the product walk
+  const int64_t tiles = (int64_t)(N / 256) * ceil_div(M, 256);
+  const dim3 grid((unsigned)(8 * std::min<int64_t>(32, ceil_div(tiles, 8)))), block(512);
+  hipLaunchKernelGGL((gemm_pipe_kernel<EPI_LNR16_STATS, true, 9>), grid, block, 0, stream, X, lda, W, bias, R, ldr,
+                     Y, ldy, M, N, K, lf);
   SR_LAUNCH_CHECK();
 }
 #endif  // SR_WITH_DIAG

@@ -85,6 +85,10 @@ void launch_ffn1_diag(int diag, bool f8, const void* X, int64_t lda, const void*
 // product's f16 (f8 = 0) or block-scaled fp8 (f8 = 1) shape on random operands; stamps[2 b] /
 // [2 b + 1] = d(s_memtime) / d(s_memrealtime) of block b's wave 0 around its loop.
 void launch_mfma_rate(int f8, int blocks, int iters, float* sink, uint64_t* stamps, hipStream_t st);
+// The persistent EPI_LNR16_STATS GEMM with in-kernel phase stamps (k_gemm.hip; diagnostic)
+void launch_lnr_stats_stamps(const half_t* X, int64_t lda, const half_t* W, const float* bias, const void* R,
+                             int64_t ldr, const float* mr, const float* gamma, void* Y, int64_t ldy, int M,
+                             int N, int K, float* stat_out, uint64_t* stamps, hipStream_t stream);
 #endif
 void launch_gemm_f8w(int epi, const uint8_t* X8, int64_t lda, const uint8_t* W8, const float* bias,
                      const void* R, int64_t ldr, void* Y, int64_t ldy, int M, int N, int K,

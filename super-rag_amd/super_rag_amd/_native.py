@@ -165,6 +165,9 @@ DIAG_SIGNATURES = {
     "sr_diag_gemm_lnr_stats": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                        c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
                                        c_void_p, c_int, c_void_p]),
+    "sr_diag_gemm_lnr_stats_stamps": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                                              c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
+                                              c_void_p, c_void_p, c_int, c_void_p]),
     "sr_diag_mfma_rate": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "sr_diag_gemm_stats_y8": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                       c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int,

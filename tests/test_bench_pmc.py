@@ -243,7 +243,8 @@ def test_bulk_dropin_collection_adopts_a_store_and_pools_texts():
             D.TEXT_POOL = old_pool
         c = V._collections[con.collection_name]
         assert c.store is st and len(c.texts) == 5000 and len(c.ids) == 5000
-        assert c.texts[4321] == c.texts[4321 % 700] and c.texts[-1] == c.texts[4999]
+        assert c.texts[4321].startswith(c.texts[4321 % 700].rsplit(" ", 1)[0]) and c.texts[-1] == c.texts[4999]
+        assert len(set(c.texts[i] for i in range(0, 5000, 7))) == len(range(0, 5000, 7))  # distinct
         assert c.metadatas[1403] == {"source": "d3.md"} and c.ids[12] == "bulk-12"
         with pytest.raises(IndexError):
             c.texts[5000]

@@ -135,7 +135,11 @@ def build_collection_bulk(col_id: str, rows: int, dim: int = 768, words_per_chun
     npool = min(TEXT_POOL, rows)
     w = rng.integers(0, len(WORDS), (npool, words_per_chunk))
     with c.lock:
-        c.texts = PooledRows([" ".join(WORDS[j] for j in w[i]) for i in range(npool)], rows)
+        # (each row's text is distinct, as in a real corpus -- the merge node drops repeated texts
+        # and the tokenizer cache would otherwise be warm on a 10M-row corpus: the pooled chunk
+        # plus the row's own tag)
+        pool = [" ".join(WORDS[j] for j in w[i]) for i in range(npool)]
+        c.texts = PooledRows(pool, rows, fmt=lambda r: f"{pool[r % npool]} r{r}")
         c.metadatas = PooledRows([{"source": f"d{i}.md"} for i in range(npool)], rows)
         c.ids = PooledRows(None, rows, fmt=lambda r: f"bulk-{r}")
         c.row_of = {}
@@ -284,23 +288,25 @@ def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup
     else:
         build_collection(col_id, rows)
     setup = time.time() - t
-    rng = np.random.default_rng(7)
-    queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
-    # warm up: models resident, kernels compiled, coalescers created
-    measure(min(warmup, max(concurrency)), 3.0, col_id, queries)
-    out = {"path": ("execute_search_flow (collection_service.py:229-366) -> pack vector_search / "
-                    "merge / rerank runners -> EmbeddingService.embed_query + connector.search + "
-                    "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
-                    "(synthetic weights, hashing tokenizer); vector_topk 100, S_pair <= 128"),
-           "rows": rows, "setup_s": round(setup, 1),
-           "collection": ("bulk: rows on the device (NativeStore.add_dev or the headline's store), "
-                          f"texts pooled over {TEXT_POOL} chunks") if bulk else "connector add()",
-           "runs": [measure(c, seconds, col_id, queries,
-                            lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None))
-                    for c in _windows(concurrency, seconds, start_at)],
-           "reference_orchestration_ms_per_query": 5.14}
-    if store is not None:
-        release_collection(col_id)
+    try:
+        rng = np.random.default_rng(7)
+        queries = [" ".join(WORDS[j] for j in rng.integers(0, len(WORDS), 24)) for _ in range(4096)]
+        # warm up: models resident, kernels compiled, coalescers created
+        measure(min(warmup, max(concurrency)), 3.0, col_id, queries)
+        out = {"path": ("execute_search_flow (collection_service.py:229-366) -> pack vector_search / "
+                        "merge / rerank runners -> EmbeddingService.embed_query + connector.search + "
+                        "RerankService.async_rerank, coalesced; 12-layer bge-base-en + bge-reranker-base "
+                        "(synthetic weights, hashing tokenizer); vector_topk 100, S_pair <= 128"),
+               "rows": rows, "setup_s": round(setup, 1),
+               "collection": ("bulk: rows on the device (NativeStore.add_dev or the headline's store), "
+                              f"texts: one of {TEXT_POOL} pooled chunks + the row tag, distinct per row") if bulk else "connector add()",
+               "runs": [measure(c, seconds, col_id, queries,
+                                lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None))
+                        for c in _windows(concurrency, seconds, start_at)],
+               "reference_orchestration_ms_per_query": 5.14}
+    finally:
+        if store is not None:
+            release_collection(col_id)
     return out
 
 

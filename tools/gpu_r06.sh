@@ -21,6 +21,7 @@ for P in ${PARTS//,/ }; do
             echo "== $(basename $D) r$r" >> gpurun_out/$TAG/f8ab.log
             SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 200 python -u tools/ffn1_bench.py --f8 --M 1638400 --diags 0 --rounds 2 >> gpurun_out/$TAG/f8ab.log 2>&1 || exit 1
           done; done ;;
+    lnrst) timeout -k 10 300 python -u tools/lnr_stamps.py > gpurun_out/$TAG/lnr_stamps.log 2>&1 || exit 1 ;;
     peaks) timeout -k 10 200 python -u -c "import torch, json, bench; print(json.dumps(bench.mfma_rate_peaks(torch.device('cuda', 0))))" > gpurun_out/$TAG/peaks.log 2>&1 || exit 1 ;;
     c3) timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -k config3 -x -v -s --timeout 240 --timeout-method thread > gpurun_out/$TAG/c3.log 2>&1 || exit 1 ;;
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=15 > gpurun_out/$TAG/gpu_tests.log 2>&1 || exit 1 ;;
