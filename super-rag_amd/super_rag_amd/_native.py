@@ -297,7 +297,10 @@ def load_diag() -> ctypes.CDLL:
         except OSError as e:
             raise NativeUnavailableError(f"cannot load {path}: {e}") from e
         for name, (res, args) in {**SIGNATURES, **DIAG_SIGNATURES}.items():
-            fn = getattr(lib, name)
+            # (an A/B variant built from older sources may lack a newer diagnostic: skip it)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         _diag = lib
