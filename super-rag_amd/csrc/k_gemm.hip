@@ -690,6 +690,9 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
       const auto r8 = panel_rsrc(reinterpret_cast<const half_t*>(Y8 ? lf.y8 + (int64_t)row0 * ldy + nw0 : nullptr),
                                  Y8 ? nr * ldy : 0);
       (void)r8;
+      typedef int v2i __attribute__((ext_vector_type(2)));
+      v2i keep8 = {0, 0};  // Y8: the e4m3 bytes of the even q, paired with the odd q's below
+      (void)keep8;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const half8 o = *reinterpret_cast<const half8*>(reinterpret_cast<const char*>(scr) +
@@ -698,10 +701,23 @@ __device__ __forceinline__ void store_tile_wide(float4v (&acc)[8][4], int nw0, i
         typedef int v4i __attribute__((ext_vector_type(4)));
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, o), ry, bo_st + q * (uint32_t)(8 * ldy), 0, 0);
         if constexpr (Y8) {  // e4m3 copy of the stored fp16 values for the next fp8 GEMM
-          typedef int v2i __attribute__((ext_vector_type(2)));
           const v2i q8 = {(int)e4m3x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]),
                           (int)e4m3x4((float)o[4], (float)o[5], (float)o[6], (float)o[7])};
-          __builtin_amdgcn_raw_buffer_store_b64(q8, r8, (bo_st >> 1) + q * (uint32_t)(4 * ldy), 0, 0);
+          if ((q & 1) == 0) {
+            keep8 = q8;
+          } else {
+            // 16-byte copy stores (half the store instructions: the epilogue is store-issue
+            // bound): the lanes of a chunk pair (2k, 2k + 1: the same row) trade 8 bytes -- the
+            // even lane sends its odd-q chunk, the odd lane its even-q chunk -- so the even lane
+            // stores chunks 2k, 2k + 1 of row 4 (q - 1) + lane / 16, the odd lane those of row
+            // 4 q + lane / 16
+            const int odd = lane_id_here() & 1;
+            const v2i send = odd ? keep8 : q8;
+            const v2i recv = {__shfl_xor(send.x, 1, 64), __shfl_xor(send.y, 1, 64)};
+            const v4i w = odd ? v4i{recv.x, recv.y, q8.x, q8.y} : v4i{keep8.x, keep8.y, recv.x, recv.y};
+            __builtin_amdgcn_raw_buffer_store_b128(w, r8, (bo_st >> 1) - 8 * odd + (uint32_t)(q - 1 + odd) * (uint32_t)(4 * ldy),
+                                                   0, 0);
+          }
         }
 #else
         (void)o;
