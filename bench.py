@@ -321,7 +321,12 @@ def run_bench(a, mp=None):
     # ---- recall@10 of the search stage vs exact fp32 (outside the timed region) -----------------
     recall = search_recall(W, a, dev) if world == 1 and not a.no_extras else None
 
-    peaks = measured_peaks(dev) if rank == 0 and not a.no_extras else None
+    peaks = None
+    if rank == 0 and not a.no_extras:
+        try:  # (the diagnostic library: reported, never a reason to lose the product's line)
+            peaks = measured_peaks(dev)
+        except Exception as e:  # noqa: BLE001
+            peaks = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     # ---- search-only at B = 32 (config 2's query block) on this rank's shard: fp16 and fp8 -----
     search32 = None

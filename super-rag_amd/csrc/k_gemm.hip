@@ -177,9 +177,6 @@ __device__ __forceinline__ void gelu_t_tab_init(float2* __restrict__ tab, int ti
 // clamped), v_cvt_u32, one address op, one ds_read_b32, v_mul -- 5 VALU against the interpolated
 // form's 7.  |T error| <= h8 / 2 max|T'| = 1.1e-3 (x > 0: <= 0.11 % of x T; x = -2: 0.33 %), against
 // e4m3's relative half-step of 3.1 %.
-#ifndef SR_F8_GELU_NEAREST
-#define SR_F8_GELU_NEAREST 1  // (A/B of round 6; resolved after the measurement)
-#endif
 constexpr int GELU_NT8 = 4096;
 __device__ __forceinline__ void gelu_t8_tab_init(float* __restrict__ tab, int tid, int nthreads) {
   constexpr double h = 2.0 * (double)GELU_XMAX / (double)GELU_NT8;
@@ -829,7 +826,7 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
     }
     // the 8 table reads issued together, consumed after a scheduling fence (left to the
     // scheduler, each read was awaited right behind its own issue)
-    if constexpr (OUT8 && SR_F8_GELU_NEAREST) {  // nearest node of the 4,097-entry fp32 table
+    if constexpr (OUT8) {  // nearest node of the 4,097-entry fp32 table
       const float* const t8 = reinterpret_cast<const float*>(gtab);
       float tn[8];
 #pragma unroll
@@ -858,8 +855,6 @@ __device__ __forceinline__ void store_tile_gelu(float4v (&acc)[8][4], int nw0, i
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       v[r] *= fmaf(fr[r], tv[r].y, tv[r].x);
-      // e4m3: 2 GELU >= -0.34, so only the upper saturation bound can apply (e4m3x4's clamp)
-      if constexpr (OUT8) v[r] = fminf(v[r], 448.f);
       asm("" : "+v"(v[r]));
     }
   };
@@ -1078,11 +1073,14 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
   constexpr bool LNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
   static_assert(LNR || EPI == EPI_RES16_STATS || EPI == EPI_RES16_STATS_Y8, "store_tile_res: residual epilogues");
   static_assert(PERM, "store_tile_res: the W tile staged in perm32 order (8 consecutive columns per lane)");
-  const int g = lane >> 4, odd = g & 1;
-  const int clane = ln0 + 16 * odd + 4 * (g & 2);  // the lane's column in the tile's table (+ 32 p)
-  // lane-constant byte offsets: the residual segment of row (lane & 15) (+ 64 B per column group),
-  // the scratch write / read-back and the row-group store offsets of store_tile_gelu
+  // (the lane recomputed here: the caller's copy, live across the K-loop, was spilled at 256 VGPRs
+  // and its reload's vmcnt(0) waited for the epilogue's residual loads)
+  (void)lane;
   const int lid = lane_id_here();
+  const int g = lid >> 4, odd = g & 1;
+  const int clane = ln0 + 16 * odd + 4 * (g & 2);  // the lane's column in the tile's table (+ 32 p)
+  // lane-constant byte offsets: the residual segment of row (lid & 15) (+ 64 B per column group),
+  // the scratch write / read-back and the row-group store offsets of store_tile_gelu
   const uint32_t bo_res = (uint32_t)(((lid & 15) * (int)ldr + 16 * ((lid >> 4) & 1) + 4 * ((lid >> 4) & 2)) * 2);
   const uint32_t wofs = (uint32_t)((lid & 15) * 128 + (((2 * ((lid >> 4) & 1) + (lid >> 5)) ^ (lid & 7)) << 4));
   const uint32_t rofs = (uint32_t)((lid >> 3) * 128 + (((lid & 7) ^ (lid >> 3)) << 4));
@@ -1130,7 +1128,7 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
     if (st < 7) load_res((st & 1) ? rA : rB, st + 1);
     float mu = 0.f, rstd = 1.f;
     if constexpr (LNR) {
-      const float2 mr = *reinterpret_cast<const float2*>(cst + 512 + 2 * (lm0 + j * 16 + (lane & 15)));
+      const float2 mr = *reinterpret_cast<const float2*>(cst + 512 + 2 * (lm0 + j * 16 + (lid & 15)));
       mu = mr.x;
       rstd = mr.y;
     }
@@ -1169,7 +1167,7 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
       park_q = mine ? hq : park_q;
       park_nc = mine ? nc : park_nc;
     } else {
-      nc = __shfl(park_nc, (lane & 15) + 16 * j, 64);
+      nc = __shfl(park_nc, (lid & 15) + 16 * j, 64);
       half_span_stats<false>(hv[0], hv[1], nc, hs, hq);
     }
     // read back as 8 rows x 128 B per instruction and store (rows past M dropped by the range)
@@ -1197,10 +1195,10 @@ __device__ __forceinline__ void store_tile_res(float4v (&acc)[8][4], int nw0, in
 #endif
     }
     if (h == 1) {
-      const float2 sm = span_stats(nc, __shfl(park_s, (lane & 15) + 16 * j, 64), __shfl(park_q, (lane & 15) + 16 * j, 64),
+      const float2 sm = span_stats(nc, __shfl(park_s, (lid & 15) + 16 * j, 64), __shfl(park_q, (lid & 15) + 16 * j, 64),
                                    hs, hq);
       const float sum = sm.x, m2 = sm.y;
-      const int m_row = row0 + (lane & 15);
+      const int m_row = row0 + (lid & 15);
       if (g == 0 && (!CHECK || m_row < M)) {
         float2 stv;
         stv.x = sum;
@@ -1428,7 +1426,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   constexpr bool GLUT = (DIAG == 0 || DIAG == 5 || DIAG == 6 || DIAG == 7 || STAMP) &&
                         (EPI == EPI_LNF_GELU_F16 || EPI == EPI_LNF_GELU_F8);
   // float2 entries (the fp8 FFN1's nearest-node table: GELU_NT8 + 1 floats)
-  constexpr int GTAB = (EPI == EPI_LNF_GELU_F8 && SR_F8_GELU_NEAREST) ? (GELU_NT8 + 2) / 2 : GELU_NT + 1;
+  constexpr int GTAB = (EPI == EPI_LNF_GELU_F8) ? (GELU_NT8 + 2) / 2 : GELU_NT + 1;
   // PERMW: the W tile's rows are staged in perm32 order (wide epilogues only: the scan epilogue
   // and the 32-bit-output epilogues index the rows as staged)
   constexpr bool PERMW = PipeEpi<EPI>::WIDE && !SCAN && (DIAG == 0 || DIAG >= 5);
@@ -1613,7 +1611,7 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
     for (int q = tid; q < 256; q += blockDim.x) tau_lds[q] = q < M ? bias[q] : INFINITY;
   }
   if constexpr (GLUT) {  // published by the prologue's barrier
-    if constexpr (EPI == EPI_LNF_GELU_F8 && SR_F8_GELU_NEAREST)
+    if constexpr (EPI == EPI_LNF_GELU_F8)
       gelu_t8_tab_init(reinterpret_cast<float*>(gtab), tid, blockDim.x);
     else
       gelu_t_tab_init(gtab, tid, blockDim.x);

@@ -21,6 +21,16 @@ for P in ${PARTS//,/ }; do
             echo "== $(basename $D) r$r" >> gpurun_out/$TAG/f8ab.log
             SUPER_RAG_AMD_DIAG_LIB=$D timeout -k 10 200 python -u tools/ffn1_bench.py --f8 --M 1638400 --diags 0 --rounds 2 >> gpurun_out/$TAG/f8ab.log 2>&1 || exit 1
           done; done ;;
+    lnrab) L=$PWD/super-rag_amd/super_rag_amd/lib_ab; V=${VAR:?VAR}
+         SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so timeout -k 10 300 python -u tools/lnr_stamps.py > gpurun_out/$TAG/lnr_stamps_$V.log 2>&1 || exit 1
+         SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so timeout -k 10 300 \
+           python -u -m pytest tests/test_gpu_gemm.py -k stats -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG/stats_$V.log 2>&1 || exit 1
+         SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/$TAG/bench_20x5_$V.log 2>&1 || exit 1 ;;
+    benchab) L=$PWD/super-rag_amd/super_rag_amd/lib_ab
+         for V in ${VARS:?VARS}; do
+           if [ $V = prod ]; then E=""; else E="SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so"; fi
+           env $E timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-extras > gpurun_out/$TAG/benchab_$V.log 2>&1 || exit 1
+         done ;;
     lnrst) timeout -k 10 300 python -u tools/lnr_stamps.py > gpurun_out/$TAG/lnr_stamps.log 2>&1 || exit 1 ;;
     peaks) timeout -k 10 200 python -u -c "import torch, json, bench; print(json.dumps(bench.mfma_rate_peaks(torch.device('cuda', 0))))" > gpurun_out/$TAG/peaks.log 2>&1 || exit 1 ;;
     c3) timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -k config3 -x -v -s --timeout 240 --timeout-method thread > gpurun_out/$TAG/c3.log 2>&1 || exit 1 ;;

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 from super_rag_amd import _native as N  # noqa: E402
 
 
-def run_shape(M, Nn, K, reps, dev):
+def run_shape(M, Nn, K, reps, dev, ldr0=False):
     g = torch.Generator(device=dev).manual_seed(K)
     X = (torch.randn(M, K, device=dev, generator=g) * 0.5).half()
     W = (torch.randn(Nn, K, device=dev, generator=g) * 0.02).half()
@@ -43,8 +43,9 @@ def run_shape(M, Nn, K, reps, dev):
                     mr.data_ptr(), gamma.data_ptr(), Y.data_ptr(), Nn, M, Nn, K, st.data_ptr(), 0, stream)
 
     def stamped():
+        # (ldr0: every row reads the residual of row 0 -- L1 / L2 hits, wrong results: timing only)
         N.call_diag("sr_diag_gemm_lnr_stats_stamps", X.data_ptr(), K, W.data_ptr(), b.data_ptr(), R.data_ptr(),
-                    Nn, mr.data_ptr(), gamma.data_ptr(), Y.data_ptr(), Nn, M, Nn, K, st.data_ptr(),
+                    0 if ldr0 else Nn, mr.data_ptr(), gamma.data_ptr(), Y.data_ptr(), Nn, M, Nn, K, st.data_ptr(),
                     stamps.data_ptr(), 0, stream)
 
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,7 +70,7 @@ def run_shape(M, Nn, K, reps, dev):
     per = s[:, :, 1:6] / tr[..., None]
     nk = int(s[0, 0, 6].item())
     names = ["K-step 0", "K-step 1", "rest of K-loop", "epilogue", "transition"]
-    print(f"M {M} N {Nn} K {K}: product {tf:.1f} TF/s, {nk} K-steps per tile, "
+    print(f"M {M} N {Nn} K {K}{' (residual rows all row 0: timing only)' if ldr0 else ''}: product {tf:.1f} TF/s, {nk} K-steps per tile, "
           f"{tr.mean().item():.1f} tiles per wave", flush=True)
     for grp, sl in (("all", slice(0, 8)), ("group 0", slice(0, 4)), ("group 1", slice(4, 8))):
         m = per[:, sl, :].mean(dim=(0, 1))
@@ -86,6 +87,7 @@ def main():
     dev = torch.device("cuda", 0)
     for K in (768, 3072):
         run_shape(a.M, 768, K, a.reps, dev)
+    run_shape(a.M, 768, 768, a.reps, dev, ldr0=True)
 
 
 if __name__ == "__main__":
