@@ -300,6 +300,8 @@ void Encoder::ensure_ws(int64_t tokens, int B) {
   y32_.reserve((size_t)tokens * d * sizeof(float));
   ffn_.reserve((size_t)tokens * F * sizeof(half_t));
   u8_.reserve((size_t)tokens * d);
+  // split-K partial tiles of the short-M GEMMs (launch_gemm: LnFold.chunk_ws), a fixed 64 MiB
+  if (!fold_enabled()) chunk_ws_.reserve(kChunkWsBytes);
   if (cfg_.residual_fp16) {
     statA_.reserve((size_t)tokens * (d / 128 + 1) * 2 * sizeof(float));
     statB_.reserve((size_t)tokens * (d / 128 + 1) * 2 * sizeof(float));
@@ -513,6 +515,8 @@ void Encoder::forward_dev(const int32_t* ids, const int32_t* mask, const int32_t
                    const void* R, int64_t ldr, void* Y, int64_t ldy, int Mm, int Nn, int Kx) {
       LnFold lx;
       lx.x_k = split_ ? Kx : 0;
+      lx.chunk_ws = chunk_ws_.as<float>();
+      lx.chunk_ws_bytes = (int64_t)chunk_ws_.bytes;
       launch_gemm(epi, X, lda, W, b, R, ldr, Y, ldy, Mm, Nn, kr * Kx, s, &lx);
     };
     for (size_t l = 0; l < (fold ? 0 : layers_.size()); ++l) {

@@ -2113,13 +2113,27 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(
     PipeEpi<EPI>::template run<true>(acc, nw0, mw0, lane, M, N, bias, R, ldr, Y, ldy, lf);
 }
 
+// K-chunked accumulation of the 128 x 128 kernel (GEMM_SMALL, the embedders' GEMMs): the K-steps
+// form chunks of KCHUNK, each chunk's MFMA chain starts from zero and the chunk sums are added in
+// chunk order into an fp32 total.  With few tiles (a short M: the query embeddings of drop-in
+// requests, M = 32-1,024 rows, where one tile's serial K-loop of up to 96 K-steps was the whole
+// GEMM's time) the chunks run in separate workgroups (split-K, blockIdx.y = a group of cpg
+// chunks) that store their partial tiles to `part`, and gemm_chunk_reduce_kernel adds them in the
+// same order before the same epilogue: the outputs are bit-identical either way, so an embedding
+// never depends on the batch it was coalesced into.
+constexpr int KCHUNK = 6;
+constexpr int64_t kSplitMaxTiles = 128;  // split only below half a workgroup per CU slot pair
+
 template <int EPI, int BN, int BM, int WN, int WM, bool PERSIST>
 __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) void gemm_f16_kernel(
     const half_t* __restrict__ X, int64_t lda, const half_t* __restrict__ W,
     const float* __restrict__ bias, const void* __restrict__ R, int64_t ldr,
-    void* __restrict__ Y, int64_t ldy, int M, int N, int K, int kxs) {
+    void* __restrict__ Y, int64_t ldy, int M, int N, int K, int kxs, float4v* __restrict__ part,
+    int cpg, int kchunk) {
   constexpr int WAVES = WN * WM;
   constexpr int FN = BN / WN / 16, FM = BM / WM / 16;  // 16x16 tiles per wave
+  // (the 256 x 256 form keeps one chain: a second 128-VGPR set does not fit; host: no split)
+  constexpr bool CHUNKED = FN * FM <= 16 && !PERSIST;
   constexpr int NIA = BN / 8 / WAVES, NIB = BM / 8 / WAVES;
   constexpr int STAGE = (BN + BM) * GBK;  // halfs per stage
   static_assert(NIA * WAVES * 8 == BN && NIB * WAVES * 8 == BM, "tile/wave mismatch");
@@ -2148,50 +2162,87 @@ __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) vo
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (LDS-DMA base in M0)
   const int wn = wave / WM, wm = wave % WM;
-  const int nk = K / GBK;
+  // K-steps [kb, ke) of this workgroup: all of them, or chunks [cpg y, cpg (y + 1)) (split);
+  // kchunk = 0: one chunk (the callers that did not ask for chunked sums: plain accumulation)
+  int kb = 0, ke = K / GBK;
+  if (CHUNKED && part != nullptr) {
+    kb = (int)blockIdx.y * cpg * kchunk;
+    ke = min(ke, kb + cpg * kchunk);
+  }
+  const int kstride = CHUNKED && kchunk > 0 ? kchunk : ke;
 
   // stage buffer b: W tile (BN rows) at lds + b*STAGE, X tile (BM rows) right after it.
   if (t < t_end) {
-    stage_tile<NIA>(W, K, n0, N, 0, lds, wave, lane);
-    stage_tile<NIB>(X, lda, m0, M, 0, lds + BN * GBK, wave, lane);
+    const int kx = kb >= kxs ? kb - kxs : kb;
+    stage_tile<NIA>(W, K, n0, N, kb * GBK, lds, wave, lane);
+    stage_tile<NIB>(X, lda, m0, M, kx * GBK, lds + BN * GBK, wave, lane);
   }
   __syncthreads();
 
   for (; t < t_end; t += t_step) {
-  float4v acc[FN][FM];
+  float4v acc[FN][FM], tot[CHUNKED ? FN : 1][CHUNKED ? FM : 1];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const half_t* As = lds + cur * STAGE;
-    const half_t* Bs = As + BN * GBK;
-    if (kt + 1 < nk) {
-      half_t* An = lds + (cur ^ 1) * STAGE;
-      const int kx = kt + 1 >= kxs ? kt + 1 - kxs : kt + 1;   // split weights: X repeats
-      stage_tile<NIA>(W, K, n0, N, (kt + 1) * GBK, An, wave, lane);
-      stage_tile<NIB>(X, lda, m0, M, kx * GBK, An + BN * GBK, wave, lane);
+  // (chunks as an outer loop: the chunk-end work stays out of the K-step loop's body)
+  for (int c0 = kb; c0 < ke; c0 += kstride) {
+    const int c1 = min(ke, c0 + kstride);
+    for (int kt = c0; kt < c1; ++kt) {
+      const int cur = (kt - kb) & 1;
+      const half_t* As = lds + cur * STAGE;
+      const half_t* Bs = As + BN * GBK;
+      if (kt + 1 < ke) {
+        half_t* An = lds + (cur ^ 1) * STAGE;
+        const int kx = kt + 1 >= kxs ? kt + 1 - kxs : kt + 1;   // split weights: X repeats
+        stage_tile<NIA>(W, K, n0, N, (kt + 1) * GBK, An, wave, lane);
+        stage_tile<NIB>(X, lda, m0, M, kx * GBK, An + BN * GBK, wave, lane);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        half8 a[FN], b[FM];
+        const int chunk = (lane >> 4) + 4 * s;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) a[i] = read_frag(As, wn * (BN / WN) + i * 16 + (lane & 15), chunk);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) b[j] = read_frag(Bs, wm * (BM / WM) + j * 16 + (lane & 15), chunk);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      __syncthreads();
     }
+    if constexpr (CHUNKED) {  // a chunk ends: into the total, or stored (split)
+      if (part != nullptr) {
+        const int c = c0 / kchunk;
+        float4v* pt = part + ((int64_t)(c * (int)(gridDim.x) + t) * WAVES + wave) * (FN * FM * 64) + lane;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      half8 a[FN], b[FM];
-      const int chunk = (lane >> 4) + 4 * s;
+        for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int i = 0; i < FN; ++i) a[i] = read_frag(As, wn * (BN / WN) + i * 16 + (lane & 15), chunk);
+          for (int j = 0; j < FM; ++j) pt[(i * FM + j) * 64] = acc[i][j];
+      } else if (c0 == kb) {  // (the first chunk is copied: kchunk = 0 stays plain accumulation)
 #pragma unroll
-      for (int j = 0; j < FM; ++j) b[j] = read_frag(Bs, wm * (BM / WM) + j * 16 + (lane & 15), chunk);
-      __builtin_amdgcn_s_setprio(1);
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) tot[i][j] = acc[i][j];
+      } else {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) tot[i][j] += acc[i][j];
+      }
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+        for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
     }
-    __syncthreads();
   }
+  if (CHUNKED && part != nullptr) return;  // (split: gemm_chunk_reduce_kernel runs the epilogue)
 
   // Next tile: its first K-step lands in buffer 0 while this tile's epilogue runs (every LDS read
   // of this tile finished before the K-loop's last barrier).
@@ -2202,8 +2253,12 @@ __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) vo
     stage_tile<NIB>(X, lda, m0_next, M, 0, lds + BN * GBK, wave, lane);
   }
 
-  store_tile<EPI, FN, FM>(acc, n0 + wn * (BN / WN), m0 + wm * (BM / WM), lane, M, bias, R, ldr, Y,
-                          ldy);
+  if constexpr (CHUNKED)
+    store_tile<EPI, FN, FM>(tot, n0 + wn * (BN / WN), m0 + wm * (BM / WM), lane, M, bias, R, ldr, Y,
+                            ldy);
+  else
+    store_tile<EPI, FN, FM>(acc, n0 + wn * (BN / WN), m0 + wm * (BM / WM), lane, M, bias, R, ldr, Y,
+                            ldy);
   if constexpr (PERSIST) {
     __syncthreads();  // next tile's first K-step has landed in buffer 0
     m0 = m0_next;
@@ -2212,15 +2267,44 @@ __global__ __launch_bounds__(64 * WN * WM, (WN * WM > 8) ? (WN * WM) / 4 : 2) vo
   }  // tile loop
 }
 
+// The split-K epilogue of the 128 x 128 kernel: tile blockIdx.x's chunk partials summed in chunk
+// order (the unsplit kernel's total, operation for operation), then its epilogue.
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_chunk_reduce_kernel(
+    const float4v* __restrict__ part, int nchunk, const float* __restrict__ bias,
+    const void* __restrict__ R, int64_t ldr, void* __restrict__ Y, int64_t ldy, int M, int N) {
+  const int t = blockIdx.x, tiles_n = N / 128;
+  const int m0 = (t / tiles_n) * 128, n0 = (t % tiles_n) * 128;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float4v acc[4][4];
+  const float4v* p0 = part + ((int64_t)t * 4 + wave) * (16 * 64) + lane;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = p0[(i * 4 + j) * 64];
+  for (int c = 1; c < nchunk; ++c) {
+    const float4v* pt = part + ((int64_t)(c * (int)gridDim.x + t) * 4 + wave) * (16 * 64) + lane;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += pt[(i * 4 + j) * 64];
+  }
+  store_tile<EPI, 4, 4>(acc, n0 + (wave >> 1) * 64, m0 + (wave & 1) * 64, lane, M, bias, R, ldr, Y, ldy);
+}
+
 template <int BN, int BM, int WN, int WM, bool PERSIST>
 void launch_tile(int epi, dim3 grid, hipStream_t stream, const half_t* X, int64_t lda,
                  const half_t* W, const float* bias, const void* R, int64_t ldr, void* Y,
-                 int64_t ldy, int M, int N, int K, int kxs) {
+                 int64_t ldy, int M, int N, int K, int kxs, float4v* part = nullptr, int cpg = 0,
+                 int kchunk = 0) {
   const dim3 block(64 * WN * WM);
 #define SR_GEMM_CASE(E)                                                                        \
   case E:                                                                                      \
     hipLaunchKernelGGL((gemm_f16_kernel<E, BN, BM, WN, WM, PERSIST>), grid, block, 0, stream, \
-                       X, lda, W, bias, R, ldr, Y, ldy, M, N, K, kxs);                         \
+                       X, lda, W, bias, R, ldr, Y, ldy, M, N, K, kxs, part, cpg, kchunk);      \
+    if (part != nullptr)                                                                       \
+      hipLaunchKernelGGL((gemm_chunk_reduce_kernel<E>), dim3(grid.x), dim3(256), 0, stream,    \
+                         part, (int)ceil_div(K / GBK, KCHUNK), bias, R, ldr, Y, ldy, M, N);     \
     break;
   switch (epi) {
     SR_GEMM_CASE(EPI_BIAS_F16)
@@ -2705,8 +2789,21 @@ void launch_gemm_variant(int variant, int epi, const half_t* X, int64_t lda, con
   } else {
     const int64_t tiles = (int64_t)(N / 128) * ceil_div(M, 128);
     SR_CHECK(tiles < (1ll << 31), "gemm: too many tiles");
-    launch_tile<128, 128, 2, 2, false>(epi, dim3((unsigned)tiles), stream, X, lda, W, bias, R,
-                                       ldr, Y, ldy, M, N, K, x_k / GBK);
+    // split-K over the K chunks (see KCHUNK) when the tiles alone leave the CUs idle and the
+    // caller lent a workspace for the partial tiles (64 KiB per tile and chunk): chunk groups of
+    // cpg chunks, about 512 workgroups in all
+    const int64_t nchunk = ceil_div(K / GBK, KCHUNK);
+    int64_t groups = 1, cpg = 0;
+    if (lf && lf->chunk_ws && nchunk >= 2 && tiles <= kSplitMaxTiles &&
+        nchunk * tiles * 65536 <= lf->chunk_ws_bytes) {
+      cpg = ceil_div(nchunk, std::min<int64_t>(nchunk, ceil_div(512, tiles)));
+      groups = ceil_div(nchunk, cpg);
+    }
+    // (chunked sums only for the callers that lent a workspace: the same chunks split or not)
+    launch_tile<128, 128, 2, 2, false>(epi, dim3((unsigned)tiles, (unsigned)groups), stream, X, lda, W,
+                                       bias, R, ldr, Y, ldy, M, N, K, x_k / GBK,
+                                       cpg ? reinterpret_cast<float4v*>(lf->chunk_ws) : nullptr, (int)cpg,
+                                       lf && lf->chunk_ws ? KCHUNK : 0);
   }
   SR_LAUNCH_CHECK();
 }

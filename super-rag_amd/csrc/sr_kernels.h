@@ -55,6 +55,8 @@ struct LnFold {
   int x_k = 0;                     // split weights: X has x_k columns and K = 2 x_k; the K-steps
                                    // past x_k re-read X from k = 0, so W = [W_hi | W_lo] (N x 2 x_k)
                                    // gives X W_hi^T + X W_lo^T in one fp32 accumulation (0 = K)
+  float* chunk_ws = nullptr;        // GEMM_SMALL (128 x 128, short M): workspace for split-K
+  int64_t chunk_ws_bytes = 0;      // partial tiles (k_gemm.hip KCHUNK); null: never split
   // EPI_SCAN(8) re-uses the fields (kernel-argument SGPRs are scarce in the persistent kernels):
   // stat_out = per-query candidate counts (int*), stat_ld = global row id of the chunk's first
   // row; bias = tau[B], R = live flags of the chunk, Y = candidate keys [B][cap] (ldy = cap).

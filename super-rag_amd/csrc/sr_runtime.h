@@ -231,6 +231,8 @@ class Encoder {
   bool split_ = false;
   DevBuf u8_;  // e4m3 copy of the residual sums (fp8 modes 2 / 3) or normalised rows (mode 4)
   DevBuf unit_mr_;  // (mu, rstd) = (0, 1): fp8 mode 4 QKV statistics (stat_ld 0)
+  static constexpr size_t kChunkWsBytes = size_t(64) << 20;
+  DevBuf chunk_ws_;  // split-K partial tiles of the unfolded (embedder) GEMMs at short M
   int64_t ws_tokens_ = 0;
 };
 

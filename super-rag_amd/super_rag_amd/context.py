@@ -32,6 +32,18 @@ class ContextManager:
         import asyncio
         return (await asyncio.to_thread(conn.search, query_embedding, **kw)).results
 
+    async def aquery_text(self, query, score_threshold=0.5, topk=3, index_types=None, chat_id=None):
+        """aquery without a precomputed vector, when the connector can embed and search the
+        query in one coalesced step (MI355XVectorStoreConnector.asearch_text); otherwise aquery.
+        Same results."""
+        conn = self.adaptor.connector
+        if not (hasattr(conn, "asearch_text") and conn.can_fuse_embed(self.embedding_model)):
+            return await self.aquery(query, score_threshold=score_threshold, topk=topk,
+                                     index_types=index_types, chat_id=chat_id)
+        filter_condition = self._create_combined_filter(index_types, chat_id)
+        return (await conn.asearch_text(query, self.embedding_model, topk,
+                                        score_threshold=score_threshold, filter=filter_condition)).results
+
     def _search_args(self, query, score_threshold, topk, vector, index_types, chat_id):
         filter_condition = self._create_combined_filter(index_types, chat_id)
         query_embedding = QueryWithEmbedding(query=query, top_k=topk, embedding=vector)

@@ -204,12 +204,12 @@ class VectorSearchService:
             cm = ContextManager(name, embedding_model, VECTOR_DB_TYPE, ctx)
 
             # The reference runs these synchronously on the event loop (vector_search.py:76-86);
-            # here the coalesced embed and search await their shared device batches (coalesce.py)
-            # without holding a thread, so the loop stays free and concurrent requests batch.
-            # Same calls, same results.
-            vector = await embedding_model.aembed_query(query)
-            results = await cm.aquery(query, score_threshold=similarity_threshold, topk=top_k,
-                                      vector=vector, index_types=["vector"], chat_id=chat_id)
+            # here the query is embedded and searched as one coalesced device step
+            # (ContextManager.aquery_text: concurrent requests share one embed batch and one
+            # search batch) awaited without holding a thread, so the loop stays free and
+            # concurrent requests batch.  Same calls, same results.
+            results = await cm.aquery_text(query, score_threshold=similarity_threshold, topk=top_k,
+                                           index_types=["vector"], chat_id=chat_id)
             for item in results:
                 if item.metadata is None:
                     item.metadata = {}

@@ -132,6 +132,7 @@ class _Collection:
         self.metadatas: List[Optional[dict]] = []
         self.lock = threading.RLock()
         self.coalescer = None   # created on first coalesced search (coalesce.py)
+        self.text_coalescers: Dict[int, Any] = {}  # encoder id -> fused embed + search batches
         self.version = 0        # bumped on every add / delete / compaction
         # filter -> (version, mask_key, allow mask): a small LRU (each mask is n_rows bytes)
         self.masks: "OrderedDict[str, tuple]" = OrderedDict()
@@ -426,6 +427,55 @@ class MI355XVectorStoreConnector:
         thr = kwargs.get("score_threshold") if self.honor_score_threshold else None
         results = await self._coalescer(c).acall((q, int(query.top_k), flt))
         return QueryResult(query=query.query, results=self._threshold(results, thr))
+
+    def can_fuse_embed(self, embedding_model) -> bool:
+        """Whether asearch_text applies: a coalescing dense connector and this package's
+        coalescing EmbeddingService (its encoder and tokenizer in this process)."""
+        # (SUPER_RAG_AMD_FUSE_EMBED_SEARCH=0: the two coalesced steps, for A/B measurements)
+        if os.environ.get("SUPER_RAG_AMD_FUSE_EMBED_SEARCH", "1") == "0":
+            return False
+        return (self.coalesce and not self.hybrid and bool(getattr(embedding_model, "coalesce", False))
+                and getattr(embedding_model, "encoder", None) is not None
+                and getattr(embedding_model, "tokenizer", None) is not None
+                and hasattr(type(embedding_model), "_embed_with"))
+
+    async def asearch_text(self, text: str, embedding_model, top_k: int, **kwargs):
+        """embed_query + search of one request as ONE coalesced step: concurrent requests' query
+        texts are embedded in one device batch and searched in one device batch, back to back,
+        by the same leader (instead of an embed batch and then a separate search batch, whose
+        coalescers each saw about half the requests in flight).  Same embedding bits (the encoder's
+        outputs do not depend on the batch: k_gemm.hip KCHUNK), same search, same errors
+        (EmptyTextError before anything runs, BatchProcessingError for a failed device batch)."""
+        from .errors import EmptyTextError
+        if not text or not text.strip():
+            raise EmptyTextError(1)
+        c = _get(self.collection_name)
+        if c is None or top_k is None or top_k <= 0:
+            await embedding_model.aembed_query(text)
+            return QueryResult(query=text, results=[])
+        flt = kwargs.get("filter") if self.honor_filter else None
+        thr = kwargs.get("score_threshold") if self.honor_score_threshold else None
+        item = (text.replace("\n", " "), int(top_k), flt)
+        results = await self._text_coalescer(c, embedding_model).acall(item)
+        return QueryResult(query=text, results=self._threshold(results, thr))
+
+    def _text_coalescer(self, c, em):
+        key = id(em.encoder)
+        co = c.text_coalescers.get(key)
+        if co is None:
+            with c.lock:
+                co = c.text_coalescers.get(key)
+                if co is None:
+                    from .coalesce import Coalescer
+                    enc, tok, dev_b = em.encoder, em.tokenizer, em.device_batch
+                    embed_with = type(em)._embed_with
+
+                    def run(items, c=c):
+                        vecs = embed_with(enc, tok, dev_b, [t for t, _, _ in items])
+                        return self._search_batch(c, [(vecs[i], k, flt) for i, (_, k, flt) in enumerate(items)])
+                    co = Coalescer(run, max_batch=min(self.max_batch, dev_b))
+                    c.text_coalescers[key] = co
+        return co
 
     def _coalescer(self, c):
         if c.coalescer is None:

@@ -302,6 +302,60 @@ def test_async_paths_equal_the_sync_ones():
         V.set_store_backend(V._native_store, V._native_load)
 
 
+def test_fused_embed_search_equals_embed_then_search():
+    """ContextManager.aquery_text (the flow's vector search: one coalesced embed + search step,
+    MI355XVectorStoreConnector.asearch_text) returns what aembed_query + aquery return, for
+    concurrent requests with mixed top_k, batches them, and keeps the empty-query error; a
+    connector that cannot fuse (not coalescing) falls back to the two-step path."""
+    import asyncio
+    from super_rag_amd import vectorstore as V
+    from super_rag_amd.context import ContextManager
+    from super_rag_amd.embed import EmbeddingService
+    from super_rag_amd.errors import EmptyTextError
+    from super_rag_amd.models import TextNode
+    V.set_store_backend(lambda dim, dev: NumpyStore(dim, dev), NumpyStore.load)
+    V._collections.clear()
+    try:
+        tok = TextTokenizer()
+        enc = HashEncoder(tok, 16)
+        emb = EmbeddingService("openai", "BAAI/bge-m3", "", "", 10, encoder=enc, tokenizer=tok)
+        ctx = {"collection": "fused", "coalesce": True, "max_batch": 16}
+        conn = V.MI355XVectorStoreConnector(dict(ctx))
+        rng = np.random.default_rng(2)
+        conn.store.add([TextNode(text=f"passage {i}", metadata={"i": i},
+                                 embedding=rng.standard_normal(16).tolist()) for i in range(400)])
+        cm = ContextManager("fused", emb, "mi355x", dict(ctx))
+        queries = [f"query {i}\nline two" if i % 5 == 0 else f"query {i}" for i in range(60)]
+
+        async def two_step(q):
+            v = await emb.aembed_query(q)
+            docs = await cm.aquery(q, topk=1 + i_of[q] % 9, vector=v, index_types=["vector"])
+            return [(d.text, d.score) for d in docs]
+
+        async def fused(q):
+            docs = await cm.aquery_text(q, topk=1 + i_of[q] % 9, index_types=["vector"])
+            return [(d.text, d.score) for d in docs]
+
+        i_of = {q: i for i, q in enumerate(queries)}
+
+        async def run_all(fn):
+            return await asyncio.gather(*[fn(q) for q in queries])
+
+        want = asyncio.run(run_all(two_step))
+        got = asyncio.run(run_all(fused))
+        assert got == want
+        co = list(V._collections["fused"].text_coalescers.values())
+        assert len(co) == 1 and co[0].items == len(queries) and co[0].batches < len(queries)
+        with pytest.raises(EmptyTextError):
+            asyncio.run(cm.aquery_text("  ", topk=3))
+        solo = ContextManager("fused", emb, "mi355x", {"collection": "fused", "coalesce": False})
+        assert asyncio.run(solo.aquery_text(queries[3], topk=4, index_types=["vector"])) == \
+            asyncio.run(cm.aquery(queries[3], topk=4, index_types=["vector"]))
+    finally:
+        V._collections.clear()
+        V.set_store_backend(V._native_store, V._native_load)
+
+
 def test_thread_caller_does_not_serve_coroutines_after_its_own_batch():
     """A thread caller that leads a batch hands the coroutines queued behind it to the coalescer's
     own leader thread: it returns after its own batch instead of running theirs."""

@@ -73,6 +73,23 @@ def test_bge_base_shape_embedding_tolerance():
     assert err.max() <= 1e-3, err
 
 
+def test_bge_base_embedding_independent_of_batch_split_k():
+    # Short M runs the embedder's GEMMs split over K chunks (k_gemm.hip KCHUNK: partial tiles +
+    # gemm_chunk_reduce_kernel), long M unsplit with the same chunked sums: a query's embedding is
+    # bit-identical alone, in a small batch (some GEMMs split, some not) and in a large one (none
+    # split: M = 300 x 32 rows gives >= 450 tiles per GEMM).
+    from super_rag_amd.encoder import MODELS, Encoder, random_weights
+    spec = MODELS["bge-base-en"]
+    w = random_weights(spec, seed=7, style="test")
+    enc = Encoder(spec, weights=w)
+    ids, mask = _batch(spec, 300, 32, seed=4)
+    full = enc.embed(ids, mask)
+    for b in (1, 3, 8, 21, 32):
+        np.testing.assert_array_equal(enc.embed(ids[:b], mask[:b]), full[:b])
+    ref = R.embed(_ref_cfg(spec), w, ids[:3], mask[:3])
+    assert _rel(full[:3], ref).max() <= 1e-3
+
+
 @pytest.mark.parametrize("res16", [False, True])
 @pytest.mark.parametrize("S", [16, 64, 130])
 def test_tiny_cross_encoder(S, res16):

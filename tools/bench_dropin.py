@@ -171,6 +171,8 @@ def _coalescers():
     for col in list(V._collections.values()):
         if col.coalescer is not None:
             out["search"] = col.coalescer
+        for co in list(getattr(col, "text_coalescers", {}).values()):
+            out["embed_search"] = co
     return out
 
 

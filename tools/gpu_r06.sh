@@ -11,6 +11,21 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$T
 for P in ${PARTS//,/ }; do
   case $P in
     stats) timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm.py -k "stats" -v -s --timeout 240 --timeout-method thread > gpurun_out/$TAG/stats.log 2>&1 || exit 1 ;;
+    embedsm) for B in ${EMB_B:-1 8 32 256}; do
+               timeout -k 10 200 python -u tools/embed_profile.py --batch $B --reps 30 > gpurun_out/$TAG/embed_profile_b$B.json 2> gpurun_out/$TAG/embed_profile_b$B.err || exit 1
+             done ;;
+    enct) timeout -k 10 400 python -u -m pytest tests/test_gpu_encoder.py -x -v --timeout 300 --timeout-method thread > gpurun_out/$TAG/enc_tests.log 2>&1 || exit 1 ;;
+    embedab) L=$PWD/super-rag_amd/super_rag_amd/lib_ab
+         for V in ${VARS:?VARS}; do for B in ${EMB_B:-8 256}; do
+           if [ $V = prod ]; then E=""; else E="SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so"; fi
+           env $E timeout -k 10 200 python -u tools/embed_profile.py --batch $B --reps 30 > gpurun_out/$TAG/embed_${V}_b$B.json 2> gpurun_out/$TAG/embed_${V}_b$B.err || exit 1
+         done; done ;;
+    dmp) L=$PWD/super-rag_amd/super_rag_amd/lib_ab
+         for V in ${VARS:?VARS}; do
+           if [ $V = prod ]; then E=""; else E="SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so"; fi
+           env $E DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=${DROPIN_ROWS:-10000000} DROPIN_OUT=gpurun_out/$TAG/dmp_$V \
+             timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
+         done ;;
     embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
     xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
              echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
