@@ -1449,12 +1449,12 @@ __global__ __launch_bounds__(512, 2) void gemm_pipe_kernel(
   // RHALF: the persistent residual + statistics epilogues in half-tile order (store_tile_res): a
   // 2 KiB line scratch per wave and the same 4 KiB constants table ([256 bias][256 gamma][256 x
   // (mu, rstd)]; RES16: the bias only), the next tile's staging issued from inside the epilogue
-  constexpr bool RESEPI = EPI == EPI_RES16_STATS || EPI == EPI_LNR16_STATS || EPI == EPI_RES16_STATS_Y8 ||
-                          EPI == EPI_LNR16_STATS_Y8;
   constexpr bool RLNR = EPI == EPI_LNR16_STATS || EPI == EPI_LNR16_STATS_Y8;
-  // (EPI_LNR16_STATS on fp16 operands only: the RES16 and fp8-operand instantiations spilled
-  // 12-36 B in this form, RES16 measured 907 -> 860 TF/s and the e4m3-copy LNR (fp8 mode 3's
-  // O-projection) 777 -> 761, profiles/r05_res_half/, r05_wexp_lds/)
+  // (EPI_LNR16_STATS on fp16 operands only.  Round 5: the RES16 and fp8-operand instantiations
+  // spilled 12-36 B in this form, profiles/r05_res_half/, r05_wexp_lds/.  Round 6: with the parked
+  // statistics the RES16 and the e4m3-copy LNR (fp8 mode 3's O-projection) fit with no spills, and
+  // measured the same as the old epilogue: config 5 619.6-622.4 vs 620.5-621.0 q/s, config 4
+  // 500.5 vs 500.5 q/s, one box (profiles/r06_res_half_y8/); left as they were.)
   constexpr bool RHALF = EPI == EPI_LNR16_STATS && !F8IN && LINE && PERSIST;
   constexpr bool CSTX = CSTL || RHALF;              // an epilogue constants table in LDS
   constexpr int NCST = CSTL ? 4 : RHALF ? (RLNR ? 4 : 1) : 0;  // its 1 KiB pieces (one per wave)

@@ -26,6 +26,13 @@ for P in ${PARTS//,/ }; do
            env $E DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=${DROPIN_ROWS:-10000000} DROPIN_OUT=gpurun_out/$TAG/dmp_$V \
              timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
          done ;;
+    c5ab) L=$PWD/super-rag_amd/super_rag_amd/lib_ab
+         for V in ${VARS:?VARS}; do
+           if [ $V = prod ]; then E=""; else E="SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so"; fi
+           env $E timeout -k 10 400 python -u bench.py --workload config5 --fp8 3 --steps 10 --warmup 3 --no-extras > gpurun_out/$TAG/c5ab_$V.log 2>&1 || exit 1
+           tail -n 1 gpurun_out/$TAG/c5ab_$V.log >> gpurun_out/$TAG/c5ab_all.jsonl
+         done ;;
+    restests) timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_rerank_fidelity.py tests/test_gpu_rerank_fidelity_v2m3.py tests/test_gpu_configs.py tests/test_gpu_encoder.py -x -q --timeout 300 --timeout-method thread > gpurun_out/$TAG/restests.log 2>&1 || exit 1 ;;
     embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
     xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
              echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
@@ -45,6 +52,7 @@ for P in ${PARTS//,/ }; do
          for V in ${VARS:?VARS}; do
            if [ $V = prod ]; then E=""; else E="SUPER_RAG_AMD_LIB=$L/libsrmi_$V.so SUPER_RAG_AMD_DIAG_LIB=$L/libsrmi_diag_$V.so"; fi
            env $E timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-extras > gpurun_out/$TAG/benchab_$V.log 2>&1 || exit 1
+           tail -n 1 gpurun_out/$TAG/benchab_$V.log >> gpurun_out/$TAG/benchab_all.jsonl
          done ;;
     lnrst) timeout -k 10 300 python -u tools/lnr_stamps.py > gpurun_out/$TAG/lnr_stamps.log 2>&1 || exit 1 ;;
     peaks) timeout -k 10 200 python -u -c "import torch, json, bench; print(json.dumps(bench.mfma_rate_peaks(torch.device('cuda', 0))))" > gpurun_out/$TAG/peaks.log 2>&1 || exit 1 ;;
