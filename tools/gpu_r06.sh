@@ -33,6 +33,13 @@ for P in ${PARTS//,/ }; do
            tail -n 1 gpurun_out/$TAG/c5ab_$V.log >> gpurun_out/$TAG/c5ab_all.jsonl
          done ;;
     restests) timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_rerank_fidelity.py tests/test_gpu_rerank_fidelity_v2m3.py tests/test_gpu_configs.py tests/test_gpu_encoder.py -x -q --timeout 300 --timeout-method thread > gpurun_out/$TAG/restests.log 2>&1 || exit 1 ;;
+    hostcost) timeout -k 10 200 python -u tools/embed_host_cost.py > gpurun_out/$TAG/embed_host_cost.log 2>&1 || exit 1 ;;
+    gilab) for G in ${GILS:-0 0.5}; do
+             SUPER_RAG_AMD_GIL_SWITCH_MS=$G timeout -k 10 400 python -u tools/bench_dropin.py --rows 10000000 --concurrency 64 --seconds 10 \
+               > gpurun_out/$TAG/d1_gil$G.json 2> gpurun_out/$TAG/d1_gil$G.err || exit 1
+             SUPER_RAG_AMD_GIL_SWITCH_MS=$G DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=10000000 DROPIN_DELAY=100 \
+               DROPIN_OUT=gpurun_out/$TAG/dmp_gil$G timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
+           done ;;
     embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
     xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
              echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
