@@ -40,6 +40,12 @@ for P in ${PARTS//,/ }; do
              SUPER_RAG_AMD_GIL_SWITCH_MS=$G DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=10000000 DROPIN_DELAY=100 \
                DROPIN_OUT=gpurun_out/$TAG/dmp_gil$G timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
            done ;;
+    tokab) for T in ${TOKS:-1 0}; do
+             SUPER_RAG_AMD_TOK_SLOW=$T timeout -k 10 400 python -u tools/bench_dropin.py --rows 10000000 --concurrency 64 --seconds 10 \
+               > gpurun_out/$TAG/d1_tok$T.json 2> gpurun_out/$TAG/d1_tok$T.err || exit 1
+             SUPER_RAG_AMD_TOK_SLOW=$T DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=10000000 DROPIN_DELAY=100 \
+               DROPIN_OUT=gpurun_out/$TAG/dmp_tok$T timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
+           done ;;
     embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
     xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
              echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
