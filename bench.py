@@ -226,7 +226,7 @@ class DropinProcs:
             err = open(os.path.join(self.dir, f"p{i}.err"), "w")
             self.procs.append((subprocess.Popen(cmd, stdout=out, stderr=err), out, err))
 
-    def release(self, delay_s=60.0):
+    def release(self, delay_s=90.0):
         with open(self.go + ".tmp", "w") as f:
             json.dump({"start_at": time.time() + delay_s}, f)
         os.replace(self.go + ".tmp", self.go)
@@ -257,6 +257,7 @@ class DropinProcs:
             windows.append({
                 "concurrency_per_proc": c, "callers": c * len(rw), "qps": round(qps, 1),
                 "per_proc_qps": [r["qps"] for r in rw],
+                "per_proc_late_s": [r.get("late_s", 0.0) for r in rw],
                 "p50_ms": round(float(np.percentile(lat, 50)), 1),
                 "p99_ms": round(float(np.percentile(lat, 99)), 1),
                 "mean_ms": round(float(lat.mean()), 1),

@@ -165,11 +165,15 @@ def test_dropin_windows_start_together():
     from tools.bench_dropin import WINDOW_GAP_S, _windows
     t0 = time.time() + 0.3
     seen = []
-    for c in _windows([16, 32], 0.2, t0):
-        seen.append((c, time.time()))
-    assert [c for c, _ in seen] == [16, 32]
+    for c, late in _windows([16, 32], 0.2, t0):
+        seen.append((c, time.time(), late))
+    assert [c for c, _, _ in seen] == [16, 32]
     assert seen[0][1] >= t0 and seen[1][1] >= t0 + 0.2 + WINDOW_GAP_S
-    assert [c for c in _windows([8], 5.0, 0.0)] == [8]
+    assert all(0.0 <= late < 0.2 for _, _, late in seen)
+    assert list(_windows([8], 5.0, 0.0)) == [(8, 0.0)]
+    # a start time already past: the window begins at once and reports how late it is
+    (c, late), = list(_windows([4], 1.0, time.time() - 2.0))
+    assert c == 4 and late >= 2.0
 
 
 def test_config5_workload_section(tmp_path):

@@ -267,14 +267,15 @@ WINDOW_GAP_S = 4.0
 
 
 def _windows(concurrency, seconds: float, start_at: float):
-    """Yield each concurrency at its window's start: with a common start time (several serving
-    processes on one GPU) window i starts at start_at + i (seconds + WINDOW_GAP_S) in every
-    process, so the processes measure every window together."""
+    """Yield (concurrency, seconds late) at each window's start: with a common start time
+    (several serving processes on one GPU) window i starts at start_at + i (seconds +
+    WINDOW_GAP_S) in every process, so the processes measure every window together; a process
+    whose setup overran the start reports how late its window began."""
     for i, c in enumerate(concurrency):
         t = start_at + i * (seconds + WINDOW_GAP_S) if start_at > 0 else 0.0
         if t > time.time():
             time.sleep(t - time.time())
-        yield c
+        yield c, (round(max(0.0, time.time() - t), 2) if start_at > 0 else 0.0)
 
 
 def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup: int = 16,
@@ -302,9 +303,9 @@ def run(rows: int = 100000, concurrency=(64, 256), seconds: float = 15.0, warmup
                "rows": rows, "setup_s": round(setup, 1),
                "collection": ("bulk: rows on the device (NativeStore.add_dev or the headline's store), "
                               f"texts: one of {TEXT_POOL} pooled chunks + the row tag, distinct per row") if bulk else "connector add()",
-               "runs": [measure(c, seconds, col_id, queries,
-                                lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None))
-                        for c in _windows(concurrency, seconds, start_at)],
+               "runs": [dict(measure(c, seconds, col_id, queries,
+                                     lat_out=(f"{lat_out}_c{c}.npy" if lat_out else None)), late_s=late)
+                        for c, late in _windows(concurrency, seconds, start_at)],
                "reference_orchestration_ms_per_query": 5.14}
     finally:
         if store is not None:
