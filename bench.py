@@ -211,6 +211,13 @@ class DropinProcs:
     Closed-loop callers obey Little's law: mean latency = callers / throughput, so N x C callers
     at X q/s wait N C / X on average whatever the batching policy (4 x 64 at ~420 q/s: ~610 ms)."""
 
+    # The serving processes' configuration (a deployment of N serving processes sets it in their
+    # environment): the rerank coalescer waits up to 30 ms for 24 queued requests when it finds
+    # fewer.  With N processes sharing the GPU the wait costs no device time (the others fill it),
+    # and larger rerank batches run more efficiently: 4 x 32 at 415.8 -> 428.9-430.2 q/s with
+    # lower p50 (DESIGN, profiles/r06_fill/).  One process keeps the default (no wait).
+    SERVING_ENV = {"SUPER_RAG_AMD_RERANK_MIN_FILL": "24", "SUPER_RAG_AMD_RERANK_MAX_WAIT_MS": "30"}
+
     def __init__(self, n, rows, seconds, concurrency=(32, 64), script=None):
         import tempfile
         self.dir = tempfile.mkdtemp(prefix="sr_dropin_")
@@ -224,7 +231,8 @@ class DropinProcs:
                    "--go-file", self.go, "--lat-out", os.path.join(self.dir, f"lat{i}")]
             out = open(os.path.join(self.dir, f"p{i}.json"), "w")
             err = open(os.path.join(self.dir, f"p{i}.err"), "w")
-            self.procs.append((subprocess.Popen(cmd, stdout=out, stderr=err), out, err))
+            env = {**os.environ, **self.SERVING_ENV}
+            self.procs.append((subprocess.Popen(cmd, stdout=out, stderr=err, env=env), out, err))
 
     def release(self, delay_s=90.0):
         with open(self.go + ".tmp", "w") as f:
@@ -265,7 +273,7 @@ class DropinProcs:
                 "requests": int(sum(r["requests"] for r in rw)),
                 "seconds": max(r["seconds"] for r in rw),
                 "rerank_mean_batch": [r["coalesced"].get("rerank", {}).get("mean_batch") for r in rw]})
-        return {"procs": len(runs), "windows": windows,
+        return {"procs": len(runs), "windows": windows, "serving_env": dict(self.SERVING_ENV),
                 "note": "closed-loop callers: mean latency = callers / q/s (Little's law)"}
 
     def stop(self):

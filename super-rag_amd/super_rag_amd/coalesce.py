@@ -24,6 +24,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import threading
+import time
 from typing import Any, Callable, List, Sequence
 
 
@@ -56,10 +57,16 @@ def _finish(slots) -> None:
 
 
 class Coalescer:
-    def __init__(self, run_batch: Callable[[Sequence[Any]], List[Any]], max_batch: int = 256):
+    def __init__(self, run_batch: Callable[[Sequence[Any]], List[Any]], max_batch: int = 256,
+                 min_fill: int = 1, max_wait_s: float = 0.0):
         self._run = run_batch
         self.max_batch = max(1, int(max_batch))
+        # fill wait: a leader that finds fewer than min_fill items queued waits up to max_wait_s
+        # for more before running the batch (1 / 0: run at once, the batch-while-busy default)
+        self.min_fill = max(1, int(min_fill))
+        self.max_wait_s = max(0.0, float(max_wait_s))
         self._lock = threading.Lock()
+        self._more = threading.Condition(self._lock)
         self._queue: List[_Slot] = []
         self._busy = False
         self.batches = 0        # number of device batches run (diagnostics)
@@ -73,6 +80,7 @@ class Coalescer:
         slot = _Slot(item)
         with self._lock:
             self._queue.append(slot)
+            self._more.notify()
             if not self._busy:
                 self._busy = True
                 slot.lead = True
@@ -92,6 +100,7 @@ class Coalescer:
         lead = False
         with self._lock:
             self._queue.append(slot)
+            self._more.notify()
             if not self._busy:
                 self._busy = True
                 lead = True
@@ -135,6 +144,13 @@ class Coalescer:
 
     def _lead_one(self, caller: bool = False) -> bool:
         with self._lock:
+            if self.min_fill > 1 and self.max_wait_s > 0 and len(self._queue) < self.min_fill:
+                deadline = time.monotonic() + self.max_wait_s
+                while len(self._queue) < self.min_fill:
+                    rem = deadline - time.monotonic()
+                    if rem <= 0:
+                        break
+                    self._more.wait(rem)
             batch = self._queue[: self.max_batch]
             del self._queue[: self.max_batch]
         try:

@@ -10,6 +10,7 @@ scores exactly as the reference does (:74).
 from __future__ import annotations
 
 import asyncio
+import os
 import logging
 from typing import List, Optional
 
@@ -143,7 +144,9 @@ class RerankService:
             from .coalesce import Coalescer
             enc, dev_b = self.encoder, self.device_batch
             coal = Coalescer(lambda items: RerankService._score_encoded(enc, dev_b, items),
-                             max_batch=max(1, dev_b // 100))
+                             max_batch=max(1, dev_b // 100),
+                             min_fill=int(os.environ.get("SUPER_RAG_AMD_RERANK_MIN_FILL", "1")),
+                             max_wait_s=float(os.environ.get("SUPER_RAG_AMD_RERANK_MAX_WAIT_MS", "0")) * 1e-3)
             setattr(self.encoder, "_encoded_pair_coalescer", coal)
         return coal
 

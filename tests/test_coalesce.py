@@ -302,6 +302,36 @@ def test_async_paths_equal_the_sync_ones():
         V.set_store_backend(V._native_store, V._native_load)
 
 
+def test_coalescer_fill_wait():
+    """min_fill / max_wait_s: a leader that finds fewer than min_fill items waits (up to
+    max_wait_s) for more, so items arriving meanwhile share its batch; alone, it runs once the
+    wait expires.  Results stay per item."""
+    from super_rag_amd.coalesce import Coalescer
+    sizes = []
+
+    def run(items):
+        sizes.append(len(items))
+        return [i * 10 for i in items]
+
+    c = Coalescer(run, max_batch=16, min_fill=4, max_wait_s=2.0)
+    out = {}
+
+    def call(i):
+        out[i] = c(i)
+
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+        time.sleep(0.05)
+    for t in ts:
+        t.join(10)
+    assert out == {i: i * 10 for i in range(4)} and sizes == [4]
+    c2 = Coalescer(run, max_batch=16, min_fill=8, max_wait_s=0.1)
+    t0 = time.monotonic()
+    assert c2(7) == 70
+    assert 0.09 <= time.monotonic() - t0 < 2.0 and sizes[-1] == 1
+
+
 def test_fused_embed_search_equals_embed_then_search():
     """ContextManager.aquery_text (the flow's vector search: one coalesced embed + search step,
     MI355XVectorStoreConnector.asearch_text) returns what aembed_query + aquery return, for

@@ -46,6 +46,16 @@ for P in ${PARTS//,/ }; do
              SUPER_RAG_AMD_TOK_SLOW=$T DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=10000000 DROPIN_DELAY=100 \
                DROPIN_OUT=gpurun_out/$TAG/dmp_tok$T timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
            done ;;
+    fillab) for F in ${FILLS:-1:0 12:10 16:20}; do
+             MF=${F%%:*}; MW=${F##*:}
+             SUPER_RAG_AMD_RERANK_MIN_FILL=$MF SUPER_RAG_AMD_RERANK_MAX_WAIT_MS=$MW DROPIN_PROCS=4 DROPIN_C=32 DROPIN_ROWS=10000000 \
+               DROPIN_DELAY=100 DROPIN_OUT=gpurun_out/$TAG/dmp_fill${MF}_${MW} timeout -k 10 400 bash tools/gpu_dropin_mp.sh || exit 1
+           done ;;
+    fill1) for F in ${FILLS:-1:0 16:20}; do
+             MF=${F%%:*}; MW=${F##*:}
+             SUPER_RAG_AMD_RERANK_MIN_FILL=$MF SUPER_RAG_AMD_RERANK_MAX_WAIT_MS=$MW timeout -k 10 400 python -u tools/bench_dropin.py \
+               --rows 10000000 --concurrency 64 --seconds 10 > gpurun_out/$TAG/d1_fill${MF}_${MW}.json 2> gpurun_out/$TAG/d1_fill${MF}_${MW}.err || exit 1
+           done ;;
     embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
     xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
              echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
