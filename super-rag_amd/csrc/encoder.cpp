@@ -43,8 +43,14 @@ Encoder::Encoder(const sr_encoder_config& cfg, int device) : cfg_(cfg), device_(
 
   const int64_t D = d, F = cfg.intermediate;
   {
-    const char* e = std::getenv("SR_WEIGHT_SPLIT");  // A/B of the precision mode (default on)
-    split_ = !cfg.residual_fp16 && !(e && e[0] == '0');
+    // split weights for the DEEP fp32-residual embedders only: measured against the fp32 oracle
+    // (tools/embed_split_error.py), the 24-layer bge-m3 needs them (1.07e-3 max relative error
+    // without, 5.3e-4 with; bar 1e-3), the 12-layer bge-base does not (6.1e-4 without, 4.1e-4
+    // with) and embeds 1.5x faster without (B = 256: 4.28 -> 2.86 ms).  SR_WEIGHT_SPLIT = 0 / 1
+    // forces the choice.
+    const char* e = std::getenv("SR_WEIGHT_SPLIT");
+    const bool deep = cfg.layers > 12;
+    split_ = !cfg.residual_fp16 && (e && e[0] ? e[0] != '0' : deep);
   }
   const int64_t sk = split_ ? D : 0, skf = split_ ? F : 0;
   register_target("embeddings.word_embeddings.weight", wemb_, (int64_t)cfg.vocab_size * D, true);

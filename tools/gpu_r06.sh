@@ -56,6 +56,7 @@ for P in ${PARTS//,/ }; do
              SUPER_RAG_AMD_RERANK_MIN_FILL=$MF SUPER_RAG_AMD_RERANK_MAX_WAIT_MS=$MW timeout -k 10 400 python -u tools/bench_dropin.py \
                --rows 10000000 --concurrency 64 --seconds 10 > gpurun_out/$TAG/d1_fill${MF}_${MW}.json 2> gpurun_out/$TAG/d1_fill${MF}_${MW}.err || exit 1
            done ;;
+    spliterr) timeout -k 10 600 python -u tools/embed_split_error.py > gpurun_out/$TAG/embed_split_error.log 2>&1 || exit 1 ;;
     embedprof) timeout -k 10 200 python -u tools/embed_profile.py > gpurun_out/$TAG/embed_profile.json 2> gpurun_out/$TAG/embed_profile.err || exit 1 ;;
     xstag) for S in ${XSTAG:-0 -4 -8 -11 -16 0}; do
              echo "== stagger $S" >> gpurun_out/$TAG/xstag.log
