@@ -1061,14 +1061,26 @@ def source_fingerprint(root=ROOT):
 
 
 def pmc_file(root=ROOT):
-    """(relative path, parsed summary) of the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, tools/pmc_traffic.py), or (None, None)."""
+    """(relative path, parsed summary) of the committed PMC summary (profiles/*_pmc_traffic.json,
+    tools/pmc_traffic.py) taken on the current native sources (its source fingerprint), else the
+    last one by name, or (None, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(root, "profiles", "*_pmc_traffic.json")))
     if not files:
         return None, None
-    with open(files[-1]) as f:
-        return os.path.relpath(files[-1], root), json.load(f)
+    fp = source_fingerprint(root)
+    parsed = []
+    for path in files:
+        try:
+            with open(path) as f:
+                parsed.append((path, json.load(f)))
+        except (OSError, ValueError):
+            continue
+    if not parsed:
+        return None, None
+    match = [(p, d) for p, d in parsed if d.get("source_sha256") == fp]
+    path, d = (match or parsed)[-1]
+    return os.path.relpath(path, root), d
 
 
 # ProfScope names (the bench's kernel table) that differ from the logical names tools/pmc_traffic.py
